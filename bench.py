@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""Benchmark of the gfx950 go-lsm block codec (BASELINE.json metric).
+
+Default workload (N=1): BASELINE config 2 -- batch-decode 100,000 synthetic
+4 KiB KV blocks (33 records of 16 B keys / 100 B values, 4,092 parsed bytes
+per 4,096-byte slot), device resident, descriptor output.  One step = one
+lsm_decode_blocks launch over the whole batch.
+
+N>1 (torchrun, one process per GPU): the global batch is N x 100,000 blocks
+dealt round-robin (block i -> rank i mod N); no data-path collective, the
+ranks only meet at the barriers around the timed region (weak scaling).
+
+value = sum of parsed block bytes over all ranks / max-over-ranks wall time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "go-lsm_amd"))
+
+import lsmgpu  # noqa: E402
+from lsmgpu import synth  # noqa: E402
+
+METRIC = "GiB/s of device-resident .sst data-block bytes decoded to KV records"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="decode4k",
+                    choices=["decode4k", "decode64k", "mixed", "sst"])
+    ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
+    ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(world, x):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(world, x):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def traffic_from_profile(workload_key):
+    """HBM bytes per launch from the committed PMC summary (rocprofv3 --pmc,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE), if any."""
+    d = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(d):
+        return None, None
+    best = None
+    for name in sorted(os.listdir(d)):
+        if name.endswith(".json") and "pmc" in name:
+            try:
+                j = json.load(open(os.path.join(d, name)))
+            except Exception:
+                continue
+            if j.get("workload_key") == workload_key and "hbm_bytes_per_launch" in j:
+                best = (float(j["hbm_bytes_per_launch"]), "profiles/" + name)
+    return best if best else (None, None)
+
+
+def make_workload(args, world, rank):
+    if args.config in ("decode4k", "decode64k"):
+        per = args.blocks or (100_000 if args.config == "decode4k" else 6_400)
+        ids = rank + world * np.arange(per, dtype=np.int64)  # round-robin deal
+        if args.config == "decode4k":
+            buf, off, ln = synth.uniform_kv_blocks(ids)
+            desc = "decode %d x 4 KiB KV blocks per GPU (33 x 16 B key / 100 B value)" % per
+        else:
+            # 64 KiB slots: 528 records x 124 B = 65,472 parsed bytes
+            buf, off, ln = synth.uniform_kv_blocks(ids, recs=528, slot=65536)
+            desc = "decode %d x 64 KiB KV blocks per GPU (528 x 16 B key / 100 B value)" % per
+        return buf, off, ln, desc
+    if args.config == "mixed":
+        total = (args.blocks or 1 << 30)
+        buf, off, ln, _ = synth.mixed_kv_blocks(total, seed=synth.SEED + rank)
+        return buf, off, ln, "decode mixed 4/16/64 KiB KV blocks, values log-uniform 8 B-4 KiB"
+    raise ValueError(args.config)
+
+
+def bench_decode(args, world, rank, local):
+    ctx = lsmgpu.Context(local)
+    dev = ctx.torch_device
+    buf, blk_off, blk_len, wdesc = make_workload(args, world, rank)
+    nblk = blk_off.size
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.tensor(blk_off.view(np.int64), device=dev)
+    d_len = torch.tensor(blk_len.view(np.int32), device=dev)
+    r = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()),
+                                   arena=args.arena)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate on the warmed-up output: every block decoded cleanly
+    assert int((r.status[:nblk] != 0).sum()) == 0, "decode reported errors"
+    nrec_total = int(r.nrec[:nblk].sum().item())
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    elapsed = max_over_ranks(world, t1 - t0)
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    parsed = float(blk_len.astype(np.float64).sum())
+    parsed_all = sum_over_ranks(world, parsed)
+    value = parsed_all * args.steps / elapsed / GIB
+
+    # algorithmic bytes of one launch: block bytes +
+    # per-block metadata (blk_off 8 + blk_len 4) read; 16 B per record
+    # descriptor + nrec/status (8 B per block) written; arenas add the key and
+    # value bytes written.
+    alg = parsed + 12.0 * nblk + 16.0 * nrec_total + 8.0 * nblk
+    if args.arena:
+        alg += float(nrec_total) * (16 + 100) if args.config != "mixed" else parsed
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    wkey = f"{args.config}:{nblk}:{'arena' if args.arena else 'desc'}"
+    traffic, tsrc = traffic_from_profile(wkey)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seed 0x5EED, keys k%015d, splitmix64 values)",
+        "config": {
+            "workload": wdesc,
+            "grammar": "KV (kv/kv.go:46-115)",
+            "output": "ARENA (descriptors + packed keys/values)" if args.arena else
+                      "DESC (16 B record descriptors)",
+            "blocks_per_gpu": int(nblk),
+            "records_per_gpu": nrec_total,
+            "parsed_bytes_per_gpu": int(parsed),
+            "parallelism": f"dp{world} (blocks round-robin, no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "decode_blocks_kernel<KV>",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "alg_bytes_per_launch": int(alg),
+            "kernel_ms": round(kern_ms, 5),
+        },
+    }
+    return out, (buf, blk_off, blk_len)
+
+
+def cpu_baseline(args, data):
+    """The oracle's Go-pattern decode (fresh heap buffer per key and value,
+    append-grown slices; oracle/lsm_oracle.c) timed on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as ora
+
+    buf, blk_off, blk_len = data
+    threads = min(16, os.cpu_count() or 1)
+    parsed = float(blk_len.astype(np.float64).sum())
+
+    def timed(th, nb, budget):
+        reps, t, recs = 0, 0.0, 0
+        while t < budget or reps == 0:
+            t0 = time.perf_counter()
+            recs = ora.bench_decode_golike(ora.GRAMMAR_KV, buf, blk_off[:nb], blk_len[:nb], th)
+            t += time.perf_counter() - t0
+            reps += 1
+        return reps, t, recs
+
+    reps, t, recs = timed(threads, blk_off.size, args.cpu_seconds)
+    v = parsed * reps / t / GIB
+    nb1 = max(1, blk_off.size // 10)
+    reps1, t1, _ = timed(1, nb1, args.cpu_seconds / 3)
+    p1 = float(blk_len[:nb1].astype(np.float64).sum())
+    return {
+        "value": round(v, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full workload ({blk_off.size} blocks, {recs} records) x {reps} passes "
+                  f"in {t:.1f} s on {threads} threads; 1-thread: {nb1} blocks x {reps1} passes",
+        "value_1t": round(p1 * reps1 / t1 / GIB, 3),
+    }
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    if args.config == "sst":
+        from bench_sst import bench_sst  # encode path (config 3)
+        out, data = bench_sst(args, world, rank, local)
+    else:
+        out, data = bench_decode(args, world, rank, local)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "sst":
+        out["cpu_baseline"] = cpu_baseline(args, data)
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "sst":
+        from bench_sst import cpu_baseline_sst
+        out["cpu_baseline"] = cpu_baseline_sst(args, data)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

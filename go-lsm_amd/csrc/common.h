@@ -1,0 +1,107 @@
+// common.h — shared device helpers for the gfx950 block codec kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lsm_gpu.h"
+
+#define LSM_HIP_CHECK(expr)                                 \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return -(1000 + (int)_e);     \
+    } while (0)
+
+namespace lsm {
+
+constexpr int kWave = 64;
+constexpr uint32_t kKeyCap = 1u << 20;  // kv.go:84
+constexpr uint32_t kValCap = 1u << 30;  // kv.go:102
+// Buffer-resource dword3 for gfx950 raw (stride 0) byte-addressed buffers.
+constexpr int kRsrcFlags = 0x00020000;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
+
+// Wave-uniform value: lets hipcc keep it in an SGPR (T20 in the HIP guide).
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (uint64_t)hi << 32 | lo;
+}
+
+// Raw buffer over [base, base+bytes): loads past `bytes` return 0 and touch no memory.
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes,
+                                             kRsrcFlags);
+}
+
+__device__ __forceinline__ u32x4 ld_b128(rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t ld_b32(rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+
+// Bytes [s, s+4) of a little-endian byte stream given the two aligned dwords
+// that cover them.
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s & 3);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Exclusive wave prefix sum (64 lanes) of a 32-bit value.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+    uint32_t lane = lane_id();
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, kWave);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    *total = __shfl(x, kWave - 1, kWave);
+    return x - v;
+}
+
+__device__ __forceinline__ uint64_t wave_excl_scan64(uint64_t v, uint64_t *total) {
+    uint32_t lane = lane_id();
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint64_t y = __shfl_up(x, d, kWave);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    *total = __shfl(x, kWave - 1, kWave);
+    return x - v;
+}
+
+// Copy `len` bytes from buffer offset `src` (rsrc-relative, any alignment)
+// to global `dst` (any alignment) with the whole wave: interior dwords by
+// dword stores, the <=3 edge bytes at each end by byte stores.
+__device__ __forceinline__ void wave_copy(rsrc_t r, uint32_t src, uint8_t *dst, uint32_t len) {
+    if (len == 0) return;
+    uintptr_t d0 = reinterpret_cast<uintptr_t>(dst);
+    uint32_t head = (uint32_t)(d0 & 3);
+    uint32_t *dA = reinterpret_cast<uint32_t *>(d0 - head);
+    uint32_t ndw = (head + len + 3) >> 2;
+    for (uint32_t j = lane_id(); j < ndw; j += kWave) {
+        uint32_t S = src - head + 4 * j;  // may wrap below 0: OOB loads return 0
+        uint32_t Sa = S & ~3u;
+        uint32_t v = funnel(ld_b32(r, Sa), ld_b32(r, Sa + 4), S);
+        uint32_t lo_b = (j == 0) ? head : 0;
+        uint32_t end = head + len - 4 * j;
+        uint32_t hi_b = end < 4 ? end : 4;
+        if (lo_b == 0 && hi_b == 4) {
+            dA[j] = v;
+        } else {
+            uint8_t *db = reinterpret_cast<uint8_t *>(dA + j);
+            for (uint32_t t = lo_b; t < hi_b; t++) db[t] = (uint8_t)(v >> (8 * t));
+        }
+    }
+}
+
+}  // namespace lsm

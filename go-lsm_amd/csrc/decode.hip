@@ -1,0 +1,431 @@
+// decode.hip — batched record decode of length-prefixed blocks on gfx950.
+//
+// One wavefront owns one block (go-lsm's blocks are independent units; the
+// parallelism is across blocks).  The block is streamed into a
+// 4 KiB per-wave LDS ring in 1 KiB chunks (one coalesced 16 B/lane buffer
+// load each, range-checked so a block never reads past its padded end).  The
+// record boundaries are a dependent chain (each record's position depends on
+// every earlier length, data.go:58-76), so the wave chases them with a
+// wave-uniform cursor: each step reads a 64-position window (lane j holds the
+// u32 at cursor+j, two ds_read_b32 + v_alignbyte) and resolves every length
+// field inside the window with v_readlane, i.e. one LDS round trip per
+// window instead of one per field.  Thirty-two waves per CU chase
+// concurrently, which hides the LDS latency of the chain behind the HBM
+// stream.  Decoded records are staged one per lane and written as coalesced
+// 16-byte descriptors every 64 records.
+#include "common.h"
+
+namespace lsm {
+namespace {
+
+constexpr int kWavesPerWG = 4;
+constexpr uint32_t kRingBytes = 4096;
+constexpr uint32_t kRingWords = kRingBytes / 4;
+constexpr uint32_t kChunk = 1024;  // one b128 wave-load
+constexpr uint32_t kNChunk = kRingBytes / kChunk;
+constexpr uint32_t kWindow = 64;   // positions per window read
+
+struct DecodeArgs {
+    const uint8_t *in;
+    const uint64_t *blk_off;
+    const uint32_t *blk_len;
+    uint32_t nblk;
+    u32x4 *desc;
+    const uint64_t *rec_base;
+    uint32_t *nrec;
+    int32_t *status;
+    int64_t *idx_value;
+    uint8_t *key_arena;
+    uint8_t *val_arena;
+    const uint64_t *arena_base;
+    uint64_t *key_arena_off;
+    uint64_t *val_arena_off;
+};
+
+// Streams one block through this wave's LDS ring and serves u32 length
+// fields at wave-uniform block positions.
+struct BlockReader {
+    uint32_t *ring;
+    rsrc_t rsrc;
+    uint32_t h;        // block start inside its first 16-byte line
+    uint32_t total;    // loadable stream bytes: round_up16(h + n)
+    uint32_t nchunks;  // chunks covering [0, total)
+    uint32_t hi_c;     // chunks [.., hi_c) have been issued into the ring
+    uint32_t wbase;    // window base (block position)
+    uint32_t win;      // lane j: u32 at block position wbase + j
+    bool have_win;
+
+    __device__ void init(uint32_t *ring_, const uint8_t *in, uint64_t off, uint32_t n) {
+        ring = ring_;
+        uint64_t a0 = off & ~(uint64_t)15;
+        h = (uint32_t)(off - a0);
+        uint64_t tot = ((uint64_t)h + n + 15) & ~(uint64_t)15;
+        total = (uint32_t)(tot > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : tot);
+        nchunks = (total + kChunk - 1) / kChunk;
+        rsrc = make_rsrc(in + a0, total);
+        hi_c = 0;
+        have_win = false;
+        wbase = 0;
+        win = 0;
+    }
+
+    // Make stream bytes [h+p, h+p+68) resident (clamped to the block).
+    __device__ __forceinline__ void ensure(uint32_t p) {
+        uint32_t s0 = h + p;
+        uint32_t need_end = s0 + kWindow + 4;
+        if (need_end > total) need_end = total;
+        uint32_t need_hi = (need_end + kChunk - 1) / kChunk;
+        if (need_hi <= hi_c) return;
+        uint32_t c0 = s0 / kChunk;
+        uint32_t first = hi_c > c0 ? hi_c : c0;
+        uint32_t last = c0 + kNChunk;
+        if (last > nchunks) last = nchunks;
+        uint32_t lane = lane_id();
+        u32x4 v[kNChunk];
+#pragma unroll
+        for (uint32_t i = 0; i < kNChunk; i++) {
+            if (first + i < last) v[i] = ld_b128(rsrc, (first + i) * kChunk + lane * 16);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kNChunk; i++) {
+            uint32_t c = first + i;
+            if (c < last) {
+                uint32_t w = ((c % kNChunk) * kChunk + lane * 16) / 4;
+                *reinterpret_cast<u32x4 *>(&ring[w]) = v[i];
+            }
+        }
+        hi_c = last;
+        // LDS ops of one wave execute in order; this only stops hipcc from
+        // moving the window reads above the ring writes.
+        __builtin_amdgcn_wave_barrier();
+        __asm__ __volatile__("" ::: "memory");
+    }
+
+    __device__ __forceinline__ void load_window(uint32_t p) {
+        uint32_t s = h + p + lane_id();
+        uint32_t w = s >> 2;
+        uint32_t x0 = ring[w % kRingWords];
+        uint32_t x1 = ring[(w + 1) % kRingWords];
+        win = funnel(x0, x1, s);
+        wbase = p;
+        have_win = true;
+    }
+
+    // Little-endian u32 at block position p (wave-uniform).
+    __device__ __forceinline__ uint32_t field(uint32_t p) {
+        if (!have_win || p - wbase >= kWindow) {
+            ensure(p);
+            load_window(p);
+        }
+        return __builtin_amdgcn_readlane(win, p - wbase);
+    }
+};
+
+// Records staged one per lane until 64 are ready, then stored coalesced.
+struct RecordStage {
+    uint32_t off_lo, off_hi, klen, vlen, x_lo, x_hi;
+
+    __device__ __forceinline__ void put(uint32_t slot, uint64_t off, uint32_t k, uint32_t v,
+                                        uint64_t x) {
+        if (lane_id() == slot) {
+            off_lo = (uint32_t)off;
+            off_hi = (uint32_t)(off >> 32);
+            klen = k;
+            vlen = v;
+            x_lo = (uint32_t)x;
+            x_hi = (uint32_t)(x >> 32);
+        }
+    }
+};
+
+template <int G>
+__device__ __forceinline__ void flush(const DecodeArgs &a, const RecordStage &st, uint64_t base,
+                                      uint32_t first, uint32_t cnt) {
+    uint32_t lane = lane_id();
+    if (lane < cnt) {
+        uint64_t i = base + first + lane;
+        u32x4 d;
+        d.x = st.off_lo;
+        d.y = st.off_hi;
+        d.z = st.klen;
+        d.w = st.vlen;
+        a.desc[i] = d;
+        if (G == LSM_GRAMMAR_IDX && a.idx_value)
+            a.idx_value[i] = (int64_t)((uint64_t)st.x_hi << 32 | st.x_lo);
+    }
+}
+
+template <int G, bool ARENA>
+__global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
+    const uint32_t wave = uni(threadIdx.x / kWave);
+    const uint32_t b = uni(blockIdx.x * kWavesPerWG + wave);
+    if (b >= a.nblk) return;
+
+    const uint64_t off = uni64(a.blk_off[b]);
+    const uint32_t n = uni(a.blk_len[b]);
+    // Record slots: CSR rec_base, or offset-addressed (rec_base == NULL):
+    // block b owns slots [off/R, (off+n)/R) with R the grammar's minimum
+    // record size, disjoint for non-overlapping blocks -- no scan needed.
+    constexpr uint32_t R = G == LSM_GRAMMAR_V ? 4 : G == LSM_GRAMMAR_KV ? 8 : 12;
+    uint64_t base, cap;
+    if (a.rec_base) {
+        base = uni64(a.rec_base[b]);
+        cap = uni64(a.rec_base[b + 1]) - base;
+    } else {
+        base = off / R;
+        cap = (off + n) / R - base;
+    }
+
+    BlockReader rd;
+    rd.init(ring[wave], a.in, off, n);
+    RecordStage st{};
+
+    uint64_t kcur = 0, vcur = 0;
+    if (ARENA) {
+        kcur = a.arena_base ? uni64(a.arena_base[b]) : off;  // offset-addressed arenas
+        vcur = kcur;
+    }
+
+    uint32_t pos = 0, nr = 0;
+    int32_t status = LSM_OK;
+    for (;;) {
+        uint32_t rem = n - pos;
+        uint32_t klen = 0, vlen = 0;
+        uint64_t xval = 0;
+        uint32_t vp = pos;
+        if (G == LSM_GRAMMAR_V) {
+            // data.go:58-76
+            if (rem == 0) break;
+            if (rem < 4) { status = LSM_ST_TRUNC_LEN_PREFIX; break; }
+            vlen = rd.field(pos);
+            if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
+        } else if (G == LSM_GRAMMAR_KV) {
+            // wal.go:107 loop of kv.go:77-115
+            if (rem == 0) break;
+            if (rem < 4) { status = LSM_ST_TRUNC_LEN_PREFIX; break; }
+            klen = rd.field(pos);
+            if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; break; }
+            if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; break; }
+            vp = pos + 4 + klen;
+            uint32_t rem2 = n - vp;
+            if (rem2 < 4) { status = LSM_ST_TRUNC_VLEN; break; }
+            vlen = rd.field(vp);
+            if (vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; break; }
+            if (rem2 - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
+        } else {
+            // index.go:70-98
+            if (rem == 0) break;
+            if (rem < 4) { status = LSM_ST_IDX_OVERRUN; break; }
+            klen = rd.field(pos);
+            if ((uint64_t)rem < 12ull + klen) { status = LSM_ST_IDX_OVERRUN; break; }
+            vp = pos + 4 + klen;
+            uint32_t lo = rd.field(vp);
+            uint32_t hi = rd.field(vp + 4);
+            xval = (uint64_t)hi << 32 | lo;
+            vlen = 8;
+        }
+        if (nr >= cap) { status = LSM_ST_CAPACITY; break; }
+
+        const uint32_t slot = nr % kWave;
+        st.put(slot, off + pos, klen, vlen, xval);
+        if (ARENA) {
+            if (G != LSM_GRAMMAR_V && a.key_arena) {
+                wave_copy(rd.rsrc, rd.h + pos + 4, a.key_arena + kcur, klen);
+                if (a.key_arena_off && lane_id() == 0) a.key_arena_off[base + nr] = kcur;
+                kcur += klen;
+            }
+            if (G != LSM_GRAMMAR_IDX && a.val_arena) {
+                wave_copy(rd.rsrc, rd.h + vp + 4, a.val_arena + vcur, vlen);
+                if (a.val_arena_off && lane_id() == 0) a.val_arena_off[base + nr] = vcur;
+                vcur += vlen;
+            }
+        }
+        nr++;
+        if (slot == kWave - 1) flush<G>(a, st, base, nr - kWave, kWave);
+        pos = (G == LSM_GRAMMAR_IDX) ? vp + 8 : vp + 4 + vlen;
+    }
+    if (nr % kWave) flush<G>(a, st, base, nr - nr % kWave, nr % kWave);
+    if (lane_id() == 0) {
+        a.nrec[b] = nr;
+        a.status[b] = status;
+    }
+}
+
+// ---- planning: exclusive scans over per-block quantities -----------------
+
+constexpr uint32_t kScanThreads = 256;
+constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanTile = kScanThreads * kScanPer;
+
+__device__ __forceinline__ uint64_t plan_value(int mode, uint32_t len) {
+    switch (mode) {
+    case 0: return len / 4;   // V
+    case 1: return len / 8;   // KV
+    case 2: return len / 12;  // IDX
+    default: return len;      // arena bytes
+    }
+}
+
+__device__ uint64_t block_excl_scan(uint64_t v, uint64_t *total) {
+    __shared__ uint64_t wsum[kScanThreads / kWave];
+    uint64_t wt;
+    uint64_t x = wave_excl_scan64(v, &wt);
+    uint32_t w = threadIdx.x / kWave;
+    if (lane_id() == 0) wsum[w] = wt;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (uint32_t i = 0; i < kScanThreads / kWave; i++) {
+        if (i < w) pre += wsum[i];
+        tot += wsum[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return x + pre;
+}
+
+__global__ __launch_bounds__(kScanThreads) void plan_tile_sums(int mode, const uint32_t *len,
+                                                               uint32_t n, uint64_t *partial) {
+    uint64_t s = 0;
+    uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t j = 0; j < kScanPer; j++)
+        if (i0 + j < n) s += plan_value(mode, len[i0 + j]);
+    uint64_t tot;
+    block_excl_scan(s, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanThreads) void plan_scan_partials(uint64_t *partial,
+                                                                   uint32_t ntiles, uint64_t *out,
+                                                                   uint32_t n) {
+    uint64_t carry = 0;
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += kScanThreads) {
+        uint32_t t = t0 + threadIdx.x;
+        uint64_t v = t < ntiles ? partial[t] : 0;
+        uint64_t tot;
+        uint64_t x = block_excl_scan(v, &tot);
+        if (t < ntiles) partial[t] = carry + x;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+}
+
+__global__ __launch_bounds__(kScanThreads) void plan_tile_apply(int mode, const uint32_t *len,
+                                                                uint32_t n,
+                                                                const uint64_t *partial,
+                                                                uint64_t *out) {
+    uint64_t vals[kScanPer];
+    uint64_t s = 0;
+    uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t j = 0; j < kScanPer; j++) {
+        vals[j] = (i0 + j < n) ? plan_value(mode, len[i0 + j]) : 0;
+        s += vals[j];
+    }
+    uint64_t tot;
+    uint64_t pre = block_excl_scan(s, &tot) + partial[blockIdx.x];
+    for (uint32_t j = 0; j < kScanPer; j++) {
+        if (i0 + j < n) out[i0 + j] = pre;
+        pre += vals[j];
+    }
+}
+
+int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void *ws,
+              size_t ws_bytes, hipStream_t s) {
+    uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
+    if (ntiles == 0) ntiles = 1;
+    if (ws_bytes < (size_t)ntiles * 8 || (!ws && n)) return LSM_ESPACE;
+    uint64_t *partial = static_cast<uint64_t *>(ws);
+    if (n == 0) {
+        LSM_HIP_CHECK(hipMemsetAsync(d_out, 0, 8, s));
+        return 0;
+    }
+    hipLaunchKernelGGL(plan_tile_sums, dim3(ntiles), dim3(kScanThreads), 0, s, mode, d_len, n,
+                       partial);
+    hipLaunchKernelGGL(plan_scan_partials, dim3(1), dim3(kScanThreads), 0, s, partial, ntiles,
+                       d_out, n);
+    hipLaunchKernelGGL(plan_tile_apply, dim3(ntiles), dim3(kScanThreads), 0, s, mode, d_len, n,
+                       partial, d_out);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+template <int G, bool ARENA>
+int launch_decode(const DecodeArgs &a, hipStream_t s) {
+    uint32_t grid = (a.nblk + kWavesPerWG - 1) / kWavesPerWG;
+    hipLaunchKernelGGL((decode_blocks_kernel<G, ARENA>), dim3(grid), dim3(kWave * kWavesPerWG),
+                       0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace
+}  // namespace lsm
+
+using namespace lsm;
+
+extern "C" uint64_t lsm_max_records(int grammar, uint64_t len) {
+    switch (grammar) {
+    case LSM_GRAMMAR_V: return len / 4;
+    case LSM_GRAMMAR_KV: return len / 8;
+    case LSM_GRAMMAR_IDX: return len / 12;
+    default: return 0;
+    }
+}
+
+extern "C" size_t lsm_plan_workspace_bytes(uint32_t nblk) {
+    size_t ntiles = (nblk + kScanTile - 1) / kScanTile;
+    return (ntiles ? ntiles : 1) * 8;
+}
+
+extern "C" int lsm_plan_rec_base(lsm_ctx *ctx, int grammar, const uint32_t *d_blk_len,
+                                 uint32_t nblk, uint64_t *d_rec_base, void *d_workspace,
+                                 size_t ws_bytes, void *stream) {
+    if (!ctx || !d_rec_base || (nblk && !d_blk_len)) return LSM_EINVAL;
+    if (grammar < LSM_GRAMMAR_V || grammar > LSM_GRAMMAR_IDX) return LSM_EINVAL;
+    int mode = grammar == LSM_GRAMMAR_V ? 0 : grammar == LSM_GRAMMAR_KV ? 1 : 2;
+    return plan_scan(mode, d_blk_len, nblk, d_rec_base, d_workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+extern "C" int lsm_plan_arena_base(lsm_ctx *ctx, const uint32_t *d_blk_len, uint32_t nblk,
+                                   uint64_t *d_arena_base, void *d_workspace, size_t ws_bytes,
+                                   void *stream) {
+    if (!ctx || !d_arena_base || (nblk && !d_blk_len)) return LSM_EINVAL;
+    return plan_scan(3, d_blk_len, nblk, d_arena_base, d_workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
+                                 const uint64_t *d_blk_off, const uint32_t *d_blk_len,
+                                 uint32_t nblk, const lsm_decode_out *out, void *stream) {
+    if (!ctx || !out) return LSM_EINVAL;
+    if (nblk == 0) return 0;
+    if (!d_in || !d_blk_off || !d_blk_len || !out->desc || !out->nrec || !out->status)
+        return LSM_EINVAL;
+    if (grammar < LSM_GRAMMAR_V || grammar > LSM_GRAMMAR_IDX) return LSM_EINVAL;
+    bool arena = out->key_arena || out->val_arena;
+    DecodeArgs a;
+    a.in = d_in;
+    a.blk_off = d_blk_off;
+    a.blk_len = d_blk_len;
+    a.nblk = nblk;
+    a.desc = reinterpret_cast<u32x4 *>(out->desc);
+    a.rec_base = out->rec_base;
+    a.nrec = out->nrec;
+    a.status = out->status;
+    a.idx_value = out->idx_value;
+    a.key_arena = out->key_arena;
+    a.val_arena = out->val_arena;
+    a.arena_base = out->arena_base;
+    a.key_arena_off = out->key_arena_off;
+    a.val_arena_off = out->val_arena_off;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (grammar) {
+    case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true>(a, s)
+                                     : launch_decode<LSM_GRAMMAR_V, false>(a, s);
+    case LSM_GRAMMAR_KV: return arena ? launch_decode<LSM_GRAMMAR_KV, true>(a, s)
+                                      : launch_decode<LSM_GRAMMAR_KV, false>(a, s);
+    default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true>(a, s)
+                          : launch_decode<LSM_GRAMMAR_IDX, false>(a, s);
+    }
+}

@@ -1,0 +1,110 @@
+// murmur.h — device MurmurHash3 sum256 and bloom locations (gfx950).
+//
+// Device restatement of go-lsm's digest128.sum256 (sstable/bloom/murmur.go:245-275):
+// MMH3_x64_128(seed 0) of `key` and of `key || 0x01`, computed in one pass
+// over the key (the 16-byte blocks are shared by both digests; only the tail
+// differs).  Locations follow bloom.go:133-141; `% m` uses a Barrett
+// reduction with a host-precomputed reciprocal (one correction step).
+#pragma once
+
+#include "common.h"
+
+namespace lsm {
+
+constexpr uint64_t kMC1 = 0x87c37b91114253d5ull;
+constexpr uint64_t kMC2 = 0x4cf5ad432745937full;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+__device__ __forceinline__ void mmh3_block(uint64_t &h1, uint64_t &h2, uint64_t k1, uint64_t k2) {
+    k1 *= kMC1; k1 = rotl64(k1, 31); k1 *= kMC2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= kMC2; k2 = rotl64(k2, 33); k2 *= kMC1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+}
+
+// Tail words (k1 = bytes 0..7, k2 = bytes 8..15 of a tail of tl < 16 bytes),
+// then finalization with the total length.
+__device__ __forceinline__ void mmh3_final(uint64_t h1, uint64_t h2, uint64_t k1, uint64_t k2,
+                                           uint32_t tl, uint64_t len, uint64_t &o1,
+                                           uint64_t &o2) {
+    if (tl > 8) { k2 *= kMC2; k2 = rotl64(k2, 33); k2 *= kMC1; h2 ^= k2; }
+    if (tl > 0) { k1 *= kMC1; k1 = rotl64(k1, 31); k1 *= kMC2; h1 ^= k1; }
+    h1 ^= len; h2 ^= len;
+    h1 += h2; h2 += h1;
+    h1 = fmix64(h1); h2 = fmix64(h2);
+    h1 += h2; h2 += h1;
+    o1 = h1; o2 = h2;
+}
+
+// Unaligned little-endian u32 from global memory (two aligned dword loads).
+// Requires the 4 bytes past p+3 to be readable (16-byte padded arenas).
+__device__ __forceinline__ uint32_t ldg_u32_unaligned(const uint8_t *p) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    return funnel(w[0], w[1], (uint32_t)a);
+}
+
+__device__ __forceinline__ uint64_t ldg_u64_unaligned(const uint8_t *p) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    uint32_t s = (uint32_t)a;
+    uint32_t x0 = w[0], x1 = w[1], x2 = w[2];
+    return (uint64_t)funnel(x1, x2, s) << 32 | funnel(x0, x1, s);
+}
+
+// sum256 (murmur.go:245-275) of key[0..len).
+__device__ __forceinline__ void sum256(const uint8_t *key, uint64_t len, uint64_t h[4]) {
+    uint64_t h1 = 0, h2 = 0;
+    uint64_t nb = len / 16;
+    for (uint64_t i = 0; i < nb; i++)
+        mmh3_block(h1, h2, ldg_u64_unaligned(key + 16 * i), ldg_u64_unaligned(key + 16 * i + 8));
+    uint32_t tl = (uint32_t)(len & 15);
+    const uint8_t *tail = key + 16 * nb;
+    uint64_t k1 = 0, k2 = 0;
+    if (tl) {
+        // Gather the tail bytes; bytes beyond tl are masked off.
+        uint64_t w0 = ldg_u64_unaligned(tail);
+        uint64_t w1 = tl > 8 ? ldg_u64_unaligned(tail + 8) : 0;
+        k1 = tl >= 8 ? w0 : (w0 & ((1ull << (8 * tl)) - 1));
+        k2 = tl > 8 ? (tl == 16 ? w1 : (w1 & ((1ull << (8 * (tl - 8))) - 1))) : 0;
+    }
+    mmh3_final(h1, h2, k1, k2, tl, len, h[0], h[1]);
+    // Second digest: virtually append 0x01 at tail position tl.
+    if (tl == 15) {
+        uint64_t kk2 = k2 | (1ull << 56);
+        mmh3_block(h1, h2, k1, kk2);
+        mmh3_final(h1, h2, 0, 0, 0, len + 1, h[2], h[3]);
+    } else {
+        uint64_t kk1 = k1, kk2 = k2;
+        if (tl < 8) kk1 |= 1ull << (8 * tl);
+        else kk2 |= 1ull << (8 * (tl - 8));
+        mmh3_final(h1, h2, kk1, kk2, tl + 1, len + 1, h[2], h[3]);
+    }
+}
+
+// location(h, i) before the modulo (bloom.go:133-136).
+__device__ __forceinline__ uint64_t location(const uint64_t h[4], uint32_t i) {
+    uint32_t m4 = i & 3;
+    uint64_t a = (m4 & 1) ? h[1] : h[0];
+    uint64_t b = (m4 == 0 || m4 == 3) ? h[2] : h[3];
+    return a + (uint64_t)i * b;
+}
+
+// x mod m with Barrett reciprocal r = floor((2^64-1)/m) (m < 2^63).
+__device__ __forceinline__ uint64_t mod_barrett(uint64_t x, uint64_t m, uint64_t r) {
+    uint64_t q = __umul64hi(x, r);
+    uint64_t rem = x - q * m;
+    return rem >= m ? rem - m : rem;
+}
+
+}  // namespace lsm

@@ -1,0 +1,95 @@
+"""ctypes declarations of the C ABI in include/lsm_gpu.h.
+
+The product path is liblsm_gpu.so, built in-tree by go-lsm_amd/Makefile.  There
+is no fallback: if the library is missing, importing this module raises.
+"""
+import ctypes
+import os
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "liblsm_gpu.so")
+
+c_u8p = ctypes.c_void_p
+c_u32p = ctypes.c_void_p
+c_u64p = ctypes.c_void_p
+
+
+class DecodeOut(ctypes.Structure):
+    """struct lsm_decode_out (include/lsm_gpu.h)."""
+
+    _fields_ = [
+        ("desc", ctypes.c_void_p),
+        ("rec_base", ctypes.c_void_p),
+        ("nrec", ctypes.c_void_p),
+        ("status", ctypes.c_void_p),
+        ("idx_value", ctypes.c_void_p),
+        ("key_arena", ctypes.c_void_p),
+        ("val_arena", ctypes.c_void_p),
+        ("arena_base", ctypes.c_void_p),
+        ("key_arena_off", ctypes.c_void_p),
+        ("val_arena_off", ctypes.c_void_p),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "lsm_abi_version": (ctypes.c_int, []),
+    "lsm_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "lsm_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsm_ctx_num_cus": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsm_max_records": (ctypes.c_uint64, [ctypes.c_int, ctypes.c_uint64]),
+    "lsm_plan_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32]),
+    "lsm_plan_rec_base": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_u32p, ctypes.c_uint32,
+                                         c_u64p, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p]),
+    "lsm_plan_arena_base": (ctypes.c_int, [ctypes.c_void_p, c_u32p, ctypes.c_uint32, c_u64p,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_decode_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u64p, c_u32p,
+                                         ctypes.c_uint32, ctypes.POINTER(DecodeOut),
+                                         ctypes.c_void_p]),
+    "lsm_encoded_size_host": (ctypes.c_uint64, [ctypes.c_int, c_u64p, c_u64p, ctypes.c_uint64,
+                                                ctypes.c_uint64]),
+    "lsm_encode_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u64p, c_u8p,
+                                         c_u64p, ctypes.c_void_p, c_u64p, ctypes.c_uint32, c_u8p,
+                                         c_u64p, ctypes.c_void_p]),
+    "lsm_segment_files_host": (ctypes.c_uint64, [c_u64p, c_u64p, ctypes.c_uint64,
+                                                 ctypes.c_uint64, c_u64p]),
+    "lsm_sst_image_size_host": (ctypes.c_uint64, [c_u64p, c_u64p, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_uint64]),
+    "lsm_filter_block_size": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "lsm_build_sst_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint64]),
+    "lsm_build_sst": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u8p, c_u64p, c_u64p,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                     ctypes.c_uint32, c_u8p, c_u64p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_bloom_probe": (ctypes.c_int, [ctypes.c_void_p, c_u64p, ctypes.c_uint64, ctypes.c_uint32,
+                                       c_u8p, c_u64p, ctypes.c_uint64, c_u8p, ctypes.c_void_p]),
+    "lsm_sum256": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_uint64, c_u64p,
+                                  ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load liblsm_gpu.so (in-tree).  Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `make -C go-lsm_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+    return rc

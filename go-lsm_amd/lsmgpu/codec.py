@@ -1,0 +1,403 @@
+"""Python driver of the gfx950 block codec (tests and bench).
+
+Device memory and streams come from PyTorch (plumbing); every computation
+runs in liblsm_gpu.so through the C ABI (include/lsm_gpu.h).  Unsigned C
+types are carried in signed torch dtypes of the same width (uint64 -> int64,
+uint32 -> int32); the bits are what matter.
+"""
+from dataclasses import dataclass
+from typing import Optional
+
+import ctypes
+import numpy as np
+import torch
+
+from . import _lib
+
+GRAMMAR_V, GRAMMAR_KV, GRAMMAR_IDX = 0, 1, 2
+
+STATUS_NAMES = {
+    0: "ok",
+    1: "truncated length prefix",
+    2: "truncated key",
+    3: "key too long",
+    4: "truncated value length",
+    5: "value too long",
+    6: "truncated value",
+    7: "index overrun",
+    8: "capacity",
+}
+
+DESC_DTYPE = np.dtype([("rec_off", "<u8"), ("key_len", "<u4"), ("val_len", "<u4")])
+
+# go-lsm defaults: bloom.go:79-82, sstable.go:21
+DEFAULT_BLOOM_M = 1_600_000
+DEFAULT_BLOOM_K = 16
+MAX_SSTABLE_SIZE = 2 * 1024 * 1024
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def pad16(n: int) -> int:
+    """Device inputs must be readable to the next 16-byte multiple (+16 slack)."""
+    return ((n + 15) // 16) * 16 + 16
+
+
+def to_device_bytes(buf: np.ndarray, device) -> torch.Tensor:
+    """Copy a host byte array into a 16-byte padded device buffer."""
+    n = int(buf.nbytes)
+    t = torch.zeros(pad16(n), dtype=torch.uint8, device=device)
+    if n:
+        t[:n].copy_(torch.from_numpy(np.ascontiguousarray(buf).view(np.uint8).reshape(-1)))
+    return t
+
+
+class Context:
+    """One lsm_ctx per device (and per host thread in concurrent use)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        self.device = device
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.lsm_ctx_create(device, ctypes.byref(h)), "lsm_ctx_create")
+        self.handle = h
+        self.torch_device = torch.device("cuda", device)
+
+    def close(self):
+        if self.handle:
+            self.lib.lsm_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_cus(self) -> int:
+        return self.lib.lsm_ctx_num_cus(self.handle)
+
+
+@dataclass
+class DecodePlan:
+    """Device-side output placement of one batch (lsm_plan_*)."""
+
+    rec_base: torch.Tensor            # int64[nblk+1]
+    arena_base: Optional[torch.Tensor]
+    workspace: torch.Tensor
+    total_records: int                # capacity (rec_base[nblk])
+
+
+MIN_RECORD = {GRAMMAR_V: 4, GRAMMAR_KV: 8, GRAMMAR_IDX: 12}
+
+
+@dataclass
+class DecodeResult:
+    desc: torch.Tensor                # int32[cap, 4] = lsm_rec_desc
+    nrec: torch.Tensor                # int32[nblk]
+    status: torch.Tensor              # int32[nblk]
+    rec_base: Optional[torch.Tensor]  # int64[nblk+1], or None = offset-addressed
+    idx_value: Optional[torch.Tensor] = None
+    key_arena: Optional[torch.Tensor] = None
+    val_arena: Optional[torch.Tensor] = None
+    arena_base: Optional[torch.Tensor] = None
+    key_arena_off: Optional[torch.Tensor] = None
+    val_arena_off: Optional[torch.Tensor] = None
+
+    grammar: int = GRAMMAR_KV
+
+    def desc_numpy(self) -> np.ndarray:
+        return self.desc.cpu().numpy().view(np.uint8).view(DESC_DTYPE).reshape(-1)
+
+    def bases(self, blk_off: np.ndarray) -> np.ndarray:
+        """Slot of each block's first record (host copy)."""
+        if self.rec_base is not None:
+            return self.rec_base.cpu().numpy().view(np.uint64)[:-1]
+        return np.asarray(blk_off, dtype=np.uint64) // np.uint64(MIN_RECORD[self.grammar])
+
+    def arena_bases(self, blk_off: np.ndarray) -> np.ndarray:
+        if self.arena_base is not None:
+            return self.arena_base.cpu().numpy().view(np.uint64)[:-1]
+        return np.asarray(blk_off, dtype=np.uint64)
+
+
+def plan(ctx: Context, grammar: int, blk_len: torch.Tensor, arena: bool = False,
+         stream=None) -> DecodePlan:
+    nblk = int(blk_len.numel())
+    dev = ctx.torch_device
+    ws = torch.empty(max(int(ctx.lib.lsm_plan_workspace_bytes(nblk)), 16), dtype=torch.uint8,
+                     device=dev)
+    rec_base = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    sh = _stream_handle(stream)
+    _lib.check(ctx.lib.lsm_plan_rec_base(ctx.handle, grammar, _ptr(blk_len), nblk,
+                                         _ptr(rec_base), _ptr(ws), ws.numel(), sh),
+               "lsm_plan_rec_base")
+    arena_base = None
+    if arena:
+        arena_base = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+        _lib.check(ctx.lib.lsm_plan_arena_base(ctx.handle, _ptr(blk_len), nblk,
+                                               _ptr(arena_base), _ptr(ws), ws.numel(), sh),
+                   "lsm_plan_arena_base")
+    total = int(rec_base[nblk].item()) if nblk else 0
+    return DecodePlan(rec_base, arena_base, ws, total)
+
+
+def replan(ctx: Context, grammar: int, blk_len: torch.Tensor, p: DecodePlan, stream=None):
+    """Recompute rec_base in place (no host sync): the plan step of a timed loop."""
+    nblk = int(blk_len.numel())
+    _lib.check(ctx.lib.lsm_plan_rec_base(ctx.handle, grammar, _ptr(blk_len), nblk,
+                                         _ptr(p.rec_base), _ptr(p.workspace),
+                                         p.workspace.numel(), _stream_handle(stream)),
+               "lsm_plan_rec_base")
+
+
+def alloc_decode(ctx: Context, grammar: int, nblk: int, p: DecodePlan,
+                 arena: bool = False, arena_offsets: bool = False) -> DecodeResult:
+    dev = ctx.torch_device
+    cap = max(p.total_records, 1)
+    r = DecodeResult(
+        desc=torch.empty((cap, 4), dtype=torch.int32, device=dev),
+        nrec=torch.empty(max(nblk, 1), dtype=torch.int32, device=dev),
+        status=torch.empty(max(nblk, 1), dtype=torch.int32, device=dev),
+        rec_base=p.rec_base, grammar=grammar,
+    )
+    if grammar == GRAMMAR_IDX:
+        r.idx_value = torch.empty(cap, dtype=torch.int64, device=dev)
+    if arena:
+        nbytes = int(p.arena_base[nblk].item()) if nblk else 0
+        r.arena_base = p.arena_base
+        if grammar != GRAMMAR_V:
+            r.key_arena = torch.zeros(pad16(nbytes), dtype=torch.uint8, device=dev)
+        if grammar != GRAMMAR_IDX:
+            r.val_arena = torch.zeros(pad16(nbytes), dtype=torch.uint8, device=dev)
+        if arena_offsets:
+            if grammar != GRAMMAR_V:
+                r.key_arena_off = torch.empty(cap, dtype=torch.int64, device=dev)
+            if grammar != GRAMMAR_IDX:
+                r.val_arena_off = torch.empty(cap, dtype=torch.int64, device=dev)
+    return r
+
+
+def alloc_decode_offset(ctx: Context, grammar: int, nblk: int, in_bytes: int,
+                        arena: bool = False, arena_offsets: bool = False) -> DecodeResult:
+    """Outputs for offset-addressed placement (rec_base = arena_base = NULL):
+    block b's records at slots blk_off[b]/R.., its arena bytes at blk_off[b]."""
+    dev = ctx.torch_device
+    cap = in_bytes // MIN_RECORD[grammar] + 1
+    r = DecodeResult(
+        desc=torch.empty((cap, 4), dtype=torch.int32, device=dev),
+        nrec=torch.empty(max(nblk, 1), dtype=torch.int32, device=dev),
+        status=torch.empty(max(nblk, 1), dtype=torch.int32, device=dev),
+        rec_base=None, grammar=grammar)
+    if grammar == GRAMMAR_IDX:
+        r.idx_value = torch.empty(cap, dtype=torch.int64, device=dev)
+    if arena:
+        if grammar != GRAMMAR_V:
+            r.key_arena = torch.zeros(pad16(in_bytes), dtype=torch.uint8, device=dev)
+        if grammar != GRAMMAR_IDX:
+            r.val_arena = torch.zeros(pad16(in_bytes), dtype=torch.uint8, device=dev)
+        if arena_offsets:
+            if grammar != GRAMMAR_V:
+                r.key_arena_off = torch.empty(cap, dtype=torch.int64, device=dev)
+            if grammar != GRAMMAR_IDX:
+                r.val_arena_off = torch.empty(cap, dtype=torch.int64, device=dev)
+    return r
+
+
+def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,
+                blk_len: torch.Tensor, r: DecodeResult, stream=None) -> None:
+    """lsm_decode_blocks into preallocated outputs (asynchronous)."""
+    out = _lib.DecodeOut(
+        desc=r.desc.data_ptr(),
+        rec_base=r.rec_base.data_ptr() if r.rec_base is not None else None,
+        nrec=r.nrec.data_ptr(),
+        status=r.status.data_ptr(),
+        idx_value=r.idx_value.data_ptr() if r.idx_value is not None else None,
+        key_arena=r.key_arena.data_ptr() if r.key_arena is not None else None,
+        val_arena=r.val_arena.data_ptr() if r.val_arena is not None else None,
+        arena_base=r.arena_base.data_ptr() if r.arena_base is not None else None,
+        key_arena_off=r.key_arena_off.data_ptr() if r.key_arena_off is not None else None,
+        val_arena_off=r.val_arena_off.data_ptr() if r.val_arena_off is not None else None,
+    )
+    _lib.check(ctx.lib.lsm_decode_blocks(ctx.handle, grammar, _ptr(d_in), _ptr(blk_off),
+                                         _ptr(blk_len), int(blk_off.numel()), ctypes.byref(out),
+                                         _stream_handle(stream)), "lsm_decode_blocks")
+
+
+def decode_blocks(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,
+                  blk_len: torch.Tensor, arena: bool = False, arena_offsets: bool = False,
+                  placement: str = "plan", stream=None) -> DecodeResult:
+    """placement: "plan" (dense CSR capacity via lsm_plan_*) or "offset"
+    (offset-addressed, no plan; blocks must not overlap)."""
+    nblk = int(blk_off.numel())
+    if placement == "offset":
+        r = alloc_decode_offset(ctx, grammar, nblk, int(d_in.numel()), arena=arena,
+                                arena_offsets=arena_offsets)
+    else:
+        p = plan(ctx, grammar, blk_len, arena=arena, stream=stream)
+        r = alloc_decode(ctx, grammar, nblk, p, arena=arena, arena_offsets=arena_offsets)
+    if nblk:
+        decode_into(ctx, grammar, d_in, blk_off, blk_len, r, stream=stream)
+    return r
+
+
+# ---- encode -----------------------------------------------------------------
+
+@dataclass
+class RecordBatch:
+    """Columnar (CSR) record batch on the device."""
+
+    keys: torch.Tensor   # uint8, 16-byte padded
+    koff: torch.Tensor   # int64[n+1]
+    vals: torch.Tensor
+    voff: torch.Tensor
+    n: int
+    koff_host: np.ndarray
+    voff_host: np.ndarray
+
+
+def batch_to_device(ctx: Context, keys: np.ndarray, koff: np.ndarray, vals: np.ndarray,
+                    voff: np.ndarray) -> RecordBatch:
+    dev = ctx.torch_device
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    voff = np.ascontiguousarray(voff, dtype=np.uint64)
+    return RecordBatch(
+        keys=to_device_bytes(keys, dev),
+        koff=torch.from_numpy(koff.view(np.int64)).to(dev),
+        vals=to_device_bytes(vals, dev),
+        voff=torch.from_numpy(voff.view(np.int64)).to(dev),
+        n=len(koff) - 1, koff_host=koff, voff_host=voff)
+
+
+def encoded_size(grammar: int, koff: np.ndarray, voff: np.ndarray, r0: int, r1: int) -> int:
+    n = r1 - r0
+    if grammar == GRAMMAR_V:
+        return 4 * n + int(voff[r1] - voff[r0])
+    if grammar == GRAMMAR_KV:
+        return 8 * n + int(koff[r1] - koff[r0]) + int(voff[r1] - voff[r0])
+    return 12 * n + int(koff[r1] - koff[r0])
+
+
+def encode_blocks(ctx: Context, grammar: int, batch: RecordBatch, rec_start: np.ndarray,
+                  out_off: Optional[np.ndarray] = None, out_bytes: Optional[int] = None,
+                  idx_off: Optional[np.ndarray] = None, stream=None):
+    """Encode block b = records [rec_start[b], rec_start[b+1]) at out_off[b].
+    Returns (d_out, out_off)."""
+    dev = ctx.torch_device
+    rec_start = np.ascontiguousarray(rec_start, dtype=np.uint64)
+    nblk = len(rec_start) - 1
+    sizes = np.array([encoded_size(grammar, batch.koff_host, batch.voff_host,
+                                   int(rec_start[b]), int(rec_start[b + 1]))
+                      for b in range(nblk)], dtype=np.uint64)
+    if out_off is None:
+        out_off = np.zeros(nblk, dtype=np.uint64)
+        if nblk:
+            out_off[1:] = np.cumsum(sizes)[:-1]
+    out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+    if out_bytes is None:
+        out_bytes = int((out_off + sizes).max()) if nblk else 0
+    d_out = torch.zeros(pad16(out_bytes), dtype=torch.uint8, device=dev)
+    d_rs = torch.from_numpy(rec_start.view(np.int64)).to(dev)
+    d_oo = torch.from_numpy(out_off.view(np.int64)).to(dev)
+    d_io = None
+    if grammar == GRAMMAR_IDX:
+        d_io = torch.from_numpy(np.ascontiguousarray(idx_off, dtype=np.int64)).to(dev)
+    _lib.check(ctx.lib.lsm_encode_blocks(
+        ctx.handle, grammar, _ptr(batch.keys), _ptr(batch.koff), _ptr(batch.vals),
+        _ptr(batch.voff), _ptr(d_io), _ptr(d_rs), nblk, _ptr(d_out), _ptr(d_oo),
+        _stream_handle(stream)), "lsm_encode_blocks")
+    return d_out, out_off
+
+
+# ---- .sst build ---------------------------------------------------------------
+
+def segment_files(ctx: Context, koff: np.ndarray, voff: np.ndarray,
+                  threshold: int = MAX_SSTABLE_SIZE) -> np.ndarray:
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    voff = np.ascontiguousarray(voff, dtype=np.uint64)
+    n = len(koff) - 1
+    starts = np.zeros(n + 2, dtype=np.uint64)
+    nf = ctx.lib.lsm_segment_files_host(koff.ctypes.data, voff.ctypes.data, n, threshold,
+                                        starts.ctypes.data)
+    return starts[: nf + 1].copy()
+
+
+@dataclass
+class SstBuild:
+    out: torch.Tensor
+    file_start: np.ndarray
+    file_off: np.ndarray
+    file_size: np.ndarray
+    footer: torch.Tensor
+    workspace: torch.Tensor
+    d_file_start: torch.Tensor
+    d_file_off: torch.Tensor
+    max_recs: int
+    m: int
+    k: int
+
+
+def prepare_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
+                m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K, align: int = 16) -> SstBuild:
+    dev = ctx.torch_device
+    file_start = np.ascontiguousarray(file_start, dtype=np.uint64)
+    nf = len(file_start) - 1
+    koff, voff = batch.koff_host, batch.voff_host
+    sizes = np.array([ctx.lib.lsm_sst_image_size_host(koff.ctypes.data, voff.ctypes.data,
+                                                      int(file_start[f]), int(file_start[f + 1]),
+                                                      m) for f in range(nf)], dtype=np.uint64)
+    padded = (sizes + (align - 1)) // align * align
+    file_off = np.zeros(nf, dtype=np.uint64)
+    if nf:
+        file_off[1:] = np.cumsum(padded)[:-1]
+    total = int(padded.sum())
+    ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nf, m))
+    max_recs = int(np.diff(file_start.astype(np.int64)).max()) if nf else 0
+    return SstBuild(
+        out=torch.zeros(pad16(total), dtype=torch.uint8, device=dev),
+        file_start=file_start, file_off=file_off, file_size=sizes,
+        footer=torch.zeros(max(nf, 1) * 4, dtype=torch.int64, device=dev),
+        workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
+        d_file_start=torch.from_numpy(file_start.view(np.int64)).to(dev),
+        d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
+        max_recs=max_recs, m=m, k=k)
+
+
+def build_sst_into(ctx: Context, batch: RecordBatch, sb: SstBuild, stream=None) -> None:
+    nf = len(sb.file_start) - 1
+    _lib.check(ctx.lib.lsm_build_sst(
+        ctx.handle, _ptr(batch.keys), _ptr(batch.koff), _ptr(batch.vals), _ptr(batch.voff),
+        _ptr(sb.d_file_start), nf, sb.max_recs, sb.m, sb.k, _ptr(sb.out), _ptr(sb.d_file_off),
+        _ptr(sb.footer), _ptr(sb.workspace), sb.workspace.numel(), _stream_handle(stream)),
+        "lsm_build_sst")
+
+
+def build_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
+              m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K, stream=None) -> SstBuild:
+    sb = prepare_sst(ctx, batch, file_start, m=m, k=k)
+    build_sst_into(ctx, batch, sb, stream=stream)
+    return sb
+
+
+def sum256(ctx: Context, batch: RecordBatch, stream=None) -> torch.Tensor:
+    out = torch.empty((max(batch.n, 1), 4), dtype=torch.int64, device=ctx.torch_device)
+    _lib.check(ctx.lib.lsm_sum256(ctx.handle, _ptr(batch.keys), _ptr(batch.koff), batch.n,
+                                  _ptr(out), _stream_handle(stream)), "lsm_sum256")
+    return out
+
+
+def bloom_probe(ctx: Context, words: torch.Tensor, m: int, k: int, batch: RecordBatch,
+                stream=None) -> torch.Tensor:
+    hit = torch.empty(max(batch.n, 1), dtype=torch.uint8, device=ctx.torch_device)
+    _lib.check(ctx.lib.lsm_bloom_probe(ctx.handle, _ptr(words), m, k, _ptr(batch.keys),
+                                       _ptr(batch.koff), batch.n, _ptr(hit),
+                                       _stream_handle(stream)), "lsm_bloom_probe")
+    return hit

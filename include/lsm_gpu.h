@@ -1,0 +1,195 @@
+/*
+ * lsm_gpu.h — C ABI of the MI355X (gfx950) SSTable block codec.
+ *
+ * Drop-in boundary for the go-lsm hot path (xmh1011/go-lsm @ 2025-08-24):
+ * the Go methods it replaces are cited per entry point.  Plain pointers and
+ * sizes only; `stream` is an opaque hipStream_t (NULL = default stream).
+ * Every launch entry point is asynchronous on `stream`, performs no device
+ * allocation and no host synchronisation (hipGraph-capturable); the caller
+ * owns every buffer and the library keeps no pointer after the call returns.
+ *
+ * Device input buffers must be readable up to the next multiple of 16 bytes
+ * past the last block byte (the kernels stream 16-byte aligned chunks; the
+ * bytes past a block are never interpreted).
+ *
+ * Return convention: 0 = ok; negative = LSM_E* (argument error) or
+ * -(1000 + hipError_t) for a HIP runtime error.
+ */
+#ifndef LSM_GPU_H
+#define LSM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSM_ABI_VERSION 1
+
+/* Record grammars (all fixed-width little-endian). */
+enum lsm_grammar {
+    LSM_GRAMMAR_V = 0,   /* ([u32 vlen][value])*            sstable/block/data.go:26-79   */
+    LSM_GRAMMAR_KV = 1,  /* ([u32 klen][key][u32 vlen][v])*  kv/kv.go:46-115, wal/wal.go:107 */
+    LSM_GRAMMAR_IDX = 2, /* ([u32 klen][key][i64 offset])*   sstable/block/index.go:30-101 */
+};
+
+/* Per-block decode status (d_status[b]); d_nrec[b] always counts the
+ * records decoded before the status was raised (data.go:75 keeps them). */
+enum lsm_status {
+    LSM_OK = 0,
+    LSM_ST_TRUNC_LEN_PREFIX = 1, /* 1-3 bytes left for a leading u32 length: data.go:65 "read value length failed", kv.go:80 "decode key length" */
+    LSM_ST_TRUNC_KEY = 2,        /* kv.go:90 "decode key"                          */
+    LSM_ST_KEY_TOO_LONG = 3,     /* kv.go:84 "invalid key length: %d" (> 1<<20)   */
+    LSM_ST_TRUNC_VLEN = 4,       /* kv.go:98 "decode value length"                 */
+    LSM_ST_VAL_TOO_LONG = 5,     /* kv.go:102 "invalid value length: %d" (> 1<<30) */
+    LSM_ST_TRUNC_VAL = 6,        /* data.go:71 "read value data failed", kv.go:108 "decode value" */
+    LSM_ST_IDX_OVERRUN = 7,      /* index.go:88-91 "unexpected EOF: size limit reached while reading key length" */
+    LSM_ST_CAPACITY = 8,         /* record capacity rec_base[b+1]-rec_base[b] exhausted (not a reference error) */
+};
+
+enum lsm_error {
+    LSM_EINVAL = -1,  /* bad argument                        */
+    LSM_ENODEV = -2,  /* no gfx950 device / device not found  */
+    LSM_ENOMEM = -3,  /* host allocation failed              */
+    LSM_ESPACE = -4,  /* workspace too small                 */
+};
+
+/* One decoded record: a zero-copy view into the input buffer.
+ *   KV : key  = d_in[rec_off+4 .. +key_len), value = d_in[rec_off+8+key_len .. +val_len)
+ *   V  : key_len = 0, value = d_in[rec_off+4 .. +val_len)
+ *   IDX: key  = d_in[rec_off+4 .. +key_len), val_len = 8 (the i64 offset follows the key) */
+typedef struct lsm_rec_desc {
+    uint64_t rec_off;
+    uint32_t key_len;
+    uint32_t val_len;
+} lsm_rec_desc;
+
+/* Outputs of lsm_decode_blocks.  Record i of block b goes to slot
+ * base(b) + i of every per-record array, where
+ *   rec_base != NULL : base(b) = rec_base[b], capacity rec_base[b+1]-rec_base[b]
+ *                      (lsm_plan_rec_base computes a dense-capacity plan);
+ *   rec_base == NULL : offset-addressed, base(b) = blk_off[b] / R and capacity
+ *                      (blk_off[b]+blk_len[b]) / R - base(b), R = 4 (V), 8 (KV),
+ *                      12 (IDX) -- disjoint for non-overlapping blocks, no plan
+ *                      needed; per-record arrays need (input bytes / R) + 1 slots. */
+typedef struct lsm_decode_out {
+    lsm_rec_desc *desc;         /* required                                         */
+    const uint64_t *rec_base;   /* optional, nblk+1 entries (see above)             */
+    uint32_t *nrec;             /* required, nblk                                   */
+    int32_t *status;            /* required, nblk                                   */
+    int64_t *idx_value;         /* IDX only, optional: the entry's i64 offset       */
+    /* Materialized ("ARENA") mode, all optional.  Keys / values of block b are
+     * packed, in record order, from key_arena + A(b) / val_arena + A(b), where
+     * A(b) = arena_base[b] (lsm_plan_arena_base: exclusive scan of blk_len) or,
+     * with arena_base == NULL, A(b) = blk_off[b] (arenas mirror the input's
+     * addressing; a block's keys or values never exceed blk_len bytes). */
+    uint8_t *key_arena;
+    uint8_t *val_arena;
+    const uint64_t *arena_base; /* optional, nblk+1                                 */
+    uint64_t *key_arena_off;    /* optional per record: absolute offset in key_arena */
+    uint64_t *val_arena_off;    /* optional per record: absolute offset in val_arena */
+} lsm_decode_out;
+
+typedef struct lsm_ctx lsm_ctx;
+
+/* ---- context ------------------------------------------------------------ */
+
+int lsm_abi_version(void);
+/* One context per goroutine / OS thread (callers are concurrent goroutines,
+ * sstable_test.go:379-400); no hidden global mutable state. */
+int lsm_ctx_create(int device, lsm_ctx **out);
+int lsm_ctx_destroy(lsm_ctx *ctx);
+/* Number of compute units of the context's device (grid sizing). */
+int lsm_ctx_num_cus(const lsm_ctx *ctx);
+
+/* ---- planning ------------------------------------------------------------ */
+
+/* Largest record count a block of `len` bytes can hold: KV len/8, V len/4,
+ * IDX len/12 (every record carries at least its fixed-width fields). */
+uint64_t lsm_max_records(int grammar, uint64_t len);
+size_t lsm_plan_workspace_bytes(uint32_t nblk);
+/* d_rec_base[0..nblk] = exclusive scan of lsm_max_records(grammar, blk_len[b]). */
+int lsm_plan_rec_base(lsm_ctx *ctx, int grammar, const uint32_t *d_blk_len, uint32_t nblk,
+                      uint64_t *d_rec_base, void *d_workspace, size_t ws_bytes, void *stream);
+/* d_arena_base[0..nblk] = exclusive scan of blk_len[b]. */
+int lsm_plan_arena_base(lsm_ctx *ctx, const uint32_t *d_blk_len, uint32_t nblk,
+                        uint64_t *d_arena_base, void *d_workspace, size_t ws_bytes, void *stream);
+
+/* ---- decode ---------------------------------------------------------------- */
+
+/* Batch decode of independent blocks [blk_off[b], blk_off[b]+blk_len[b]).
+ * Replaces, per block:
+ *   V   : block.DataBlock.DecodeFrom(r, size)      sstable/block/data.go:49-79
+ *   KV  : kv.KeyValuePair.DecodeFrom loop           kv/kv.go:77-115, wal/wal.go:106-118
+ *   IDX : block.IndexBlock.DecodeFrom(r, size)     sstable/block/index.go:61-101
+ * and, composed by the host layer, SSTable.DecodeDataBlock/GetDataBlockFromFile
+ * (sstable/sstable.go:214-246).  One wavefront owns one block: the block is
+ * streamed into an LDS ring and the record boundaries are chased there. */
+int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in, const uint64_t *d_blk_off,
+                      const uint32_t *d_blk_len, uint32_t nblk, const lsm_decode_out *out,
+                      void *stream);
+
+/* ---- encode ---------------------------------------------------------------- */
+
+/* Batch encode of a columnar record batch (CSR: record i's key is
+ * d_keys[d_koff[i] .. d_koff[i+1]), value d_vals[d_voff[i] .. d_voff[i+1])).
+ * Block b holds records [rec_start[b], rec_start[b+1]) and is written
+ * contiguously at d_out + out_off[b]; bytes between blocks are untouched.
+ * Replaces KeyValuePair.EncodeTo (kv.go:46-74), DataBlock.EncodeTo
+ * (data.go:26-45 / Value.EncodeTo kv.go:165-178) and IndexBlock.Encode
+ * (index.go:47-58; d_idx_off[i] is record i's i64 offset, IDX only). */
+uint64_t lsm_encoded_size_host(int grammar, const uint64_t *koff, const uint64_t *voff,
+                               uint64_t r0, uint64_t r1);
+int lsm_encode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_keys, const uint64_t *d_koff,
+                      const uint8_t *d_vals, const uint64_t *d_voff, const int64_t *d_idx_off,
+                      const uint64_t *d_rec_start, uint32_t nblk, uint8_t *d_out,
+                      const uint64_t *d_out_off, void *stream);
+
+/* ---- .sst build (builder path + fused bloom) ------------------------------ */
+
+/* Builder flush rule on host-resident CSR offsets: Builder.Add/ShouldFlush
+ * (builder.go:34-42, EstimateSize kv.go:118-121) as driven by
+ * CompactAndMergeKVs (merge.go:106-123).  threshold 0 = never flush
+ * (BuildSSTableFromIMemTable builder.go:22-31); go-lsm uses 2 MiB
+ * (sstable.go:21).  Writes file_start[0..nfile] (file_start[nfile] = n);
+ * returns nfile.  file_start must hold n+1 entries. */
+uint64_t lsm_segment_files_host(const uint64_t *koff, const uint64_t *voff, uint64_t n,
+                                uint64_t threshold, uint64_t *file_start);
+/* Exact .sst image size of records [r0, r1) (host-resident CSR offsets). */
+uint64_t lsm_sst_image_size_host(const uint64_t *koff, const uint64_t *voff, uint64_t r0,
+                                 uint64_t r1, uint64_t m);
+/* Filter block bytes for m bits: 8 + 24 + 8*ceil(m/64) (bloom.go:472-491). */
+uint64_t lsm_filter_block_size(uint64_t m);
+size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint64_t m);
+
+/* Build nfile .sst images: file f holds records [file_start[f], file_start[f+1])
+ * and its image (Header | Filter | V data | IDX index | Footer) is written at
+ * d_out + file_off[f].  Replaces Builder.Add/Build (builder.go:34-59),
+ * SSTable.Add (sstable.go:322-326), bloom Filter.Add (bloom.go:175-181,
+ * murmur.go:245-275) and SSTable.EncodeTo (sstable.go:131-193).  The bloom
+ * (m bits, k hashes; go-lsm default 1,600,000 / 16, bloom.go:79-82) is
+ * built in LDS slices and fused into the image.  d_footer (optional) gets
+ * {dataOff, dataSize, idxOff, idxSize} per file.  max_file_records bounds
+ * the grid (largest file_start[f+1]-file_start[f]).  Requires m >= 1. */
+int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                  const uint8_t *d_vals, const uint64_t *d_voff, const uint64_t *d_file_start,
+                  uint32_t nfile, uint32_t max_file_records, uint64_t m, uint32_t k,
+                  uint8_t *d_out, const uint64_t *d_file_off, int64_t *d_footer,
+                  void *d_workspace, size_t ws_bytes, void *stream);
+
+/* ---- bloom probe (verification side, Filter.Test bloom.go:371-379) ------- */
+
+/* d_hit[i] = Filter.Test(key i) against the filter words of one .sst
+ * (native u64 words, bit p -> word p>>6 bit p&63). */
+int lsm_bloom_probe(lsm_ctx *ctx, const uint64_t *d_words, uint64_t m, uint32_t k,
+                    const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
+                    uint8_t *d_hit, void *stream);
+/* sum256 (murmur.go:245-275) of each key: d_h[4*i .. 4*i+3]. */
+int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
+               uint64_t *d_h, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSM_GPU_H */

@@ -1,0 +1,504 @@
+/*
+ * lsm_oracle.c — CPU restatement of the go-lsm block-codec path.
+ * TEST INFRASTRUCTURE ONLY (see lsm_oracle.h).  Citations are
+ * path:line in xmh1011/go-lsm @ 2025-08-24.
+ */
+#include "lsm_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- little/big-endian helpers (encoding/binary) ---------------------- */
+
+static inline uint32_t ld_u32le(const uint8_t *p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+static inline uint64_t ld_u64le(const uint8_t *p) {
+    return (uint64_t)ld_u32le(p) | (uint64_t)ld_u32le(p + 4) << 32;
+}
+static inline uint64_t ld_u64be(const uint8_t *p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v = v << 8 | p[i];
+    return v;
+}
+static inline void st_u32le(uint8_t *p, uint32_t v) {
+    for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+static inline void st_u64le(uint8_t *p, uint64_t v) {
+    for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+static inline void st_u64be(uint8_t *p, uint64_t v) {
+    for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * (7 - i)));
+}
+
+#define KEY_CAP (1u << 20) /* kv.go:84  */
+#define VAL_CAP (1u << 30) /* kv.go:102 */
+
+/* ---- record decode ---------------------------------------------------- */
+
+int ora_decode_block(int grammar, const uint8_t *base, uint64_t blk_off, uint64_t blk_len,
+                     ora_desc *desc, int64_t *idx_val, uint64_t cap, uint32_t *nrec) {
+    const uint8_t *b = base + blk_off;
+    const uint64_t n = blk_len;
+    uint64_t pos = 0;
+    uint64_t cnt = 0;
+    int st = ORA_OK;
+
+    if (grammar == ORA_GRAMMAR_V) {
+        /* data.go:58-76: loop { binary.Read u32; EOF -> stop; short -> error;
+         * make(valLen); ReadFull; append }.  The block is the LimitReader. */
+        for (;;) {
+            uint64_t rem = n - pos;
+            if (rem == 0) break;                                 /* io.EOF, :62-63  */
+            if (rem < 4) { st = ORA_TRUNC_LEN_PREFIX; break; }   /* :65-66          */
+            uint32_t vlen = ld_u32le(b + pos);
+            if (rem - 4 < vlen) { st = ORA_TRUNC_VAL; break; }   /* :71-73          */
+            if (cnt >= cap) { st = ORA_CAPACITY; break; }
+            desc[cnt].rec_off = blk_off + pos;
+            desc[cnt].key_len = 0;
+            desc[cnt].val_len = vlen;
+            cnt++;
+            pos += 4 + (uint64_t)vlen;
+        }
+    } else if (grammar == ORA_GRAMMAR_KV) {
+        /* wal.go:107 `for buf.Len() > 0` around KeyValuePair.DecodeFrom kv.go:77-115 */
+        while (pos < n) {
+            uint64_t rem = n - pos;
+            if (rem < 4) { st = ORA_TRUNC_LEN_PREFIX; break; }   /* kv.go:80-82   */
+            uint32_t klen = ld_u32le(b + pos);
+            if (klen > KEY_CAP) { st = ORA_KEY_TOO_LONG; break; } /* kv.go:84-86  */
+            if (rem - 4 < klen) { st = ORA_TRUNC_KEY; break; }    /* kv.go:90-92  */
+            uint64_t vp = pos + 4 + klen;
+            uint64_t rem2 = n - vp;
+            if (rem2 < 4) { st = ORA_TRUNC_VLEN; break; }         /* kv.go:98-100 */
+            uint32_t vlen = ld_u32le(b + vp);
+            if (vlen > VAL_CAP) { st = ORA_VAL_TOO_LONG; break; } /* kv.go:102-104 */
+            if (rem2 - 4 < vlen) { st = ORA_TRUNC_VAL; break; }   /* kv.go:108-110 */
+            if (cnt >= cap) { st = ORA_CAPACITY; break; }
+            desc[cnt].rec_off = blk_off + pos;
+            desc[cnt].key_len = klen;
+            desc[cnt].val_len = vlen;
+            cnt++;
+            pos = vp + 4 + vlen;
+        }
+    } else if (grammar == ORA_GRAMMAR_IDX) {
+        /* index.go:70-98: while totalRead < size { Key.DecodeFrom; read i64;
+         * totalRead += 4+klen+8; if totalRead > size -> error }.  Bytes past
+         * the block are treated as present (the .sst footer follows the
+         * index), so any entry crossing the limit is the overrun error. */
+        while (pos < n) {
+            uint64_t rem = n - pos;
+            if (rem < 4) { st = ORA_IDX_OVERRUN; break; }
+            uint32_t klen = ld_u32le(b + pos);
+            if (rem < 12 + (uint64_t)klen) { st = ORA_IDX_OVERRUN; break; }
+            if (cnt >= cap) { st = ORA_CAPACITY; break; }
+            desc[cnt].rec_off = blk_off + pos;
+            desc[cnt].key_len = klen;
+            desc[cnt].val_len = 8;
+            if (idx_val) idx_val[cnt] = (int64_t)ld_u64le(b + pos + 4 + klen);
+            cnt++;
+            pos += 12 + (uint64_t)klen;
+        }
+    }
+    *nrec = (uint32_t)cnt;
+    return st;
+}
+
+uint64_t ora_materialize(int grammar, const uint8_t *base, const ora_desc *desc, uint64_t n,
+                         uint8_t *key_arena, uint8_t *val_arena, uint64_t *val_bytes) {
+    uint64_t kb = 0, vb = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t *r = base + desc[i].rec_off;
+        uint32_t kl = desc[i].key_len, vl = desc[i].val_len;
+        if (grammar == ORA_GRAMMAR_V) {
+            memcpy(val_arena + vb, r + 4, vl);
+            vb += vl;
+        } else if (grammar == ORA_GRAMMAR_KV) {
+            memcpy(key_arena + kb, r + 4, kl);
+            kb += kl;
+            memcpy(val_arena + vb, r + 8 + kl, vl);
+            vb += vl;
+        } else {
+            memcpy(key_arena + kb, r + 4, kl);
+            kb += kl;
+        }
+    }
+    if (val_bytes) *val_bytes = vb;
+    return kb;
+}
+
+/* ---- record encode ---------------------------------------------------- */
+
+uint64_t ora_encoded_size(int grammar, const uint64_t *koff, const uint64_t *voff, uint64_t r0,
+                          uint64_t r1) {
+    uint64_t n = r1 - r0;
+    if (grammar == ORA_GRAMMAR_V) return 4 * n + (voff[r1] - voff[r0]);
+    if (grammar == ORA_GRAMMAR_KV) return 8 * n + (koff[r1] - koff[r0]) + (voff[r1] - voff[r0]);
+    return 12 * n + (koff[r1] - koff[r0]);
+}
+
+uint64_t ora_encode_records(int grammar, const uint8_t *keys, const uint64_t *koff,
+                            const uint8_t *vals, const uint64_t *voff, uint64_t r0, uint64_t r1,
+                            const int64_t *idx_off, uint8_t *out) {
+    uint64_t w = 0;
+    for (uint64_t i = r0; i < r1; i++) {
+        if (grammar == ORA_GRAMMAR_KV || grammar == ORA_GRAMMAR_IDX) {
+            uint32_t kl = (uint32_t)(koff[i + 1] - koff[i]); /* uint32(len(key)) kv.go:48 */
+            st_u32le(out + w, kl);
+            memcpy(out + w + 4, keys + koff[i], kl);
+            w += 4 + (uint64_t)kl;
+        }
+        if (grammar == ORA_GRAMMAR_KV || grammar == ORA_GRAMMAR_V) {
+            uint32_t vl = (uint32_t)(voff[i + 1] - voff[i]);
+            st_u32le(out + w, vl);
+            memcpy(out + w + 4, vals + voff[i], vl);
+            w += 4 + (uint64_t)vl;
+        } else {
+            st_u64le(out + w, (uint64_t)idx_off[i - r0]); /* index.go:37 */
+            w += 8;
+        }
+    }
+    return w;
+}
+
+/* ---- MurmurHash3 restatement of digest128 (murmur.go) ----------------- */
+
+#define MC1 0x87c37b91114253d5ULL /* murmur.go:52 */
+#define MC2 0x4cf5ad432745937fULL /* murmur.go:53 */
+
+static inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+static inline uint64_t fmix(uint64_t k) { /* murmur.go:223-230 */
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+typedef struct { uint64_t h1, h2; } digest;
+
+static void mix_words(digest *d, uint64_t k1, uint64_t k2) { /* bmixWords murmur.go:74-95 */
+    uint64_t h1 = d->h1, h2 = d->h2;
+    k1 *= MC1; k1 = rotl64(k1, 31); k1 *= MC2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= MC2; k2 = rotl64(k2, 33); k2 *= MC1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    d->h1 = h1; d->h2 = h2;
+}
+
+/* sum128 murmur.go:104-221: fold a tail of tl (<16) bytes, then finalize
+ * with the total length.  The Go padTail switch ORs a virtual 0x01 byte at
+ * tail position len(tail); here the caller passes that byte in `tail`. */
+static void finish(const digest *d, uint64_t length, const uint8_t *tail, unsigned tl,
+                   uint64_t *o1, uint64_t *o2) {
+    uint64_t h1 = d->h1, h2 = d->h2, k1 = 0, k2 = 0;
+    for (unsigned i = 8; i < tl; i++) k2 ^= (uint64_t)tail[i] << (8 * (i - 8));
+    if (tl > 8) { k2 *= MC2; k2 = rotl64(k2, 33); k2 *= MC1; h2 ^= k2; }
+    for (unsigned i = 0; i < tl && i < 8; i++) k1 ^= (uint64_t)tail[i] << (8 * i);
+    if (tl > 0) { k1 *= MC1; k1 = rotl64(k1, 31); k1 *= MC2; h1 ^= k1; }
+    h1 ^= length; h2 ^= length;
+    h1 += h2; h2 += h1;
+    h1 = fmix(h1); h2 = fmix(h2);
+    h1 += h2; h2 += h1;
+    *o1 = h1; *o2 = h2;
+}
+
+void ora_sum256(const uint8_t *data, uint64_t len, uint64_t h[4]) { /* murmur.go:245-275 */
+    digest d = {0, 0};
+    uint64_t nb = len / 16;
+    for (uint64_t i = 0; i < nb; i++) mix_words(&d, ld_u64le(data + 16 * i), ld_u64le(data + 16 * i + 8));
+    unsigned tl = (unsigned)(len % 16);
+    const uint8_t *tail = data + len - tl;
+    finish(&d, len, tail, tl, &h[0], &h[1]);
+    uint8_t t2[16];
+    memcpy(t2, tail, tl);
+    t2[tl] = 1; /* virtually append 0x01 (murmur.go:251-270) */
+    if (tl + 1 == 16) {
+        mix_words(&d, ld_u64le(t2), ld_u64le(t2 + 8));
+        finish(&d, len + 1, t2, 0, &h[2], &h[3]);
+    } else {
+        finish(&d, len + 1, t2, tl + 1, &h[2], &h[3]);
+    }
+}
+
+/* ---- bloom (bloom.go) -------------------------------------------------- */
+
+uint64_t ora_location(const uint64_t h[4], uint64_t i) { /* bloom.go:133-136 */
+    return h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)];
+}
+
+void ora_bloom_add(uint64_t *words, uint64_t m, uint64_t k, const uint8_t *key, uint64_t len) {
+    uint64_t h[4];
+    uint64_t am = m ? m : 1, hk = k ? k : 1; /* NewBloomFilter max(1,..) bloom.go:95-101 */
+    ora_sum256(key, len, h);
+    for (uint64_t i = 0; i < hk; i++) {
+        uint64_t p = ora_location(h, i) % am; /* bloom.go:139-141 */
+        words[p >> 6] |= 1ULL << (p & 63);    /* bitset.Set         */
+    }
+}
+
+int ora_bloom_test(const uint64_t *words, uint64_t m, uint64_t k, const uint8_t *key,
+                   uint64_t len) {
+    uint64_t h[4];
+    uint64_t am = m ? m : 1, hk = k ? k : 1;
+    ora_sum256(key, len, h);
+    for (uint64_t i = 0; i < hk; i++) {
+        uint64_t p = ora_location(h, i) % am;
+        if (!(words[p >> 6] >> (p & 63) & 1)) return 0;
+    }
+    return 1;
+}
+
+void ora_estimate_parameters(uint64_t n, double p, uint64_t *m, uint64_t *k) {
+    double ln2 = log(2.0);
+    *m = (uint64_t)ceil(-1.0 * (double)n * log(p) / pow(ln2, 2));
+    *k = (uint64_t)ceil(ln2 * (double)*m / (double)n);
+}
+
+uint64_t ora_filter_block_size(uint64_t m) { return 8 + 24 + 8 * ((m + 63) / 64); }
+
+uint64_t ora_filter_encode(const uint64_t *words, uint64_t m, uint64_t k, uint8_t *out) {
+    uint64_t nw = (m + 63) / 64;
+    st_u64le(out, 24 + 8 * nw);        /* EncodeTo length prefix, bloom.go:478 */
+    st_u64be(out + 8, m ? m : 1);       /* WriteTo arraySize, bloom.go:240     */
+    st_u64be(out + 16, k ? k : 1);      /* WriteTo hashNum,  bloom.go:244      */
+    st_u64be(out + 24, m);              /* bitset length                        */
+    for (uint64_t i = 0; i < nw; i++) st_u64be(out + 32 + 8 * i, words[i]);
+    return 32 + 8 * nw;
+}
+
+int ora_filter_decode(const uint8_t *in, uint64_t n, uint64_t *m, uint64_t *k, uint64_t *nbits,
+                      uint64_t *words, uint64_t words_cap, uint64_t *consumed) {
+    if (n < 8) return -1;                       /* "decode filter length"        */
+    uint64_t L = ld_u64le(in);
+    if (L > n - 8) return -2;                   /* "decode filter data"          */
+    const uint8_t *p = in + 8;
+    if (L < 24) return -3;                      /* ReadFrom m/k/length short     */
+    *m = ld_u64be(p);
+    *k = ld_u64be(p + 8);
+    *nbits = ld_u64be(p + 16);
+    uint64_t nw = (*nbits + 63) / 64;
+    if (nw > (L - 24) / 8) return -4;           /* bitset.ReadFrom words short   */
+    if (words) {
+        if (nw > words_cap) return -5;
+        for (uint64_t i = 0; i < nw; i++) words[i] = ld_u64be(p + 24 + 8 * i);
+    }
+    *consumed = 8 + L;
+    return 0;
+}
+
+/* ---- .sst -------------------------------------------------------------- */
+
+uint64_t ora_segment_files(const uint64_t *koff, const uint64_t *voff, uint64_t n,
+                           uint64_t threshold, uint64_t *starts) {
+    uint64_t nf = 0, size = 0, start = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        size += 4 + (koff[i + 1] - koff[i]) + 4 + (voff[i + 1] - voff[i]) + 8; /* kv.go:118-121 */
+        if (threshold && size >= threshold) {                                    /* builder.go:40-42 */
+            starts[nf++] = start;
+            start = i + 1;
+            size = 0;
+        }
+    }
+    if (size > 0) starts[nf++] = start; /* merge.go:120-123 */
+    starts[nf] = n;
+    return nf;
+}
+
+static uint64_t header_size(const uint64_t *koff, uint64_t r0, uint64_t r1) {
+    if (r1 <= r0) return 8;
+    return 8 + (koff[r0 + 1] - koff[r0]) + (koff[r1] - koff[r1 - 1]);
+}
+
+uint64_t ora_sst_image_size(const uint64_t *koff, const uint64_t *voff, uint64_t r0, uint64_t r1,
+                            uint64_t m) {
+    return header_size(koff, r0, r1) + ora_filter_block_size(m) +
+           ora_encoded_size(ORA_GRAMMAR_V, koff, voff, r0, r1) +
+           ora_encoded_size(ORA_GRAMMAR_IDX, koff, voff, r0, r1) + 32;
+}
+
+uint64_t ora_build_sst(const uint8_t *keys, const uint64_t *koff, const uint8_t *vals,
+                       const uint64_t *voff, uint64_t r0, uint64_t r1, uint64_t m, uint64_t k,
+                       uint8_t *out, int64_t footer_out[4]) {
+    uint64_t w = 0;
+    /* Header (builder.go:45-53 Finalize; header.go:25-37 EncodeTo) */
+    if (r1 > r0) {
+        uint32_t l0 = (uint32_t)(koff[r0 + 1] - koff[r0]);
+        uint32_t l1 = (uint32_t)(koff[r1] - koff[r1 - 1]);
+        st_u32le(out, l0); memcpy(out + 4, keys + koff[r0], l0); w = 4 + l0;
+        st_u32le(out + w, l1); memcpy(out + w + 4, keys + koff[r1 - 1], l1); w += 4 + l1;
+    } else {
+        st_u32le(out, 0); st_u32le(out + 4, 0); w = 8;
+    }
+    /* Filter (SSTable.Add -> Filter.Add, sstable.go:322-326; EncodeTo bloom.go:472) */
+    uint64_t nw = (m + 63) / 64;
+    uint64_t *words = (uint64_t *)calloc(nw ? nw : 1, 8);
+    for (uint64_t i = r0; i < r1; i++) ora_bloom_add(words, m, k, keys + koff[i], koff[i + 1] - koff[i]);
+    w += ora_filter_encode(words, m, k, out + w);
+    free(words);
+    /* Data region: sstable.go:159-175, offsets by exclusive prefix sum */
+    int64_t data_off = (int64_t)w;
+    uint64_t n = r1 - r0;
+    int64_t *ioff = (int64_t *)malloc((n ? n : 1) * sizeof(int64_t));
+    uint64_t cur = w;
+    for (uint64_t i = r0; i < r1; i++) {
+        ioff[i - r0] = (int64_t)cur;
+        cur += 4 + (voff[i + 1] - voff[i]);
+    }
+    w += ora_encode_records(ORA_GRAMMAR_V, keys, koff, vals, voff, r0, r1, NULL, out + w);
+    int64_t data_size = (int64_t)w - data_off;
+    /* Index region: sstable.go:178-186 */
+    int64_t idx_off = (int64_t)w;
+    w += ora_encode_records(ORA_GRAMMAR_IDX, keys, koff, vals, voff, r0, r1, ioff, out + w);
+    int64_t idx_size = (int64_t)w - idx_off;
+    free(ioff);
+    /* Footer footer.go:43-55 */
+    st_u64le(out + w, (uint64_t)data_off);
+    st_u64le(out + w + 8, (uint64_t)data_size);
+    st_u64le(out + w + 16, (uint64_t)idx_off);
+    st_u64le(out + w + 24, (uint64_t)idx_size);
+    w += 32;
+    if (footer_out) {
+        footer_out[0] = data_off; footer_out[1] = data_size;
+        footer_out[2] = idx_off; footer_out[3] = idx_size;
+    }
+    return w;
+}
+
+int ora_sst_decode(const uint8_t *file, uint64_t n, ora_sst_meta *meta, ora_desc *idx_desc,
+                   int64_t *idx_val, uint64_t idx_cap, ora_desc *data_desc, uint64_t data_cap) {
+    memset(meta, 0, sizeof(*meta));
+    uint64_t pos = 0;
+    /* Header.DecodeFrom header.go:40-52 (Key.DecodeFrom kv.go:124-139, no cap) */
+    for (int j = 0; j < 2; j++) {
+        if (n - pos < 4) { meta->stage = 1; return 1; }
+        uint32_t kl = ld_u32le(file + pos);
+        if (n - pos - 4 < kl) { meta->stage = 1; return 1; }
+        if (j == 0) { meta->min_key_off = pos + 4; meta->min_key_len = kl; }
+        else { meta->max_key_off = pos + 4; meta->max_key_len = kl; }
+        pos += 4 + (uint64_t)kl;
+    }
+    /* Filter.DecodeFrom bloom.go:453-469 */
+    uint64_t used = 0;
+    if (ora_filter_decode(file + pos, n - pos, &meta->filter_m, &meta->filter_k,
+                          &meta->filter_nbits, NULL, 0, &used) != 0) {
+        meta->stage = 2; return 2;
+    }
+    meta->filter_words_off = pos + 8 + 24;
+    /* DecodeFooterFrom sstable.go:195-212 */
+    if (n < 32) { meta->stage = 3; return 3; }
+    const uint8_t *f = file + n - 32;
+    meta->data_off = (int64_t)ld_u64le(f);
+    meta->data_size = (int64_t)ld_u64le(f + 8);
+    meta->idx_off = (int64_t)ld_u64le(f + 16);
+    meta->idx_size = (int64_t)ld_u64le(f + 24);
+    /* IndexBlock.DecodeFrom(file@idx_off, idx_size) sstable.go:116-125, index.go:61-101 */
+    if (meta->idx_off < 0) { meta->stage = 4; return 4; }
+    if (meta->idx_size < 0) { meta->stage = 4; return 4; } /* index.go:65-68 */
+    uint64_t io = (uint64_t)meta->idx_off;
+    uint64_t avail = io <= n ? n - io : 0;
+    uint64_t il = (uint64_t)meta->idx_size < avail ? (uint64_t)meta->idx_size : avail;
+    if ((uint64_t)meta->idx_size > avail) {
+        /* the stream ends before the limit: whatever entries fit, then a read error */
+        uint32_t c = 0;
+        ora_decode_block(ORA_GRAMMAR_IDX, file, io, il, idx_desc, idx_val, idx_cap, &c);
+        meta->nidx = c; meta->status = ORA_IDX_OVERRUN; meta->stage = 4; return 4;
+    }
+    int st = ora_decode_block(ORA_GRAMMAR_IDX, file, io, il, idx_desc, idx_val, idx_cap, &meta->nidx);
+    if (st) { meta->status = st; meta->stage = 4; return 4; }
+    /* DecodeDataBlock sstable.go:214-225 -> DataBlock.DecodeFrom(file, size):
+     * size > 0 -> LimitReader, else unlimited to EOF (data.go:51-54). */
+    if (meta->data_off < 0) { meta->stage = 5; return 5; }
+    uint64_t dof = (uint64_t)meta->data_off;
+    uint64_t davail = dof <= n ? n - dof : 0;
+    uint64_t dl = (meta->data_size > 0 && (uint64_t)meta->data_size < davail) ? (uint64_t)meta->data_size : davail;
+    st = ora_decode_block(ORA_GRAMMAR_V, file, dof, dl, data_desc, NULL, data_cap, &meta->ndata);
+    if (st) { meta->status = st; meta->stage = 5; return 5; }
+    /* GetKeyValuePairs sstable.go:248-268 */
+    if (meta->ndata == 0 || meta->nidx == 0) return 0;
+    if (meta->ndata != meta->nidx) { meta->stage = 6; return 6; }
+    return 0;
+}
+
+/* ---- Go-pattern CPU baseline ------------------------------------------ */
+
+typedef struct { uint8_t *key; uint32_t klen; uint8_t *val; uint32_t vlen; } golike_pair;
+
+typedef struct {
+    int grammar;
+    const uint8_t *base;
+    const uint64_t *blk_off;
+    const uint32_t *blk_len;
+    uint64_t b0, b1;
+    uint64_t recs;
+} golike_job;
+
+static void *golike_worker(void *arg) {
+    golike_job *j = (golike_job *)arg;
+    uint64_t recs = 0;
+    for (uint64_t b = j->b0; b < j->b1; b++) {
+        const uint8_t *p = j->base + j->blk_off[b];
+        uint64_t n = j->blk_len[b], pos = 0;
+        golike_pair *pairs = NULL;
+        uint64_t np = 0, capp = 0;
+        while (pos < n) {
+            uint32_t kl = 0, vl;
+            uint8_t *key = NULL;
+            uint8_t lenbuf[4];
+            if (j->grammar != ORA_GRAMMAR_V) {
+                if (n - pos < 4) break;
+                memcpy(lenbuf, p + pos, 4); /* binary.Read copies into a fresh buffer */
+                kl = ld_u32le(lenbuf);
+                if (kl > KEY_CAP || n - pos - 4 < kl) break;
+                key = (uint8_t *)malloc(kl ? kl : 1);
+                memcpy(key, p + pos + 4, kl);
+                pos += 4 + (uint64_t)kl;
+            }
+            if (n - pos < 4) { free(key); break; }
+            memcpy(lenbuf, p + pos, 4);
+            vl = ld_u32le(lenbuf);
+            if (n - pos - 4 < vl) { free(key); break; }
+            uint8_t *val = (uint8_t *)malloc(vl ? vl : 1);
+            memcpy(val, p + pos + 4, vl);
+            pos += 4 + (uint64_t)vl;
+            if (np == capp) { /* append growth */
+                capp = capp ? capp * 2 : 1;
+                pairs = (golike_pair *)realloc(pairs, capp * sizeof(golike_pair));
+            }
+            pairs[np].key = key; pairs[np].klen = kl;
+            pairs[np].val = val; pairs[np].vlen = vl;
+            np++;
+        }
+        recs += np;
+        for (uint64_t i = 0; i < np; i++) { free(pairs[i].key); free(pairs[i].val); }
+        free(pairs);
+    }
+    j->recs = recs;
+    return NULL;
+}
+
+uint64_t ora_bench_decode_golike(int grammar, const uint8_t *base, const uint64_t *blk_off,
+                                 const uint32_t *blk_len, uint64_t nblk, int threads) {
+    if (threads < 1) threads = 1;
+    golike_job *jobs = (golike_job *)calloc((size_t)threads, sizeof(golike_job));
+    pthread_t *tids = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    for (int t = 0; t < threads; t++) {
+        jobs[t].grammar = grammar; jobs[t].base = base;
+        jobs[t].blk_off = blk_off; jobs[t].blk_len = blk_len;
+        jobs[t].b0 = nblk * (uint64_t)t / (uint64_t)threads;
+        jobs[t].b1 = nblk * (uint64_t)(t + 1) / (uint64_t)threads;
+        if (threads == 1) golike_worker(&jobs[t]);
+        else pthread_create(&tids[t], NULL, golike_worker, &jobs[t]);
+    }
+    uint64_t recs = 0;
+    for (int t = 0; t < threads; t++) {
+        if (threads > 1) pthread_join(tids[t], NULL);
+        recs += jobs[t].recs;
+    }
+    free(jobs); free(tids);
+    return recs;
+}

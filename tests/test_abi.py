@@ -1,0 +1,95 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol declared in
+include/lsm_gpu.h, and its host-side logic (builder flush rule, image sizes,
+capacities) matches the oracle.  No GPU compute calls here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import pyoracle as ora
+from lsmgpu import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lsm_gpu.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lsm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_functions_exported():
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in lsm_gpu.h but not exported"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with the header"
+
+
+def test_abi_version():
+    assert _lib.load().lsm_abi_version() == 1
+
+
+def test_ctx_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = _lib.load().lsm_ctx_create(0, ctypes.byref(h))
+    assert rc != 0 and not h.value
+
+
+def test_max_records():
+    lib = _lib.load()
+    assert lib.lsm_max_records(0, 4092) == 1023
+    assert lib.lsm_max_records(1, 4092) == 511
+    assert lib.lsm_max_records(2, 4092) == 341
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_segment_files_matches_oracle(seed):
+    lib = _lib.load()
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(0, 3000))
+    kl = rng.integers(0, 64, n).astype(np.uint64)
+    vl = rng.integers(0, 5000, n).astype(np.uint64)
+    koff = np.zeros(n + 1, np.uint64)
+    voff = np.zeros(n + 1, np.uint64)
+    koff[1:] = np.cumsum(kl)
+    voff[1:] = np.cumsum(vl)
+    for thr in (0, 1, 4096, 65536, 2 * 1024 * 1024):
+        want = ora.segment_files(koff, voff, thr)
+        got = np.zeros(n + 2, np.uint64)
+        nf = lib.lsm_segment_files_host(koff.ctypes.data, voff.ctypes.data, n, thr,
+                                        got.ctypes.data)
+        assert got[: nf + 1].tolist() == want.tolist()
+
+
+def test_image_size_matches_oracle():
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    n = 500
+    koff = np.zeros(n + 1, np.uint64)
+    voff = np.zeros(n + 1, np.uint64)
+    koff[1:] = np.cumsum(rng.integers(0, 40, n))
+    voff[1:] = np.cumsum(rng.integers(0, 300, n))
+    for (r0, r1) in [(0, 0), (0, 1), (3, 77), (0, n)]:
+        for m in (1, 64, 1000, 1_600_000):
+            assert lib.lsm_sst_image_size_host(koff.ctypes.data, voff.ctypes.data, r0, r1, m) == \
+                ora.lib().ora_sst_image_size(koff.ctypes.data, voff.ctypes.data, r0, r1, m)
+    for g in range(3):
+        assert lib.lsm_encoded_size_host(g, koff.ctypes.data, voff.ctypes.data, 5, 300) == \
+            ora.lib().ora_encoded_size(g, koff.ctypes.data, voff.ctypes.data, 5, 300)
+    assert lib.lsm_filter_block_size(1_600_000) == 200_032
+
+
+def test_code_object_is_gfx950():
+    so = os.path.join(ROOT, "go-lsm_amd", "liblsm_gpu.so")
+    blob = open(so, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob

@@ -1,0 +1,269 @@
+"""GPU parity: lsm_decode_blocks vs the CPU restatement (bit-exact).
+
+Translates sstable/block/data_test.go, index_test.go and kv/kv_test.go cases
+into device batches, fuzzes every grammar with corruptions, odd alignments
+and large blocks, and checks BASELINE config 2 / 5 at full size through
+size-independent properties plus a sampled oracle comparison.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+import lsmgpu
+import pyoracle as ora
+from lsmgpu import synth
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = json.load(open(os.path.join(HERE, "golden", "reference_vectors.json")))
+
+
+def dev_batch(ctx, blocks, align_pad=None, rng=None):
+    """Pack byte blocks into one buffer (optionally at odd offsets)."""
+    parts, offs, lens = [], [], []
+    pos = 0
+    for i, b in enumerate(blocks):
+        b = np.frombuffer(bytes(b), np.uint8) if not isinstance(b, np.ndarray) else b
+        gap = 0
+        if align_pad is not None:
+            gap = int(rng.integers(0, align_pad)) if rng is not None else align_pad
+        parts.append(np.zeros(gap, np.uint8))
+        pos += gap
+        offs.append(pos)
+        lens.append(b.size)
+        parts.append(b)
+        pos += b.size
+    buf = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    dev = ctx.torch_device
+    return (buf, lsmgpu.to_device_bytes(buf, dev),
+            torch.tensor(np.array(offs, np.uint64).view(np.int64), device=dev),
+            torch.tensor(np.array(lens, np.uint32).view(np.int32), device=dev))
+
+
+def check_against_oracle(grammar, buf, blk_off, blk_len, r, arena=False):
+    nrec = r.nrec.cpu().numpy()
+    status = r.status.cpu().numpy()
+    rec_base = r.bases(blk_off).astype(np.int64)
+    desc = r.desc_numpy()
+    iv = r.idx_value.cpu().numpy() if r.idx_value is not None else None
+    if arena:
+        ka = r.key_arena.cpu().numpy() if r.key_arena is not None else None
+        va = r.val_arena.cpu().numpy() if r.val_arena is not None else None
+        ab = r.arena_bases(blk_off).astype(np.int64)
+    for b, (o, l) in enumerate(zip(blk_off, blk_len)):
+        st, d, oiv = ora.decode_block(grammar, buf, int(o), int(l))
+        assert status[b] == st, (b, status[b], st)
+        assert nrec[b] == len(d), (b, nrec[b], len(d))
+        got = desc[rec_base[b]:rec_base[b] + nrec[b]]
+        assert np.array_equal(got, d), b
+        if grammar == lsmgpu.GRAMMAR_IDX:
+            assert np.array_equal(iv[rec_base[b]:rec_base[b] + nrec[b]], oiv), b
+        if arena:
+            ok, ov = ora.materialize(grammar, buf, d)
+            if ka is not None:
+                assert ka[ab[b]:ab[b] + ok.size].tobytes() == ok.tobytes(), b
+            if va is not None:
+                assert va[ab[b]:ab[b] + ov.size].tobytes() == ov.tobytes(), b
+
+
+def run(ctx, grammar, blocks, arena=False, align_pad=None, seed=0, placement="plan"):
+    rng = np.random.default_rng(seed)
+    buf, d_in, d_off, d_len = dev_batch(ctx, blocks, align_pad=align_pad, rng=rng)
+    r = lsmgpu.decode_blocks(ctx, grammar, d_in, d_off, d_len, arena=arena, arena_offsets=arena,
+                             placement=placement)
+    torch.cuda.synchronize()
+    check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
+                         d_len.cpu().numpy().view(np.uint32), r, arena=arena)
+    return r
+
+
+def v_block(values):
+    return b"".join(struct.pack("<I", len(v)) + v for v in values)
+
+
+def kv_block(pairs):
+    return b"".join(struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v for k, v in pairs)
+
+
+def idx_block(entries):
+    return b"".join(struct.pack("<I", len(k)) + k + struct.pack("<q", o) for k, o in entries)
+
+
+# ---- reference test vectors as device batches ---------------------------------
+
+def test_data_test_vectors(ctx):
+    blocks = []
+    for case in REF["data_block_roundtrip"]:
+        b = v_block([e.encode() for e in case["entries"]])
+        n = len(b) if case["size"] <= 0 else min(case["size"], len(b))
+        blocks.append(b[:n])
+    sl = REF["data_block_size_limit"]
+    full = v_block([e.encode() for e in sl["entries"]])
+    blocks.append(full[:sl["insufficient"]["size"]])
+    blocks.append(full[:sl["partial"]["size"]])
+    for case in REF["data_block_corrupt"]:
+        blocks.append(bytes.fromhex(case["bytes"]))
+    r = run(ctx, lsmgpu.GRAMMAR_V, blocks)
+    st = r.status.cpu().numpy()
+    assert list(st[:5]) == [0] * 5 and st[5] != 0 and st[6] == 0 and st[7] != 0 and st[8] != 0
+    assert list(r.nrec.cpu().numpy()[:7]) == [0, 1, 3, 2, 2, 0, 2]
+
+
+def test_kv_test_vectors(ctx):
+    pairs = [(bytes.fromhex(c["key"]), bytes.fromhex(c["value"])) for c in REF["kv_pairs"]]
+    blocks = [kv_block([p]) for p in pairs] + [kv_block(pairs)]
+    r = run(ctx, lsmgpu.GRAMMAR_KV, blocks, arena=True)
+    assert list(r.nrec.cpu().numpy()) == [1] * len(pairs) + [len(pairs)]
+
+
+def test_index_test_vectors(ctx):
+    ib = REF["index_block"]
+    ent = [(k.encode(), o) for k, o in ib["entries"]]
+    full = idx_block(ent)
+    two = idx_block(ent[:2])
+    f = ib["partial_size_first_entry"]
+    blocks = [full, two[:f], two[: f - ib["truncate_by"]], b""]
+    for case in REF["index_entry_encode"]:
+        blocks.append(bytes.fromhex(case["bytes"]))
+    r = run(ctx, lsmgpu.GRAMMAR_IDX, blocks)
+    assert list(r.nrec.cpu().numpy()) == [3, 1, 0, 0, 1, 1]
+    assert list(r.idx_value.cpu().numpy()[r.rec_base.cpu().numpy()[0]:][:3]) == [100, 200, 300]
+
+
+# ---- fuzz ---------------------------------------------------------------------------
+
+def rand_records(rng, grammar, n, kmax=40, vmax=300):
+    out = []
+    for _ in range(n):
+        k = rng.integers(0, 256, int(rng.integers(0, kmax + 1)), dtype=np.uint8).tobytes()
+        v = rng.integers(0, 256, int(rng.integers(0, vmax + 1)), dtype=np.uint8).tobytes()
+        if grammar == 0:
+            out.append(struct.pack("<I", len(v)) + v)
+        elif grammar == 1:
+            out.append(struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v)
+        else:
+            out.append(struct.pack("<I", len(k)) + k + struct.pack("<q", int(rng.integers(-2**62, 2**62))))
+    return b"".join(out)
+
+
+def corrupt(rng, b):
+    kind = int(rng.integers(0, 6))
+    if kind == 0 or len(b) == 0:
+        return b
+    if kind == 1:  # truncate anywhere
+        return b[: int(rng.integers(0, len(b)))]
+    if kind == 2:  # trailing 1-3 bytes
+        return b + bytes(int(rng.integers(1, 4)))
+    if kind == 3:  # giant length somewhere at a record start (first 4 bytes)
+        return struct.pack("<I", int(rng.choice([2**20 + 1, 2**30 + 1, 2**32 - 1, 999999]))) + b[4:]
+    if kind == 4:  # random bytes
+        return rng.integers(0, 256, len(b), dtype=np.uint8).tobytes()
+    return b[: len(b) // 2] + bytes(3)
+
+
+@pytest.mark.parametrize("grammar", [0, 1, 2])
+@pytest.mark.parametrize("arena", [False, True])
+@pytest.mark.parametrize("placement", ["plan", "offset"])
+def test_fuzz_small_blocks(ctx, grammar, arena, placement):
+    rng = np.random.default_rng(100 + grammar * 2 + arena)
+    blocks = []
+    for i in range(300):
+        b = rand_records(rng, grammar, int(rng.integers(0, 40)), kmax=24, vmax=120)
+        blocks.append(corrupt(rng, b))
+    run(ctx, grammar, blocks, arena=arena, align_pad=19, seed=grammar, placement=placement)
+
+
+@pytest.mark.parametrize("grammar", [0, 1, 2])
+def test_large_and_many_record_blocks(ctx, grammar):
+    rng = np.random.default_rng(7 + grammar)
+    blocks = [
+        rand_records(rng, grammar, 1500, kmax=8, vmax=8),        # thousands of tiny records
+        rand_records(rng, grammar, 40, kmax=64, vmax=4000),      # 64 KiB-ish, long values
+        rand_records(rng, grammar, 300, kmax=40, vmax=1500),     # ~200 KiB
+        rand_records(rng, grammar, 5, kmax=2000, vmax=20000),    # values larger than the ring
+        b"",
+    ]
+    blocks.append(corrupt(rng, blocks[1]))
+    run(ctx, grammar, blocks, arena=True, align_pad=13, seed=3)
+    run(ctx, grammar, blocks, arena=True, align_pad=13, seed=3, placement="offset")
+
+
+def test_capacity_status(ctx):
+    # A caller-provided rec_base with too little room: LSM_ST_CAPACITY, nrec = cap.
+    b = kv_block([(b"k%d" % i, b"v" * i) for i in range(10)])
+    buf, d_in, d_off, d_len = dev_batch(ctx, [b, b])
+    p = lsmgpu.plan(ctx, lsmgpu.GRAMMAR_KV, d_len)
+    p.rec_base.copy_(torch.tensor([0, 4, 14], device=ctx.torch_device))
+    r = lsmgpu.alloc_decode(ctx, lsmgpu.GRAMMAR_KV, 2, p)
+    lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r)
+    assert r.status.cpu().tolist() == [8, 0]
+    assert r.nrec.cpu().tolist() == [4, 10]
+
+
+def test_plan_matches_host(ctx):
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 70000, 10000).astype(np.uint32)
+    d_len = torch.tensor(lens.view(np.int32), device=ctx.torch_device)
+    for g, div in ((0, 4), (1, 8), (2, 12)):
+        p = lsmgpu.plan(ctx, g, d_len, arena=True)
+        want = np.zeros(lens.size + 1, np.uint64)
+        want[1:] = np.cumsum(lens // div)
+        assert np.array_equal(p.rec_base.cpu().numpy().view(np.uint64), want)
+        wa = np.zeros(lens.size + 1, np.uint64)
+        wa[1:] = np.cumsum(lens.astype(np.uint64))
+        assert np.array_equal(p.arena_base.cpu().numpy().view(np.uint64), wa)
+
+
+# ---- BASELINE configs at full size ----------------------------------------------------
+
+def test_config2_full_size(ctx):
+    """100k x 4 KiB KV blocks (16 B keys / 100 B values): every descriptor is
+    closed-form; a sample of blocks is compared with the oracle, and the
+    materialized arenas checksum against the generator's columns."""
+    nblk = 100_000
+    buf, blk_off, blk_len = synth.uniform_kv_blocks(np.arange(nblk))
+    dev = ctx.torch_device
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.tensor(blk_off.view(np.int64), device=dev)
+    d_len = torch.tensor(blk_len.view(np.int32), device=dev)
+    r = lsmgpu.decode_blocks(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, arena=True)
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0
+    assert bool((r.nrec == 33).all())
+    rb = r.rec_base.cpu().numpy()
+    assert np.array_equal(rb, np.arange(nblk + 1) * 511)
+    desc = r.desc.view(-1, 4)
+    idx = (torch.arange(nblk, device=dev)[:, None] * 511 + torch.arange(33, device=dev)[None, :]).reshape(-1)
+    d = desc[idx].cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+    want_off = (np.arange(nblk)[:, None] * 4096 + np.arange(33)[None, :] * 124).reshape(-1)
+    assert np.array_equal(d["rec_off"], want_off.astype(np.uint64))
+    assert (d["key_len"] == 16).all() and (d["val_len"] == 100).all()
+    # arenas: block b's keys are packed at arena_base[b] = 4092*b
+    ka = r.key_arena[: nblk * 4092].view(nblk, 4092)[:, : 33 * 16].cpu().numpy()
+    va = r.val_arena[: nblk * 4092].view(nblk, 4092)[:, : 33 * 100].cpu().numpy()
+    keys, _, vals, _ = synth.kv_stream(nblk * 33)
+    assert np.array_equal(ka.reshape(-1), keys)
+    assert np.array_equal(va.reshape(-1), vals)
+    # oracle on a sample of blocks
+    sample = np.random.default_rng(0).choice(nblk, 64, replace=False)
+    for b in sample:
+        st, od, _ = ora.decode_block(1, buf, int(blk_off[b]), int(blk_len[b]))
+        assert st == 0 and np.array_equal(d[b * 33:(b + 1) * 33], od)
+
+
+def test_config5_mixed_sample(ctx):
+    buf, blk_off, blk_len, nrec = synth.mixed_kv_blocks(24 << 20, seed=11)
+    dev = ctx.torch_device
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.tensor(blk_off.view(np.int64), device=dev)
+    d_len = torch.tensor(blk_len.view(np.int32), device=dev)
+    r = lsmgpu.decode_blocks(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, arena=True)
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0
+    assert np.array_equal(r.nrec.cpu().numpy(), nrec)
+    check_against_oracle(lsmgpu.GRAMMAR_KV, buf, blk_off, blk_len, r, arena=True)
