@@ -35,3 +35,90 @@ extern "C" int lsm_ctx_destroy(lsm_ctx *ctx) {
 }
 
 extern "C" int lsm_ctx_num_cus(const lsm_ctx *ctx) { return ctx ? ctx->num_cus : 0; }
+
+static int bind(lsm_ctx *ctx) {
+    if (!ctx) return LSM_EINVAL;
+    LSM_HIP_CHECK(hipSetDevice(ctx->device));
+    return 0;
+}
+
+extern "C" int lsm_dev_alloc(lsm_ctx *ctx, size_t bytes, void **out) {
+    if (!out) return LSM_EINVAL;
+    *out = nullptr;
+    int rc = bind(ctx);
+    if (rc) return rc;
+    size_t n = ((bytes + 15) & ~(size_t)15) + 16;
+    LSM_HIP_CHECK(hipMalloc(out, n));
+    return 0;
+}
+
+extern "C" int lsm_dev_free(lsm_ctx *ctx, void *p) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (p) LSM_HIP_CHECK(hipFree(p));
+    return 0;
+}
+
+extern "C" int lsm_host_alloc_pinned(lsm_ctx *ctx, size_t bytes, void **out) {
+    if (!out) return LSM_EINVAL;
+    *out = nullptr;
+    int rc = bind(ctx);
+    if (rc) return rc;
+    LSM_HIP_CHECK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return 0;
+}
+
+extern "C" int lsm_host_free_pinned(lsm_ctx *ctx, void *p) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (p) LSM_HIP_CHECK(hipHostFree(p));
+    return 0;
+}
+
+extern "C" int lsm_memcpy_h2d(lsm_ctx *ctx, void *d_dst, const void *h_src, size_t bytes,
+                              void *stream) {
+    if (!ctx || (bytes && (!d_dst || !h_src))) return LSM_EINVAL;
+    if (!bytes) return 0;
+    LSM_HIP_CHECK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice,
+                                 static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+extern "C" int lsm_memcpy_d2h(lsm_ctx *ctx, void *h_dst, const void *d_src, size_t bytes,
+                              void *stream) {
+    if (!ctx || (bytes && (!d_src || !h_dst))) return LSM_EINVAL;
+    if (!bytes) return 0;
+    LSM_HIP_CHECK(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost,
+                                 static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+extern "C" int lsm_memset_dev(lsm_ctx *ctx, void *d_dst, int value, size_t bytes, void *stream) {
+    if (!ctx || (bytes && !d_dst)) return LSM_EINVAL;
+    if (!bytes) return 0;
+    LSM_HIP_CHECK(hipMemsetAsync(d_dst, value, bytes, static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+extern "C" int lsm_stream_create(lsm_ctx *ctx, void **out) {
+    if (!out) return LSM_EINVAL;
+    int rc = bind(ctx);
+    if (rc) return rc;
+    hipStream_t s;
+    LSM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = s;
+    return 0;
+}
+
+extern "C" int lsm_stream_destroy(lsm_ctx *ctx, void *stream) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (stream) LSM_HIP_CHECK(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+extern "C" int lsm_stream_sync(lsm_ctx *ctx, void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    LSM_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return 0;
+}

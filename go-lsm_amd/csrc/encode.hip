@@ -201,6 +201,7 @@ struct BloomArgs {
     uint64_t slice_bits;   // multiple of 64
     uint64_t nwords;       // ceil(m/64)
     uint64_t *bitmap;      // nfile * nwords native u64 words
+    uint64_t nkeys;        // keys of the single filter when file_start == null
 };
 
 __global__ __launch_bounds__(1024) void bloom_slices_kernel(BloomArgs a) {
@@ -212,7 +213,8 @@ __global__ __launch_bounds__(1024) void bloom_slices_kernel(BloomArgs a) {
     const uint32_t nw32 = (uint32_t)((hi - lo + 63) / 64) * 2;
     for (uint32_t i = threadIdx.x; i < nw32; i += blockDim.x) lds_bits[i] = 0;
     __syncthreads();
-    const uint64_t s = a.file_start[f], e = a.file_start[f + 1];
+    const uint64_t s = a.file_start ? a.file_start[f] : 0;
+    const uint64_t e = a.file_start ? a.file_start[f + 1] : a.nkeys;
     for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
         uint64_t k0 = a.koff[i];
         uint64_t h[4];
@@ -526,6 +528,7 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
     b.slice_bits = slice_bits_for(m);
     b.nwords = nwords;
     b.bitmap = static_cast<uint64_t *>(d_workspace);
+    b.nkeys = 0;
     const uint32_t nslices = (uint32_t)((m + b.slice_bits - 1) / b.slice_bits);
     const size_t lds = (size_t)(b.slice_bits / 8);
     hipLaunchKernelGGL(bloom_slices_kernel, dim3(nfile, nslices), dim3(1024), lds, s, b);
@@ -582,6 +585,29 @@ extern "C" int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     uint32_t grid = (uint32_t)((nkeys + 255) / 256);
     hipLaunchKernelGGL(sum256_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
                        d_keys, d_koff, nkeys, d_h);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_bloom_build(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                               uint64_t nkeys, uint64_t m, uint32_t k, uint64_t *d_words,
+                               void *stream) {
+    if (!ctx || m == 0 || m >= (1ull << 63) || !d_words) return LSM_EINVAL;
+    if (nkeys && (!d_keys || !d_koff)) return LSM_EINVAL;
+    BloomArgs b;
+    b.keys = d_keys;
+    b.koff = d_koff;
+    b.file_start = nullptr;
+    b.m = m;
+    b.mrecip = barrett_recip(m);
+    b.k = k ? k : 1;
+    b.slice_bits = slice_bits_for(m);
+    b.nwords = (m + 63) / 64;
+    b.bitmap = d_words;
+    b.nkeys = nkeys;
+    const uint32_t nslices = (uint32_t)((m + b.slice_bits - 1) / b.slice_bits);
+    hipLaunchKernelGGL(bloom_slices_kernel, dim3(1, nslices), dim3(1024),
+                       (size_t)(b.slice_bits / 8), static_cast<hipStream_t>(stream), b);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -66,6 +66,24 @@ SIGNATURES = {
                                        c_u8p, c_u64p, ctypes.c_uint64, c_u8p, ctypes.c_void_p]),
     "lsm_sum256": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_uint64, c_u64p,
                                   ctypes.c_void_p]),
+    "lsm_bloom_build": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_uint64,
+                                       ctypes.c_uint64, ctypes.c_uint32, c_u64p,
+                                       ctypes.c_void_p]),
+    "lsm_dev_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_void_p)]),
+    "lsm_dev_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "lsm_host_alloc_pinned": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "lsm_host_free_pinned": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "lsm_memcpy_h2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_memcpy_d2h": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_memset_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_stream_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "lsm_stream_destroy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "lsm_stream_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -103,6 +103,22 @@ int lsm_ctx_destroy(lsm_ctx *ctx);
 /* Number of compute units of the context's device (grid sizing). */
 int lsm_ctx_num_cus(const lsm_ctx *ctx);
 
+/* ---- memory / stream plumbing (so a cgo or C++ host needs no HIP headers) -- */
+
+/* Device allocation, rounded up to 16 bytes plus 16 bytes of slack (the
+ * readability contract above).  Not for use inside a timed/captured region. */
+int lsm_dev_alloc(lsm_ctx *ctx, size_t bytes, void **out);
+int lsm_dev_free(lsm_ctx *ctx, void *p);
+/* Pinned (page-locked) host memory for asynchronous H2D/D2H staging. */
+int lsm_host_alloc_pinned(lsm_ctx *ctx, size_t bytes, void **out);
+int lsm_host_free_pinned(lsm_ctx *ctx, void *p);
+int lsm_memcpy_h2d(lsm_ctx *ctx, void *d_dst, const void *h_src, size_t bytes, void *stream);
+int lsm_memcpy_d2h(lsm_ctx *ctx, void *h_dst, const void *d_src, size_t bytes, void *stream);
+int lsm_memset_dev(lsm_ctx *ctx, void *d_dst, int value, size_t bytes, void *stream);
+int lsm_stream_create(lsm_ctx *ctx, void **out);
+int lsm_stream_destroy(lsm_ctx *ctx, void *stream);
+int lsm_stream_sync(lsm_ctx *ctx, void *stream);
+
 /* ---- planning ------------------------------------------------------------ */
 
 /* Largest record count a block of `len` bytes can hold: KV len/8, V len/4,
@@ -179,6 +195,11 @@ int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
                   void *d_workspace, size_t ws_bytes, void *stream);
 
 /* ---- bloom probe (verification side, Filter.Test bloom.go:371-379) ------- */
+
+/* Standalone bloom build: Filter.Add of every key (bloom.go:175-181) into
+ * d_words (ceil(m/64) native u64 words, zeroed by the call). */
+int lsm_bloom_build(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
+                    uint64_t m, uint32_t k, uint64_t *d_words, void *stream);
 
 /* d_hit[i] = Filter.Test(key i) against the filter words of one .sst
  * (native u64 words, bit p -> word p>>6 bit p&63). */
