@@ -2,17 +2,19 @@
 //
 // One wavefront owns one block (go-lsm's blocks are independent units; the
 // parallelism is across blocks).  The block is streamed into a
-// 4 KiB per-wave LDS ring in 1 KiB chunks (one coalesced 16 B/lane buffer
-// load each, range-checked so a block never reads past its padded end).  The
+// 4 KiB per-wave LDS ring in 1 KiB chunks (one coalesced 16 B/lane LDS-DMA
+// buffer load each, range-checked so a block never reads past its padded end).  The
 // record boundaries are a dependent chain (each record's position depends on
 // every earlier length, data.go:58-76), so the wave chases them with a
-// wave-uniform cursor: each step reads a 64-position window (lane j holds the
-// u32 at cursor+j, two ds_read_b32 + v_alignbyte) and resolves every length
-// field inside the window with v_readlane, i.e. one LDS round trip per
-// window instead of one per field.  Thirty-two waves per CU chase
+// wave-uniform cursor: a window read (one ds_read_b128 per lane) exposes 1 KiB
+// of the block across the wave's registers, and every length field inside it
+// is two v_readlane plus a scalar funnel shift, i.e. one LDS round trip per
+// 1 KiB instead of one per field.  Thirty-two waves per CU chase
 // concurrently, which hides the LDS latency of the chain behind the HBM
 // stream.  Decoded records are staged one per lane and written as coalesced
 // 16-byte descriptors every 64 records.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace lsm {
@@ -23,7 +25,6 @@ constexpr uint32_t kRingBytes = 4096;
 constexpr uint32_t kRingWords = kRingBytes / 4;
 constexpr uint32_t kChunk = 1024;  // one b128 wave-load
 constexpr uint32_t kNChunk = kRingBytes / kChunk;
-constexpr uint32_t kWindow = 64;   // positions per window read
 
 struct DecodeArgs {
     const uint8_t *in;
@@ -44,15 +45,22 @@ struct DecodeArgs {
 
 // Streams one block through this wave's LDS ring and serves u32 length
 // fields at wave-uniform block positions.
+//
+// Ring: 4 x 1 KiB chunks, filled by LDS-DMA (buffer_load_dwordx4 ... lds:
+// no VGPR staging, one s_waitcnt for all chunks of a refill).  Window: each
+// lane holds 16 raw bytes of a 1 KiB, 16-byte aligned slice of the stream
+// (one ds_read_b128); a field at stream byte s is two v_readlane of the
+// lanes/dwords covering [s, s+4) plus a scalar funnel shift.  A 4 KiB block
+// costs ~5 LDS round trips instead of one per record.
 struct BlockReader {
     uint32_t *ring;
     rsrc_t rsrc;
     uint32_t h;        // block start inside its first 16-byte line
     uint32_t total;    // loadable stream bytes: round_up16(h + n)
     uint32_t nchunks;  // chunks covering [0, total)
-    uint32_t hi_c;     // chunks [.., hi_c) have been issued into the ring
-    uint32_t wbase;    // window base (block position)
-    uint32_t win;      // lane j: u32 at block position wbase + j
+    uint32_t hi_c;     // chunks [.., hi_c) have been loaded into the ring
+    uint32_t wb;       // window base (stream byte, 16-aligned)
+    u32x4 raw;         // lane j: stream bytes [wb + 16j, wb + 16j + 16)
     bool have_win;
 
     __device__ void init(uint32_t *ring_, const uint8_t *in, uint64_t off, uint32_t n) {
@@ -65,59 +73,64 @@ struct BlockReader {
         rsrc = make_rsrc(in + a0, total);
         hi_c = 0;
         have_win = false;
-        wbase = 0;
-        win = 0;
+        wb = 0;
     }
 
-    // Make stream bytes [h+p, h+p+68) resident (clamped to the block).
-    __device__ __forceinline__ void ensure(uint32_t p) {
-        uint32_t s0 = h + p;
-        uint32_t need_end = s0 + kWindow + 4;
+    // Make stream bytes [s0, s0 + kChunk) resident (clamped to the block),
+    // loading every missing chunk up to 3 chunks past s0's chunk.
+    __device__ __forceinline__ void ensure(uint32_t s0) {
+        uint32_t need_end = s0 + kChunk;
         if (need_end > total) need_end = total;
-        uint32_t need_hi = (need_end + kChunk - 1) / kChunk;
+        const uint32_t need_hi = (need_end + kChunk - 1) / kChunk;
         if (need_hi <= hi_c) return;
-        uint32_t c0 = s0 / kChunk;
-        uint32_t first = hi_c > c0 ? hi_c : c0;
+        const uint32_t c0 = s0 / kChunk;
+        const uint32_t first = hi_c > c0 ? hi_c : c0;
         uint32_t last = c0 + kNChunk;
         if (last > nchunks) last = nchunks;
-        uint32_t lane = lane_id();
-        u32x4 v[kNChunk];
+        const uint32_t voff = lane_id() * 16;
 #pragma unroll
         for (uint32_t i = 0; i < kNChunk; i++) {
-            if (first + i < last) v[i] = ld_b128(rsrc, (first + i) * kChunk + lane * 16);
-        }
-#pragma unroll
-        for (uint32_t i = 0; i < kNChunk; i++) {
-            uint32_t c = first + i;
-            if (c < last) {
-                uint32_t w = ((c % kNChunk) * kChunk + lane * 16) / 4;
-                *reinterpret_cast<u32x4 *>(&ring[w]) = v[i];
-            }
+            const uint32_t c = first + i;
+            if (c < last)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsrc, (__attribute__((address_space(3))) void *)&ring[(c % kNChunk) * (kChunk / 4)],
+                    16, voff + c * kChunk, 0, 0, 0);
         }
         hi_c = last;
-        // LDS ops of one wave execute in order; this only stops hipcc from
-        // moving the window reads above the ring writes.
-        __builtin_amdgcn_wave_barrier();
-        __asm__ __volatile__("" ::: "memory");
+        // The DMA writes are invisible to the compiler's waitcnt tracking of
+        // ds_read; wait for them explicitly before the window read.
+        __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
-    __device__ __forceinline__ void load_window(uint32_t p) {
-        uint32_t s = h + p + lane_id();
-        uint32_t w = s >> 2;
-        uint32_t x0 = ring[w % kRingWords];
-        uint32_t x1 = ring[(w + 1) % kRingWords];
-        win = funnel(x0, x1, s);
-        wbase = p;
+    __device__ __forceinline__ void load_window(uint32_t s) {
+        wb = s & ~15u;
+        ensure(wb);
+        const uint32_t w = ((wb + lane_id() * 16) % kRingBytes) / 4;
+        raw = *reinterpret_cast<const u32x4 *>(&ring[w]);
         have_win = true;
+    }
+
+    // Dword d of lane l of the window (d, l wave-uniform).
+    __device__ __forceinline__ uint32_t pick(uint32_t d, uint32_t l) const {
+        uint32_t v0 = __builtin_amdgcn_readlane(raw.x, l);
+        uint32_t v1 = __builtin_amdgcn_readlane(raw.y, l);
+        uint32_t v2 = __builtin_amdgcn_readlane(raw.z, l);
+        uint32_t v3 = __builtin_amdgcn_readlane(raw.w, l);
+        return d == 0 ? v0 : d == 1 ? v1 : d == 2 ? v2 : v3;
     }
 
     // Little-endian u32 at block position p (wave-uniform).
     __device__ __forceinline__ uint32_t field(uint32_t p) {
-        if (!have_win || p - wbase >= kWindow) {
-            ensure(p);
-            load_window(p);
+        const uint32_t s = h + p;
+        if (!have_win || s - wb > kChunk - 4) load_window(s);
+        const uint32_t o = s - wb;
+        const uint32_t l = o >> 4, d = (o >> 2) & 3, sh = o & 3;
+        uint32_t lo = pick(d, l);
+        if (sh) {
+            const uint32_t hi = pick((d + 1) & 3, l + (d == 3));
+            lo = (lo >> (8 * sh)) | (hi << (32 - 8 * sh));
         }
-        return __builtin_amdgcn_readlane(win, p - wbase);
+        return lo;
     }
 };
 
@@ -155,30 +168,39 @@ __device__ __forceinline__ void flush(const DecodeArgs &a, const RecordStage &st
     }
 }
 
-template <int G, bool ARENA>
-__global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
-    const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint32_t b = uni(blockIdx.x * kWavesPerWG + wave);
-    if (b >= a.nblk) return;
+template <int G>
+struct MinRecord { static constexpr uint32_t R = G == LSM_GRAMMAR_V ? 4 : G == LSM_GRAMMAR_KV ? 8 : 12; };
 
-    const uint64_t off = uni64(a.blk_off[b]);
-    const uint32_t n = uni(a.blk_len[b]);
-    // Record slots: CSR rec_base, or offset-addressed (rec_base == NULL):
-    // block b owns slots [off/R, (off+n)/R) with R the grammar's minimum
-    // record size, disjoint for non-overlapping blocks -- no scan needed.
-    constexpr uint32_t R = G == LSM_GRAMMAR_V ? 4 : G == LSM_GRAMMAR_KV ? 8 : 12;
-    uint64_t base, cap;
+// Record slots: CSR rec_base, or offset-addressed (rec_base == NULL): block b
+// owns slots [off/R, (off+n)/R) with R the grammar's minimum record size,
+// disjoint for non-overlapping blocks -- no scan needed.
+template <int G>
+__device__ __forceinline__ void record_slots(const DecodeArgs &a, uint32_t b, uint64_t off,
+                                             uint32_t n, uint64_t &base, uint64_t &cap) {
+    constexpr uint32_t R = MinRecord<G>::R;
     if (a.rec_base) {
-        base = uni64(a.rec_base[b]);
-        cap = uni64(a.rec_base[b + 1]) - base;
+        base = a.rec_base[b];
+        cap = a.rec_base[b + 1] - base;
     } else {
         base = off / R;
         cap = (off + n) / R - base;
     }
+}
+
+// Wave-per-block path: the whole wave chases one block (any size) through a
+// 4 KiB LDS ring with a wave-uniform (scalar) cursor.  Used for ARENA mode and
+// for blocks too large for a lane slot.
+template <int G, bool ARENA>
+__device__ void decode_block_wave(const DecodeArgs &a, uint32_t b, uint32_t *ring) {
+    const uint64_t off = uni64(a.blk_off[b]);
+    const uint32_t n = uni(a.blk_len[b]);
+    uint64_t base, cap;
+    record_slots<G>(a, b, off, n, base, cap);
+    base = uni64(base);
+    cap = uni64(cap);
 
     BlockReader rd;
-    rd.init(ring[wave], a.in, off, n);
+    rd.init(ring, a.in, off, n);
     RecordStage st{};
 
     uint64_t kcur = 0, vcur = 0;
@@ -250,6 +272,150 @@ __global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
         a.nrec[b] = nr;
         a.status[b] = status;
     }
+}
+
+template <int G, bool ARENA>
+__global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
+    const uint32_t wave = uni(threadIdx.x / kWave);
+    const uint32_t b = uni(blockIdx.x * kWavesPerWG + wave);
+    if (b >= a.nblk) return;
+    decode_block_wave<G, ARENA>(a, b, ring[wave]);
+}
+
+// ---- lane-per-block path (DESC mode) ----------------------------------------
+//
+// The record chain is serial inside a block, so a wave-uniform chase is bound
+// by the CU's single scalar unit (~1 instruction/cycle/CU).  Here each lane
+// chases its own block instead: a one-wave workgroup owns kLaneBlocks blocks,
+// LDS-DMAs each (<= 4 KiB + alignment) into a private slot with four
+// coalesced 1 KiB loads, then every lane walks its block's length fields with
+// per-lane unaligned LDS reads (two ds_read_b32 + v_alignbyte per field) and
+// writes its descriptors.  Slots are skewed by 16 bytes so lanes walking
+// identically laid out blocks hit different banks.  Blocks that do not fit a
+// slot are decoded afterwards by the wave path.
+constexpr uint32_t kSlotBytes = 4096;
+constexpr uint32_t kSlotStride = kSlotBytes + 16;
+
+template <int G, uint32_t kLaneBlocks>
+__global__ __launch_bounds__(64) void decode_lanes_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t slots[kLaneBlocks * kSlotStride / 4];
+    const uint32_t lane = lane_id();
+    const uint32_t b0 = blockIdx.x * kLaneBlocks;
+    const uint32_t b = b0 + lane;
+    const bool mine = lane < kLaneBlocks && b < a.nblk;
+    uint64_t off = 0;
+    uint32_t n = 0;
+    if (mine) {
+        off = a.blk_off[b];
+        n = a.blk_len[b];
+    }
+    const uint32_t h = (uint32_t)(off & 15);
+    const bool small = mine && (uint64_t)h + n <= kSlotBytes;
+    const uint64_t small_mask = __ballot(small);
+
+    // Stage every small block into its slot: 4 x 1 KiB LDS-DMA per block.
+    for (uint32_t j = 0; j < kLaneBlocks; j++) {
+        if (!((small_mask >> j) & 1)) continue;
+        const uint64_t offj = uni64(__shfl(off, j, kWave));
+        const uint32_t nj = uni(__shfl(n, j, kWave));
+        const uint64_t a0 = offj & ~(uint64_t)15;
+        const uint32_t tot = (uint32_t)(((offj - a0) + nj + 15) & ~(uint64_t)15);
+        const rsrc_t r = make_rsrc(a.in + a0, tot);
+        const uint32_t nck = (tot + kChunk - 1) / kChunk;
+        for (uint32_t c = 0; c < nck; c++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r, (__attribute__((address_space(3))) void *)&slots[(j * kSlotStride + c * kChunk) / 4],
+                16, c * kChunk + lane * 16, 0, 0, 0);
+    }
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if (small) {
+        // Byte address of this lane's slot; reads past the slot return
+        // another slot's bytes or 0 (LDS bounds) and are never accepted.
+        const uint32_t sbase = lane * kSlotStride + h;
+        auto rd = [&](uint32_t p) -> uint32_t {
+            const uint32_t sb = sbase + p;
+            const uint32_t *w = &slots[sb >> 2];
+            return funnel(w[0], w[1], sb);
+        };
+        uint64_t base, cap;
+        record_slots<G>(a, b, off, n, base, cap);
+        u32x4 *dp = a.desc + base;
+        int64_t *xp = a.idx_value ? a.idx_value + base : nullptr;
+        const uint32_t ncap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
+        uint32_t pos = 0, nr = 0;
+        // Straight-line record step; a failing check ends the lane's loop and
+        // the (rare) status is resolved once afterwards from pos.
+        for (;;) {
+            const uint32_t rem = n - pos;
+            uint32_t klen = 0, vlen, vp = pos, nxt;
+            bool ok;
+            if (G == LSM_GRAMMAR_V) {
+                vlen = rd(pos);
+                ok = (rem >= 4) & (rem - 4 >= vlen);
+                nxt = pos + 4 + vlen;
+            } else if (G == LSM_GRAMMAR_KV) {
+                klen = rd(pos);
+                vp = pos + 4 + klen;
+                vlen = rd(vp);
+                const uint32_t rem2 = n - vp;
+                ok = (rem >= 4) & (klen <= kKeyCap) & (rem - 4 >= klen) & (rem2 >= 4) &
+                     (vlen <= kValCap) & (rem2 - 4 >= vlen);
+                nxt = vp + 4 + vlen;
+            } else {
+                klen = rd(pos);
+                vp = pos + 4 + klen;
+                vlen = 8;
+                ok = (rem >= 12) & (rem - 12 >= klen);
+                nxt = vp + 8;
+            }
+            ok = ok & (nr < ncap);
+            if (!ok) break;
+            const uint64_t ro = off + pos;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = klen;
+            d.w = vlen;
+            dp[nr] = d;
+            if (G == LSM_GRAMMAR_IDX && xp) xp[nr] = (int64_t)((uint64_t)rd(vp + 4) << 32 | rd(vp));
+            nr++;
+            pos = nxt;
+        }
+        // Status of the stop at pos (same precedence as the reference).
+        int32_t status = LSM_OK;
+        const uint32_t rem = n - pos;
+        if (rem != 0) {
+            if (G == LSM_GRAMMAR_V) {
+                status = rem < 4 ? LSM_ST_TRUNC_LEN_PREFIX
+                       : rem - 4 < rd(pos) ? LSM_ST_TRUNC_VAL : LSM_ST_CAPACITY;
+            } else if (G == LSM_GRAMMAR_KV) {
+                if (rem < 4) status = LSM_ST_TRUNC_LEN_PREFIX;
+                else {
+                    const uint32_t klen = rd(pos);
+                    if (klen > kKeyCap) status = LSM_ST_KEY_TOO_LONG;
+                    else if (rem - 4 < klen) status = LSM_ST_TRUNC_KEY;
+                    else {
+                        const uint32_t vp = pos + 4 + klen, rem2 = n - vp;
+                        const uint32_t vlen = rem2 >= 4 ? rd(vp) : 0;
+                        status = rem2 < 4 ? LSM_ST_TRUNC_VLEN
+                               : vlen > kValCap ? LSM_ST_VAL_TOO_LONG
+                               : rem2 - 4 < vlen ? LSM_ST_TRUNC_VAL : LSM_ST_CAPACITY;
+                    }
+                }
+            } else {
+                status = (rem < 12 || rem - 12 < rd(pos)) ? LSM_ST_IDX_OVERRUN : LSM_ST_CAPACITY;
+            }
+        }
+        a.nrec[b] = nr;
+        a.status[b] = status;
+    }
+
+    // Blocks too large for a slot: whole-wave streaming path, slot 0 as ring.
+    const uint64_t big_mask = __ballot(mine && !small);
+    for (uint32_t j = 0; j < kLaneBlocks; j++)
+        if ((big_mask >> j) & 1) decode_block_wave<G, false>(a, b0 + j, slots);
 }
 
 // ---- planning: exclusive scans over per-block quantities -----------------
@@ -349,11 +515,35 @@ int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void
     return 0;
 }
 
+template <int G, uint32_t B>
+int launch_lanes(const DecodeArgs &a, hipStream_t s) {
+    uint32_t grid = (a.nblk + B - 1) / B;
+    hipLaunchKernelGGL((decode_lanes_kernel<G, B>), dim3(grid), dim3(kWave), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 template <int G, bool ARENA>
 int launch_decode(const DecodeArgs &a, hipStream_t s) {
-    uint32_t grid = (a.nblk + kWavesPerWG - 1) / kWavesPerWG;
-    hipLaunchKernelGGL((decode_blocks_kernel<G, ARENA>), dim3(grid), dim3(kWave * kWavesPerWG),
-                       0, s, a);
+    if (!ARENA) {
+        // Blocks per wave (LDS slots): 3 admits 13 one-wave workgroups per CU.
+        static const int lb = [] {
+            const char *e = getenv("LSM_LANE_BLOCKS");
+            return e ? atoi(e) : 3;
+        }();
+        switch (lb) {
+        case 3: return launch_lanes<G, 3>(a, s);
+        case 4: return launch_lanes<G, 4>(a, s);
+        case 8: return launch_lanes<G, 8>(a, s);
+        case 15: return launch_lanes<G, 15>(a, s);
+        case 7: return launch_lanes<G, 7>(a, s);
+        default: return launch_lanes<G, 3>(a, s);
+        }
+    } else {
+        uint32_t grid = (a.nblk + kWavesPerWG - 1) / kWavesPerWG;
+        hipLaunchKernelGGL((decode_blocks_kernel<G, ARENA>), dim3(grid),
+                           dim3(kWave * kWavesPerWG), 0, s, a);
+    }
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }
