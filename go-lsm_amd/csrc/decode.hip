@@ -14,6 +14,7 @@
 // stream.  Decoded records are staged one per lane and written as coalesced
 // 16-byte descriptors every 64 records.
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -274,6 +275,135 @@ __device__ void decode_block_wave(const DecodeArgs &a, uint32_t b, uint32_t *rin
     }
 }
 
+// Speculative parallel runs (DESC mode).  After each exactly-decoded record of
+// size S (key length K, value length V), all 64 lanes test the hypothesis
+// "the next 64 records have the same K and V": lane i reads the length fields
+// at cur + i*S (and cur + i*S + 4 + K) straight from the LDS ring.  The
+// ballot's count of leading successes j is the verified run: records
+// [0, j) sit exactly where predicted (each check reads the record's own
+// fields), so j descriptors are stored coalesced and the cursor jumps j*S.
+// The first mismatching record is re-decoded by the exact scalar step, which
+// also produces the precise error status.  A block of equal-size records
+// (the common LSM case) costs one exact step and one run per 64 records.
+template <int G>
+__device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *ring) {
+    const uint64_t off = uni64(a.blk_off[b]);
+    const uint32_t n = uni(a.blk_len[b]);
+    uint64_t base, cap;
+    record_slots<G>(a, b, off, n, base, cap);
+    base = uni64(base);
+    cap = uni64(cap);
+    const uint32_t lane = lane_id();
+
+    BlockReader rd;
+    rd.init(ring, a.in, off, n);
+    auto lds_u32 = [&](uint32_t p) -> uint32_t {  // per-lane read, block position p
+        const uint32_t sb = rd.h + p;
+        const uint32_t w = sb >> 2;
+        return funnel(ring[w % kRingWords], ring[(w + 1) % kRingWords], sb);
+    };
+
+    uint32_t pos = 0, nr = 0;
+    int32_t status = LSM_OK;
+    for (;;) {
+        // ---- exact step at pos (same checks and order as the reference) ----
+        const uint32_t rem = n - pos;
+        uint32_t klen = 0, vlen = 0, vp = pos;
+        uint64_t xval = 0;
+        if (rem == 0) break;
+        if (rem < 4) {
+            status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
+            break;
+        }
+        if (G == LSM_GRAMMAR_V) {
+            vlen = rd.field(pos);
+            if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
+        } else if (G == LSM_GRAMMAR_KV) {
+            klen = rd.field(pos);
+            if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; break; }
+            if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; break; }
+            vp = pos + 4 + klen;
+            const uint32_t rem2 = n - vp;
+            if (rem2 < 4) { status = LSM_ST_TRUNC_VLEN; break; }
+            vlen = rd.field(vp);
+            if (vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; break; }
+            if (rem2 - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
+        } else {
+            klen = rd.field(pos);
+            if ((uint64_t)rem < 12ull + klen) { status = LSM_ST_IDX_OVERRUN; break; }
+            vp = pos + 4 + klen;
+            xval = (uint64_t)rd.field(vp + 4) << 32 | rd.field(vp);
+            vlen = 8;
+        }
+        if (nr >= cap) { status = LSM_ST_CAPACITY; break; }
+        if (lane == 0) {
+            const uint64_t ro = off + pos;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = klen;
+            d.w = vlen;
+            a.desc[base + nr] = d;
+            if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr] = (int64_t)xval;
+        }
+        nr++;
+        const uint32_t S = G == LSM_GRAMMAR_V ? 4 + vlen : G == LSM_GRAMMAR_KV ? 8 + klen + vlen
+                                                                              : 12 + klen;
+        pos += S;
+
+        // ---- speculative runs of records shaped like the last one ----
+        for (;;) {
+            if (pos >= n) break;
+            rd.ensure(rd.h + pos);
+            uint32_t res = rd.hi_c * kChunk;  // resident stream end
+            if (res > rd.total) res = rd.total;
+            const uint32_t lim = (res - rd.h) < n ? (res - rd.h) : n;
+            const uint64_t pe = (uint64_t)pos + (uint64_t)(lane + 1) * S;  // record end
+            const uint32_t p = pos + lane * S;
+            bool ok = pe <= lim && (uint64_t)nr + lane < cap;
+            uint64_t x = 0;
+            if (ok) {
+                if (G == LSM_GRAMMAR_V) {
+                    ok = lds_u32(p) == vlen;
+                } else if (G == LSM_GRAMMAR_KV) {
+                    ok = (int)(lds_u32(p) == klen) & (int)(lds_u32(p + 4 + klen) == vlen);
+                } else {
+                    ok = lds_u32(p) == klen;
+                    x = (uint64_t)lds_u32(p + 8 + klen) << 32 | lds_u32(p + 4 + klen);
+                }
+            }
+            const uint64_t m = __ballot(ok);
+            const uint32_t j = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+            if (lane < j) {
+                const uint64_t ro = off + p;
+                u32x4 d;
+                d.x = (uint32_t)ro;
+                d.y = (uint32_t)(ro >> 32);
+                d.z = klen;
+                d.w = vlen;
+                a.desc[base + nr + lane] = d;
+                if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + lane] = (int64_t)x;
+            }
+            nr += j;
+            pos += j * S;
+            if (j < 64) break;
+        }
+    }
+    if (lane == 0) {
+        a.nrec[b] = nr;
+        a.status[b] = status;
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void decode_spec_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
+    const uint32_t wave = uni(threadIdx.x / kWave);
+    const uint32_t b = uni(blockIdx.x * kWavesPerWG + wave);
+    if (b >= a.nblk) return;
+    decode_block_spec<G>(a, b, ring[wave]);
+}
+
 template <int G, bool ARENA>
 __global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
@@ -297,9 +427,21 @@ __global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
 constexpr uint32_t kSlotBytes = 4096;
 constexpr uint32_t kSlotStride = kSlotBytes + 16;
 
+#ifdef LSM_STAMPS
+// Diagnostic build only (liblsm_gpu_stamps.so): per-workgroup s_memrealtime
+// stamps {start, DMA landed, chase done, end} into a buffer of their own.
+__device__ uint64_t *g_stamps;
+__device__ __forceinline__ void stamp(uint32_t k) {
+    if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
+#else
+__device__ __forceinline__ void stamp(uint32_t) {}
+#endif
+
 template <int G, uint32_t kLaneBlocks>
 __global__ __launch_bounds__(64) void decode_lanes_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t slots[kLaneBlocks * kSlotStride / 4];
+    stamp(0);
     const uint32_t lane = lane_id();
     const uint32_t b0 = blockIdx.x * kLaneBlocks;
     const uint32_t b = b0 + lane;
@@ -329,6 +471,7 @@ __global__ __launch_bounds__(64) void decode_lanes_kernel(DecodeArgs a) {
                 16, c * kChunk + lane * 16, 0, 0, 0);
     }
     __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(1);
 
     if (small) {
         // Byte address of this lane's slot; reads past the slot return
@@ -412,10 +555,12 @@ __global__ __launch_bounds__(64) void decode_lanes_kernel(DecodeArgs a) {
         a.status[b] = status;
     }
 
+    stamp(2);
     // Blocks too large for a slot: whole-wave streaming path, slot 0 as ring.
     const uint64_t big_mask = __ballot(mine && !small);
     for (uint32_t j = 0; j < kLaneBlocks; j++)
         if ((big_mask >> j) & 1) decode_block_wave<G, false>(a, b0 + j, slots);
+    stamp(3);
 }
 
 // ---- planning: exclusive scans over per-block quantities -----------------
@@ -515,6 +660,144 @@ int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void
     return 0;
 }
 
+// ---- streaming lane-per-block path (DESC mode, default) ------------------
+//
+// Each lane owns one block of any size and chases it through a per-wave LDS
+// ring of W rows; row r holds stream bytes [16r, 16r+16) of every lane's own
+// block, gathered by ONE global_load_lds_dwordx4 per row (per-lane source
+// address, lane L's 16 bytes land at row + 16L).  A round refills rows
+// [r_lo, r_lo + W) (r_lo = the lowest row any lane still needs), waits once,
+// then every lane consumes as many length fields as the window holds.  The
+// chase is a field-granular state machine so one long key never stalls the
+// window, and rows that every lane has jumped over are never loaded.
+template <int G, uint32_t BL, uint32_t W>
+__global__ __launch_bounds__(64) void decode_stream_kernel(DecodeArgs a) {
+    constexpr uint32_t kRow = BL * 16;  // bytes per ring row
+    __shared__ __attribute__((aligned(16))) uint32_t ring[W * kRow / 4];
+    stamp(0);
+    const uint32_t lane = lane_id();
+    const uint32_t b = blockIdx.x * BL + lane;
+    const bool mine = lane < BL && b < a.nblk;
+    uint64_t off = 0;
+    uint32_t n = 0;
+    if (mine) {
+        off = a.blk_off[b];
+        n = a.blk_len[b];
+    }
+    const uint64_t a0 = off & ~(uint64_t)15;
+    const uint32_t h = (uint32_t)(off - a0);
+    const uint8_t *g = a.in + a0;
+    const uint32_t rows = (uint32_t)(((uint64_t)h + n + 15) / 16);
+    uint64_t base = 0, cap = 0;
+    if (mine) record_slots<G>(a, b, off, n, base, cap);
+    u32x4 *dp = a.desc + base;
+    int64_t *xp = (G == LSM_GRAMMAR_IDX && a.idx_value) ? a.idx_value + base : nullptr;
+    const uint32_t ncap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
+
+    const uint32_t lane_w = lane * 4;  // this lane's dword inside a row
+    auto dword = [&](uint32_t i) -> uint32_t {  // stream dword i of this lane
+        return ring[((i >> 2) % W) * (kRow / 4) + lane_w + (i & 3)];
+    };
+
+    bool active = mine;
+    int32_t status = LSM_OK;
+    uint32_t pos = 0, vp = 0, klen = 0, phase = 0, nr = 0;
+    uint32_t r_lo = 0, r_loaded = 0;
+    for (;;) {
+        // Refill rows [max(r_loaded, r_lo), r_lo + W): one gather per row.
+        const uint32_t r1 = r_lo + W;
+        for (uint32_t r = r_loaded > r_lo ? r_loaded : r_lo; r < r1; r++) {
+            if (active && r < rows)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(g + 16 * (uint64_t)r),
+                    (__attribute__((address_space(3))) void *)&ring[(r % W) * (kRow / 4)], 16, 0, 0);
+        }
+        r_loaded = r1;
+        __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t win_end = 16 * r1;
+
+        // Consume every field the window holds.
+        while (active) {
+            const uint32_t fp = phase ? vp : pos;
+            const uint32_t rem = n - fp;
+            if (phase == 0 && rem == 0) { active = false; break; }  // clean end
+            const uint32_t need = (G == LSM_GRAMMAR_IDX && phase) ? 8 : 4;
+            if (rem < need) {
+                status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN
+                       : phase ? LSM_ST_TRUNC_VLEN : LSM_ST_TRUNC_LEN_PREFIX;
+                active = false;
+                break;
+            }
+            const uint32_t sb = h + fp;
+            if (sb + need > win_end) break;  // next round
+            const uint32_t i = sb >> 2;
+            const uint32_t d0 = dword(i), d1 = dword(i + 1);
+            const uint32_t f = funnel(d0, d1, sb);
+            if (phase == 0 && G != LSM_GRAMMAR_V) {
+                klen = f;
+                if (G == LSM_GRAMMAR_KV) {
+                    if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; active = false; break; }
+                    if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; active = false; break; }
+                } else if ((uint64_t)rem < 12ull + klen) {
+                    status = LSM_ST_IDX_OVERRUN;
+                    active = false;
+                    break;
+                }
+                vp = pos + 4 + klen;
+                phase = 1;
+                continue;
+            }
+            // value length (V, KV) or index offset (IDX): the record is complete
+            uint32_t vlen;
+            uint64_t xval = 0;
+            if (G == LSM_GRAMMAR_IDX) {
+                xval = (uint64_t)funnel(d1, dword(i + 2), sb) << 32 | f;
+                vlen = 8;
+            } else {
+                vlen = f;
+                if (G == LSM_GRAMMAR_KV && vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; active = false; break; }
+                if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; active = false; break; }
+            }
+            if (nr >= ncap) { status = LSM_ST_CAPACITY; active = false; break; }
+            const uint64_t ro = off + pos;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = G == LSM_GRAMMAR_V ? 0u : klen;
+            d.w = vlen;
+            dp[nr] = d;
+            if (G == LSM_GRAMMAR_IDX && xp) xp[nr] = (int64_t)xval;
+            nr++;
+            const uint32_t rs = G == LSM_GRAMMAR_V ? pos : vp;
+            pos = G == LSM_GRAMMAR_IDX ? rs + 8 : rs + 4 + vlen;
+            phase = 0;
+        }
+        // Lowest row any lane still needs; all lanes done -> exit.
+        uint32_t need_row = active ? (h + (phase ? vp : pos)) >> 4 : 0xFFFFFFFFu;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(need_row, d, kWave);
+            need_row = o < need_row ? o : need_row;
+        }
+        r_lo = uni(need_row);
+        if (r_lo == 0xFFFFFFFFu) break;
+    }
+    stamp(2);
+    if (mine) {
+        a.nrec[b] = nr;
+        a.status[b] = status;
+    }
+    stamp(3);
+}
+
+template <int G, uint32_t BL, uint32_t W>
+int launch_stream(const DecodeArgs &a, hipStream_t s) {
+    uint32_t grid = (a.nblk + BL - 1) / BL;
+    hipLaunchKernelGGL((decode_stream_kernel<G, BL, W>), dim3(grid), dim3(kWave), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 template <int G, uint32_t B>
 int launch_lanes(const DecodeArgs &a, hipStream_t s) {
     uint32_t grid = (a.nblk + B - 1) / B;
@@ -526,6 +809,33 @@ int launch_lanes(const DecodeArgs &a, hipStream_t s) {
 template <int G, bool ARENA>
 int launch_decode(const DecodeArgs &a, hipStream_t s) {
     if (!ARENA) {
+        // Default: wave-per-block with speculative parallel runs.
+        // LSM_DECODE_KERNEL selects variants for A/B measurement.
+        static const int variant = [] {
+            const char *e = getenv("LSM_DECODE_KERNEL");
+            if (!e) return 0;
+            if (!strcmp(e, "stream64x16")) return 1;
+            if (!strcmp(e, "stream32x64")) return 2;
+            if (!strcmp(e, "stream64x32")) return 3;
+            if (!strcmp(e, "lanes")) return 9;
+            if (!strcmp(e, "stream32x32")) return 4;
+            return 0;
+        }();
+        switch (variant) {
+        case 0: {
+            uint32_t grid = (a.nblk + kWavesPerWG - 1) / kWavesPerWG;
+            hipLaunchKernelGGL((decode_spec_kernel<G>), dim3(grid), dim3(kWave * kWavesPerWG),
+                               0, s, a);
+            LSM_HIP_CHECK(hipGetLastError());
+            return 0;
+        }
+        case 4: return launch_stream<G, 32, 32>(a, s);
+        case 1: return launch_stream<G, 64, 16>(a, s);
+        case 2: return launch_stream<G, 32, 64>(a, s);
+        case 3: return launch_stream<G, 64, 32>(a, s);
+        case 9: break;
+        default: return launch_stream<G, 32, 32>(a, s);
+        }
         // Blocks per wave (LDS slots): 3 admits 13 one-wave workgroups per CU.
         static const int lb = [] {
             const char *e = getenv("LSM_LANE_BLOCKS");
@@ -619,3 +929,10 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
                           : launch_decode<LSM_GRAMMAR_IDX, false>(a, s);
     }
 }
+
+#ifdef LSM_STAMPS
+extern "C" int lsm_debug_set_stamps(void *d_buf) {
+    LSM_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(lsm::g_stamps), &d_buf, sizeof(void *)));
+    return 0;
+}
+#endif
