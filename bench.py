@@ -196,7 +196,7 @@ def bench_decode(args, world, rank, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "decode_blocks_kernel<KV>",
+            "kernel": "decode_spec_kernel<KV>",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

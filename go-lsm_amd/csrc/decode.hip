@@ -26,6 +26,19 @@ constexpr uint32_t kRingBytes = 4096;
 constexpr uint32_t kRingWords = kRingBytes / 4;
 constexpr uint32_t kChunk = 1024;  // one b128 wave-load
 constexpr uint32_t kNChunk = kRingBytes / kChunk;
+constexpr uint32_t kSlotBytes = 4096;              // whole-block LDS slot
+constexpr uint32_t kSlotStride = kSlotBytes + 16;  // skewed: lanes hit different banks
+
+#ifdef LSM_STAMPS
+// Diagnostic build only (liblsm_gpu_stamps.so): per-workgroup s_memrealtime
+// stamps {start, DMA landed, chase done, end} into a buffer of their own.
+__device__ uint64_t *g_stamps;
+__device__ __forceinline__ void stamp(uint32_t k) {
+    if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
+#else
+__device__ __forceinline__ void stamp(uint32_t) {}
+#endif
 
 struct DecodeArgs {
     const uint8_t *in;
@@ -286,9 +299,8 @@ __device__ void decode_block_wave(const DecodeArgs &a, uint32_t b, uint32_t *rin
 // also produces the precise error status.  A block of equal-size records
 // (the common LSM case) costs one exact step and one run per 64 records.
 template <int G>
-__device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *ring) {
-    const uint64_t off = uni64(a.blk_off[b]);
-    const uint32_t n = uni(a.blk_len[b]);
+__device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
+                                  uint32_t n, bool staged = false) {
     uint64_t base, cap;
     record_slots<G>(a, b, off, n, base, cap);
     base = uni64(base);
@@ -297,6 +309,11 @@ __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *rin
 
     BlockReader rd;
     rd.init(ring, a.in, off, n);
+    if (staged) rd.hi_c = rd.nchunks < kNChunk ? rd.nchunks : kNChunk;  // DMA'd and landed
+#ifdef LSM_STAMPS
+    rd.ensure(rd.h);
+    stamp(1);
+#endif
     auto lds_u32 = [&](uint32_t p) -> uint32_t {  // per-lane read, block position p
         const uint32_t sb = rd.h + p;
         const uint32_t w = sb >> 2;
@@ -395,13 +412,297 @@ __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *rin
     }
 }
 
-template <int G>
-__global__ __launch_bounds__(256) void decode_spec_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
+// Each wave decodes K consecutive blocks one after the other; the metadata of
+// all K is fetched up front (one vector load per array), so only the block
+// DMA remains on each block's critical path.
+template <int G, uint32_t K, uint32_t WPG>
+__global__ __launch_bounds__(64 * WPG) void decode_spec_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[WPG][kRingWords];
     const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint32_t b = uni(blockIdx.x * kWavesPerWG + wave);
+    const uint32_t b0 = uni((blockIdx.x * WPG + wave) * K);
+    if (b0 >= a.nblk) return;
+    const uint32_t lane = lane_id();
+    uint64_t moff = 0;
+    uint32_t mlen = 0;
+    if (lane < K && b0 + lane < a.nblk) {
+        moff = a.blk_off[b0 + lane];
+        mlen = a.blk_len[b0 + lane];
+    }
+    stamp(0);
+    for (uint32_t k = 0; k < K; k++) {
+        const uint32_t b = b0 + k;
+        if (b >= a.nblk) break;
+        const uint64_t off = uni64(__builtin_amdgcn_readlane((uint32_t)moff, k) |
+                                   (uint64_t)__builtin_amdgcn_readlane((uint32_t)(moff >> 32), k) << 32);
+        const uint32_t n = __builtin_amdgcn_readlane(mlen, k);
+        decode_block_spec<G>(a, b, ring[wave], off, n);
+    }
+    stamp(3);
+}
+
+// ---- group-per-block speculative path (DESC mode, blocks <= 4 KiB) --------
+//
+// A group of H lanes owns one block (64/H blocks per wave), staged whole in
+// an LDS slot by LDS-DMA.  Every round each lane t of a group reads the
+// length fields at pos + t*S', where S' (and K', V') is the shape of the
+// group's previous record, in one batch of independent LDS reads.  Lane 0's
+// position is always right; its fields are checked exactly (re-reading the
+// value length when its key length differs from K') and give the shape S of
+// the record at pos.  Lane t >= 1 is accepted iff S == S' and its own fields
+// equal (K, V) and the record fits: then the records before it all had shape
+// S and its position was right.  The group's leading run of accepted lanes
+// is emitted (coalesced descriptors) and the cursor jumps.  No scalar chase:
+// the control is per-lane VALU, and uniform blocks need two rounds per
+// group of H records.  Oversized blocks go to the wave path afterwards.
+template <int G, uint32_t H>
+__global__ __launch_bounds__(64) void decode_group_kernel(DecodeArgs a) {
+    constexpr uint32_t NB = kWave / H;  // blocks per wave
+    constexpr uint32_t kStride = kSlotBytes + 16;
+    __shared__ __attribute__((aligned(16))) uint32_t slots[NB * kStride / 4];
+    const uint32_t lane = lane_id();
+    const uint32_t grp = lane / H, t = lane % H;
+    const uint32_t b0 = blockIdx.x * NB;
+    const uint32_t b = b0 + grp;
+    const bool mine = b < a.nblk;
+    uint64_t off = 0;
+    uint32_t n = 0;
+    if (mine) {
+        off = a.blk_off[b];
+        n = a.blk_len[b];
+    }
+    const uint32_t h = (uint32_t)(off & 15);
+    const bool small = mine && (uint64_t)h + n <= kSlotBytes;
+    const uint64_t small_mask = __ballot(small);
+    for (uint32_t j = 0; j < NB; j++) {
+        if (!((small_mask >> (j * H)) & 1)) continue;
+        const uint64_t offj = uni64(__builtin_amdgcn_readlane((uint32_t)off, j * H) |
+                                    (uint64_t)__builtin_amdgcn_readlane((uint32_t)(off >> 32), j * H) << 32);
+        const uint32_t nj = __builtin_amdgcn_readlane(n, j * H);
+        const uint64_t a0 = offj & ~(uint64_t)15;
+        const uint32_t tot = (uint32_t)(((offj - a0) + nj + 15) & ~(uint64_t)15);
+        const rsrc_t r = make_rsrc(a.in + a0, tot);
+        const uint32_t nck = (tot + kChunk - 1) / kChunk;
+        for (uint32_t c = 0; c < nck; c++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r, (__attribute__((address_space(3))) void *)&slots[(j * kStride + c * kChunk) / 4],
+                16, c * kChunk + lane * 16, 0, 0, 0);
+    }
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+
+    const uint32_t sbase = grp * kStride + h;
+    auto rd = [&](uint32_t p) -> uint32_t {
+        const uint32_t sb = sbase + p;
+        const uint32_t *w = &slots[sb >> 2];
+        return funnel(w[0], w[1], sb);
+    };
+    uint64_t base = 0, cap = 0;
+    if (small) record_slots<G>(a, b, off, n, base, cap);
+    const uint32_t ncap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
+    const uint32_t glead = grp * H;  // group's lane 0
+
+    bool live = small;
+    int32_t status = LSM_OK;
+    uint32_t pos = 0, nr = 0;
+    uint32_t Kp = 0xFFFFFFFFu, Sp = 0xFFFFFFFFu;  // previous record's key length and size
+    while (__ballot(live)) {
+        uint32_t acc = 0, K = 0, V = 0, S = 0;
+        uint64_t x = 0;
+        const uint32_t p = pos + t * (Sp == 0xFFFFFFFFu ? 0u : Sp);
+        const uint32_t rem = n - pos;
+        if (live) {
+            // speculative field reads at p (independent of each other)
+            uint32_t kl = 0, vl;
+            if (G == LSM_GRAMMAR_V) {
+                vl = rd(p);
+            } else {
+                kl = rd(p);
+                vl = rd(p + 4 + (Kp == 0xFFFFFFFFu ? 0u : Kp));
+            }
+            // lane 0: exact record at pos
+            uint32_t k0 = kl, v0 = vl;
+            int32_t st0 = LSM_OK;
+            if (t == 0) {
+                if (rem == 0) {
+                    st0 = -1;  // clean end
+                } else if (rem < 4) {
+                    st0 = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
+                } else if (G == LSM_GRAMMAR_V) {
+                    if (rem - 4 < v0) st0 = LSM_ST_TRUNC_VAL;
+                } else if (G == LSM_GRAMMAR_KV) {
+                    if (k0 > kKeyCap) st0 = LSM_ST_KEY_TOO_LONG;
+                    else if (rem - 4 < k0) st0 = LSM_ST_TRUNC_KEY;
+                    else {
+                        const uint32_t vp = pos + 4 + k0, rem2 = n - vp;
+                        if (rem2 < 4) st0 = LSM_ST_TRUNC_VLEN;
+                        else {
+                            if (k0 != Kp) v0 = rd(vp);
+                            if (v0 > kValCap) st0 = LSM_ST_VAL_TOO_LONG;
+                            else if (rem2 - 4 < v0) st0 = LSM_ST_TRUNC_VAL;
+                        }
+                    }
+                } else {
+                    if ((uint64_t)rem < 12ull + k0) st0 = LSM_ST_IDX_OVERRUN;
+                }
+                if (st0 == LSM_OK && nr >= ncap) st0 = LSM_ST_CAPACITY;
+            }
+            // broadcast lane 0's verdict and shape to its group
+            st0 = __shfl(st0, glead, kWave);
+            K = __shfl(k0, glead, kWave);
+            V = __shfl(v0, glead, kWave);
+            if (st0 != LSM_OK) {
+                if (st0 > 0) status = st0;
+                live = false;
+            } else {
+                S = G == LSM_GRAMMAR_V ? 4 + V : G == LSM_GRAMMAR_KV ? 8 + K + V : 12 + K;
+                bool ok;
+                if (t == 0) {
+                    ok = true;
+                } else {
+                    ok = (S == Sp) & ((uint64_t)p + S <= n) & (nr + t < ncap);
+                    if (G == LSM_GRAMMAR_V) ok = ok & (vl == V);
+                    else if (G == LSM_GRAMMAR_KV) ok = ok & (kl == K) & (vl == V);
+                    else ok = ok & (kl == K);
+                }
+                acc = ok;
+                if (G == LSM_GRAMMAR_IDX && ok) x = (uint64_t)rd(p + 8 + K) << 32 | rd(p + 4 + K);
+            }
+        }
+        // leading run of accepted lanes in each group
+        const uint64_t m = __ballot(acc);
+        constexpr uint64_t kGM = H == 64 ? ~0ull : ((1ull << (H % 64)) - 1);
+        const uint64_t gm = (m >> glead) & kGM;
+        const uint64_t inv = ~gm & kGM;
+        const uint32_t j = inv ? (uint32_t)__builtin_ctzll(inv) : H;
+        if (live && t < j) {
+            const uint64_t ro = off + p;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = G == LSM_GRAMMAR_V ? 0u : K;
+            d.w = G == LSM_GRAMMAR_IDX ? 8u : V;
+            a.desc[base + nr + t] = d;
+            if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + t] = (int64_t)x;
+        }
+        if (live) {
+            nr += j;
+            pos += j * S;
+            Kp = K;
+            Sp = S;
+        }
+    }
+    if (small && t == 0) {
+        a.nrec[b] = nr;
+        a.status[b] = status;
+    }
+    // Blocks too large for a slot: wave path with slot 0 as its ring.
+    const uint64_t big_mask = __ballot(mine && !small && t == 0);
+    for (uint32_t j = 0; j < NB; j++)
+        if ((big_mask >> (j * H)) & 1) {
+            const uint32_t bb = b0 + j;
+            decode_block_spec<G>(a, bb, slots, uni64(a.blk_off[bb]), uni(a.blk_len[bb]));
+        }
+}
+
+template <int G, uint32_t H>
+int launch_group(const DecodeArgs &a, hipStream_t s) {
+    constexpr uint32_t NB = kWave / H;
+    const uint32_t grid = (a.nblk + NB - 1) / NB;
+    hipLaunchKernelGGL((decode_group_kernel<G, H>), dim3(grid), dim3(kWave), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// ---- persistent, double-buffered speculative path (DESC mode, default) ----
+//
+// Each wave walks blocks w, w + W, w + 2W, ... (W = resident waves) with two
+// 4 KiB ring slots: block k+1's four 1 KiB LDS-DMAs are issued before block k
+// is decoded, and a static s_waitcnt vmcnt(4) (the four younger DMAs may stay
+// in flight) releases block k.  So every wave always has a block in flight
+// and the DMA latency hides behind the previous block's chase -- the
+// occupancy needed for HBM rate (Little's law: ~18 blocks per CU at ~3 us)
+// is reached with 20 waves per CU.  Metadata of block k+2 is prefetched with
+// scalar loads.  Blocks larger than the 4 KiB ring stream on through the
+// ring's own refills.
+__device__ __forceinline__ void stage_block(uint32_t *ring, const uint8_t *in, uint64_t off,
+                                            uint32_t n) {
+    const uint64_t a0 = off & ~(uint64_t)15;
+    uint64_t tot = ((off - a0) + n + 15) & ~(uint64_t)15;
+    if (tot > kRingBytes) tot = kRingBytes;  // first 4 KiB; larger blocks refill later
+    const rsrc_t r = make_rsrc(in + a0, (uint32_t)tot);
+    const uint32_t v = lane_id() * 16;
+#pragma unroll
+    for (uint32_t c = 0; c < kNChunk; c++)  // always 4 ops: OOB chunks read as 0
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void *)&ring[c * (kChunk / 4)], 16, c * kChunk + v,
+            0, 0, 0);
+}
+
+constexpr uint32_t kPipeWaves = 4;  // waves per workgroup (32 KiB LDS)
+
+template <int G>
+__global__ __launch_bounds__(256) void decode_pipe_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t slots[kPipeWaves][2][kRingWords];
+    const uint32_t wave = uni(threadIdx.x / kWave);
+    const uint32_t W = gridDim.x * kPipeWaves;
+    uint32_t b = uni(blockIdx.x * kPipeWaves + wave);
     if (b >= a.nblk) return;
-    decode_block_spec<G>(a, b, ring[wave]);
+    uint64_t off = uni64(a.blk_off[b]);
+    uint32_t n = uni(a.blk_len[b]);
+    stage_block(slots[wave][0], a.in, off, n);
+    uint32_t nb = b + W;
+    uint64_t noff = 0;
+    uint32_t nn = 0;
+    if (nb < a.nblk) {
+        noff = uni64(a.blk_off[nb]);
+        nn = uni(a.blk_len[nb]);
+    }
+    for (uint32_t k = 0;; k++) {
+        uint32_t *cur = slots[wave][k & 1];
+        const bool more = nb < a.nblk;
+        if (more) {
+            stage_block(slots[wave][(k + 1) & 1], a.in, noff, nn);
+            __asm__ __volatile__("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        // prefetch metadata two blocks ahead
+        const uint32_t nnb = nb + W;
+        uint64_t poff = 0;
+        uint32_t pn = 0;
+        if (more && nnb < a.nblk) {
+            poff = uni64(a.blk_off[nnb]);
+            pn = uni(a.blk_len[nnb]);
+        }
+        decode_block_spec<G>(a, b, cur, off, n, true);
+        if (!more) break;
+        b = nb;
+        off = noff;
+        n = nn;
+        nb = nnb;
+        noff = poff;
+        nn = pn;
+    }
+}
+
+template <int G>
+int launch_pipe(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
+    // 5 workgroups (20 waves) per CU fit the LDS; a fixed residency-sized grid.
+    const uint32_t cus = ctx ? (uint32_t)lsm_ctx_num_cus(ctx) : 256u;
+    const uint32_t want = cus * 5;
+    const uint32_t need = (a.nblk + kPipeWaves - 1) / kPipeWaves;
+    const uint32_t grid = need < want ? need : want;
+    hipLaunchKernelGGL((decode_pipe_kernel<G>), dim3(grid), dim3(kWave * kPipeWaves), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+template <int G, uint32_t K, uint32_t WPG = kWavesPerWG>
+int launch_spec(const DecodeArgs &a, hipStream_t s) {
+    const uint32_t waves = (a.nblk + K - 1) / K;
+    const uint32_t grid = (waves + WPG - 1) / WPG;
+    hipLaunchKernelGGL((decode_spec_kernel<G, K, WPG>), dim3(grid), dim3(kWave * WPG), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 template <int G, bool ARENA>
@@ -424,19 +725,6 @@ __global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
 // writes its descriptors.  Slots are skewed by 16 bytes so lanes walking
 // identically laid out blocks hit different banks.  Blocks that do not fit a
 // slot are decoded afterwards by the wave path.
-constexpr uint32_t kSlotBytes = 4096;
-constexpr uint32_t kSlotStride = kSlotBytes + 16;
-
-#ifdef LSM_STAMPS
-// Diagnostic build only (liblsm_gpu_stamps.so): per-workgroup s_memrealtime
-// stamps {start, DMA landed, chase done, end} into a buffer of their own.
-__device__ uint64_t *g_stamps;
-__device__ __forceinline__ void stamp(uint32_t k) {
-    if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
-}
-#else
-__device__ __forceinline__ void stamp(uint32_t) {}
-#endif
 
 template <int G, uint32_t kLaneBlocks>
 __global__ __launch_bounds__(64) void decode_lanes_kernel(DecodeArgs a) {
@@ -807,7 +1095,7 @@ int launch_lanes(const DecodeArgs &a, hipStream_t s) {
 }
 
 template <int G, bool ARENA>
-int launch_decode(const DecodeArgs &a, hipStream_t s) {
+int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
     if (!ARENA) {
         // Default: wave-per-block with speculative parallel runs.
         // LSM_DECODE_KERNEL selects variants for A/B measurement.
@@ -819,16 +1107,32 @@ int launch_decode(const DecodeArgs &a, hipStream_t s) {
             if (!strcmp(e, "stream64x32")) return 3;
             if (!strcmp(e, "lanes")) return 9;
             if (!strcmp(e, "stream32x32")) return 4;
+            if (!strcmp(e, "spec4")) return 10;
+            if (!strcmp(e, "spec")) return 30;
+            if (!strcmp(e, "spec_w1")) return 31;
+            if (!strcmp(e, "spec_w2")) return 32;
+            if (!strcmp(e, "pipe")) return 33;
+            if (!strcmp(e, "group64")) return 20;
+            if (!strcmp(e, "group32")) return 21;
+            if (!strcmp(e, "group16")) return 22;
+            if (!strcmp(e, "spec2")) return 11;
+            if (!strcmp(e, "spec8")) return 12;
+            if (!strcmp(e, "spec16")) return 13;
             return 0;
         }();
         switch (variant) {
-        case 0: {
-            uint32_t grid = (a.nblk + kWavesPerWG - 1) / kWavesPerWG;
-            hipLaunchKernelGGL((decode_spec_kernel<G>), dim3(grid), dim3(kWave * kWavesPerWG),
-                               0, s, a);
-            LSM_HIP_CHECK(hipGetLastError());
-            return 0;
-        }
+        case 0: return launch_spec<G, 1>(a, s);
+        case 33: return launch_pipe<G>(ctx, a, s);
+        case 30: return launch_spec<G, 1>(a, s);
+        case 31: return launch_spec<G, 1, 1>(a, s);
+        case 32: return launch_spec<G, 1, 2>(a, s);
+        case 20: return launch_group<G, 64>(a, s);
+        case 21: return launch_group<G, 32>(a, s);
+        case 22: return launch_group<G, 16>(a, s);
+        case 10: return launch_spec<G, 4>(a, s);
+        case 11: return launch_spec<G, 2>(a, s);
+        case 12: return launch_spec<G, 8>(a, s);
+        case 13: return launch_spec<G, 16>(a, s);
         case 4: return launch_stream<G, 32, 32>(a, s);
         case 1: return launch_stream<G, 64, 16>(a, s);
         case 2: return launch_stream<G, 32, 64>(a, s);
@@ -921,12 +1225,12 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
     a.val_arena_off = out->val_arena_off;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (grammar) {
-    case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true>(a, s)
-                                     : launch_decode<LSM_GRAMMAR_V, false>(a, s);
-    case LSM_GRAMMAR_KV: return arena ? launch_decode<LSM_GRAMMAR_KV, true>(a, s)
-                                      : launch_decode<LSM_GRAMMAR_KV, false>(a, s);
-    default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true>(a, s)
-                          : launch_decode<LSM_GRAMMAR_IDX, false>(a, s);
+    case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true>(ctx, a, s)
+                                     : launch_decode<LSM_GRAMMAR_V, false>(ctx, a, s);
+    case LSM_GRAMMAR_KV: return arena ? launch_decode<LSM_GRAMMAR_KV, true>(ctx, a, s)
+                                      : launch_decode<LSM_GRAMMAR_KV, false>(ctx, a, s);
+    default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true>(ctx, a, s)
+                          : launch_decode<LSM_GRAMMAR_IDX, false>(ctx, a, s);
     }
 }
 

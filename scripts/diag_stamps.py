@@ -19,7 +19,7 @@ lib = _lib.load()
 lib.lsm_debug_set_stamps.argtypes = [ctypes.c_void_p]
 lib.lsm_debug_set_stamps.restype = ctypes.c_int
 
-B = int(os.environ.get("LSM_LANE_BLOCKS", "3"))
+B = int(os.environ.get("DIAG_BLOCKS_PER_WG", "4"))  # spec kernel: 4 waves x 1 block
 ctx = lsmgpu.Context(0)
 dev = ctx.torch_device
 nblk = 100_000
