@@ -65,22 +65,29 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(world, x):
+def _reduce(world, x, op):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def max_over_ranks(world, x):
+    import torch.distributed as dist
+    return _reduce(world, x, dist.ReduceOp.MAX if world > 1 else None)
 
 
 def sum_over_ranks(world, x):
-    if world == 1:
-        return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(world, x, dist.ReduceOp.SUM if world > 1 else None)
+
+
+def shard_block_ids(rank, world, per):
+    """Round-robin deal of the global batch: block i -> rank i mod N."""
+    return rank + world * np.arange(per, dtype=np.int64)
 
 
 def traffic_from_profile(workload_key):
@@ -104,7 +111,7 @@ def traffic_from_profile(workload_key):
 def make_workload(args, world, rank):
     if args.config in ("decode4k", "decode64k"):
         per = args.blocks or (100_000 if args.config == "decode4k" else 6_400)
-        ids = rank + world * np.arange(per, dtype=np.int64)  # round-robin deal
+        ids = shard_block_ids(rank, world, per)
         if args.config == "decode4k":
             buf, off, ln = synth.uniform_kv_blocks(ids)
             desc = "decode %d x 4 KiB KV blocks per GPU (33 x 16 B key / 100 B value)" % per
