@@ -18,8 +18,12 @@ def _ensure_built():
     if not os.path.exists(ora):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                        stdout=subprocess.DEVNULL)
-    if not os.path.exists(gpu):
+    mirror = os.path.join(ROOT, "go-lsm_amd", "libgolsm.so")
+    if not (os.path.exists(gpu) and os.path.exists(mirror)):
         subprocess.run(["make", "-C", os.path.join(ROOT, "go-lsm_amd"), "-j4"], check=True,
+                       stdout=subprocess.DEVNULL)
+    if not os.path.exists(os.path.join(ROOT, "tests", "cpp", "mirror_test")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp")], check=True,
                        stdout=subprocess.DEVNULL)
 
 
