@@ -158,6 +158,351 @@ __device__ void encode_chunk(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint
     }
 }
 
+
+// ---- LDS-staged chunk encoder (the fast path) -----------------------------
+//
+// The chunk's source bytes (its keys span and/or values span, each contiguous
+// in the CSR batch) are staged into LDS with coalesced 16 B loads, all issued
+// before the first use, so the chunk costs one memory latency.  Output is
+// then assembled in aligned 16 B segments: a segment inside one key or value
+// is five LDS dwords and four v_alignbyte, a segment across a length field or
+// record boundary is built per dword, and the two chunk-edge segments (bytes
+// shared with neighbour chunks) are stored byte by byte.
+constexpr uint32_t kStageBytes = 8192;  // per wave
+
+struct StagedTable {
+    uint32_t P[kWave + 1];  // chunk-relative record start; P[cnt] = chunk bytes
+    uint32_t ks[kWave], vs[kWave];  // stage offsets of the key / value bytes
+    uint32_t kl[kWave], vl[kWave];
+    uint32_t xlo[kWave], xhi[kWave];  // IDX offset
+};
+
+struct StageLds {
+    StagedTable tb;
+    uint32_t w[kStageBytes / 4 + 8];
+};
+
+__device__ __forceinline__ uint32_t stage_byte(const uint32_t *w, uint32_t q) {
+    return (w[q >> 2] >> (8 * (q & 3))) & 0xff;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t staged_byte(const StageLds &L, uint32_t r, uint32_t w) {
+    const StagedTable &t = L.tb;
+    if (G == LSM_GRAMMAR_V) {
+        if (w < 4) return (t.vl[r] >> (8 * w)) & 0xff;
+        return stage_byte(L.w, t.vs[r] + w - 4);
+    }
+    const uint32_t kl = t.kl[r];
+    if (w < 4) return (kl >> (8 * w)) & 0xff;
+    if (w < 4 + kl) return stage_byte(L.w, t.ks[r] + w - 4);
+    const uint32_t w2 = w - 4 - kl;
+    if (G == LSM_GRAMMAR_IDX) return ((w2 < 4 ? t.xlo[r] : t.xhi[r]) >> (8 * (w2 & 3))) & 0xff;
+    if (w2 < 4) return (t.vl[r] >> (8 * w2)) & 0xff;
+    return stage_byte(L.w, t.vs[r] + w2 - 4);
+}
+
+// Stage offset of record-relative bytes [w, w+len) if they lie inside one
+// key or value of record r, else ~0u.
+template <int G>
+__device__ __forceinline__ uint32_t staged_src(const StagedTable &t, uint32_t r, uint32_t w,
+                                               uint32_t len) {
+    if (G == LSM_GRAMMAR_V) {
+        return (w >= 4 && w + len <= 4 + t.vl[r]) ? t.vs[r] + w - 4 : ~0u;
+    }
+    const uint32_t kl = t.kl[r];
+    if (w >= 4 && w + len <= 4 + kl) return t.ks[r] + w - 4;
+    if (G == LSM_GRAMMAR_KV && w >= 8 + kl && w + len <= 8 + kl + t.vl[r]) return t.vs[r] + w - 8 - kl;
+    return ~0u;
+}
+
+// Stage two byte spans [srcA, srcA+nA) and [srcB, srcB+nB) (either may be
+// empty) by LDS-DMA (buffer_load_dwordx4 ... lds: 1 KiB per wave
+// instruction, no VGPR staging): span A's 16-byte lines at stage offset 0,
+// span B's at the next 1 KiB boundary.  All loads are in flight together and
+// one s_waitcnt releases them.  Returns the stage offsets of srcA and srcB.
+__device__ __forceinline__ uint32_t span_lines(uint64_t src, uint32_t n) {
+    return n ? (uint32_t)(((src & 15) + n + 15) >> 4) : 0;
+}
+__device__ __forceinline__ uint32_t span_stage_bytes(uint32_t lines) {
+    return (lines * 16 + 1023) & ~1023u;
+}
+
+__device__ __forceinline__ void dma_span(uint32_t *w, uint32_t at, const uint8_t *base, uint64_t src,
+                                         uint32_t lines) {
+    const uint64_t a0 = src & ~(uint64_t)15;
+    const rsrc_t r = make_rsrc(base + a0, lines * 16);
+    const uint32_t v = lane_id() * 16;
+    for (uint32_t c = 0; c * kWave < lines; c++)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void *)&w[(at + 1024 * c) / 4], 16, 1024 * c + v, 0,
+            0, 0);
+}
+
+__device__ __forceinline__ void stage_spans(uint32_t *w, const uint8_t *baseA, uint64_t srcA,
+                                            uint32_t nA, const uint8_t *baseB, uint64_t srcB,
+                                            uint32_t nB, uint32_t &offA, uint32_t &offB) {
+    const uint32_t lA = span_lines(srcA, nA), lB = span_lines(srcB, nB);
+    const uint32_t atB = span_stage_bytes(lA);
+    if (lA) dma_span(w, 0, baseA, srcA, lA);
+    if (lB) dma_span(w, atB, baseB, srcB, lB);
+    // The DMA writes are invisible to the compiler's LDS tracking.
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+    offA = (uint32_t)(srcA & 15);
+    offB = atB + (uint32_t)(srcB & 15);
+}
+
+// Encode records [c0, c0+cnt) (cnt <= 64) to dst through LDS.  Returns false
+// (nothing written) when the chunk's source bytes exceed the stage.
+template <int G>
+__device__ bool encode_chunk_staged(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint8_t *dst,
+                                    StageLds *L) {
+    using T = GrammarTraits<G>;
+    const uint32_t lane = lane_id();
+    const bool useK = T::K;
+    const bool useV = T::V;
+    const uint64_t Kc = useK ? uni64(S.koff[c0]) : 0, Ke = useK ? uni64(S.koff[c0 + cnt]) : 0;
+    const uint64_t Vc = (useV || (G == LSM_GRAMMAR_IDX && !S.idx_off)) ? uni64(S.voff[c0]) : 0;
+    const uint64_t Ve = useV ? uni64(S.voff[c0 + cnt]) : 0;
+    const uint64_t nK = Ke - Kc, nV = Ve - Vc;
+    if (nK > kStageBytes || nV > kStageBytes) return false;
+    const uint32_t need = span_stage_bytes(useK ? span_lines(Kc, (uint32_t)nK) : 0) +
+                          span_stage_bytes(useV ? span_lines(Vc, (uint32_t)nV) : 0);
+    if (need > kStageBytes) return false;
+
+    uint32_t kbase = 0, vbase = 0;
+    stage_spans(L->w, S.keys, Kc, useK ? (uint32_t)nK : 0, S.vals, Vc, useV ? (uint32_t)nV : 0,
+                kbase, vbase);
+
+    uint32_t kl = 0, vl = 0, ks = 0, vs = 0, sz = 0;
+    uint64_t xo = 0;
+    if (lane < cnt) {
+        const uint64_t i = c0 + lane;
+        uint64_t K0 = 0, V0 = 0;
+        if (useK) { K0 = S.koff[i]; kl = (uint32_t)(S.koff[i + 1] - K0); ks = kbase + (uint32_t)(K0 - Kc); }
+        if (useV || (G == LSM_GRAMMAR_IDX && !S.idx_off)) V0 = S.voff[i];
+        if (useV) { vl = (uint32_t)(S.voff[i + 1] - V0); vs = vbase + (uint32_t)(V0 - Vc); }
+        if (G == LSM_GRAMMAR_IDX)
+            xo = S.idx_off ? (uint64_t)S.idx_off[i]
+                           : (uint64_t)(S.idx_base + (int64_t)(4 * (i - S.rs) + (V0 - S.vrs)));
+        sz = T::pre + (useK ? kl : 0) + (useV ? vl : 0);
+    }
+    uint32_t tot;
+    const uint32_t P = wave_excl_scan(sz, &tot);
+    if (lane < cnt) {
+        L->tb.P[lane] = P;
+        L->tb.ks[lane] = ks;
+        L->tb.vs[lane] = vs;
+        L->tb.kl[lane] = kl;
+        L->tb.vl[lane] = vl;
+        L->tb.xlo[lane] = (uint32_t)xo;
+        L->tb.xhi[lane] = (uint32_t)(xo >> 32);
+    }
+    if (lane == 0) L->tb.P[cnt] = tot;
+    // LDS ops of one wave complete in order: the stage and table are visible
+    // to every lane's later reads.
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+
+    const StagedTable &t = L->tb;
+    const uintptr_t Ob = reinterpret_cast<uintptr_t>(dst);
+    const uint32_t head = (uint32_t)(Ob & 15);
+    u32x4 *dA = reinterpret_cast<u32x4 *>(Ob - head);
+    const uint32_t nseg = (head + tot + 15) >> 4;
+    uint32_t r = 0;
+    for (uint32_t e = lane; e < nseg; e += kWave) {
+        const int32_t u0 = (int32_t)(16 * e) - (int32_t)head;
+        const uint32_t uf = u0 < 0 ? 0 : (uint32_t)u0;
+        while (r + 1 < cnt && t.P[r + 1] <= uf) r++;
+        if (u0 >= 0 && (uint32_t)u0 + 16 <= tot) {
+            u32x4 out;
+            const uint32_t q = staged_src<G>(t, r, (uint32_t)u0 - t.P[r], 16);
+            if (q != ~0u) {
+                const uint32_t a = q >> 2;
+                const uint32_t s0 = L->w[a], s1 = L->w[a + 1], s2 = L->w[a + 2], s3 = L->w[a + 3],
+                               s4 = L->w[a + 4];
+                out.x = funnel(s0, s1, q);
+                out.y = funnel(s1, s2, q);
+                out.z = funnel(s2, s3, q);
+                out.w = funnel(s3, s4, q);
+            } else {
+                uint32_t dw[4];
+                uint32_t rr = r;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t u = (uint32_t)u0 + 4 * i;
+                    while (rr + 1 < cnt && t.P[rr + 1] <= u) rr++;
+                    const uint32_t w = u - t.P[rr];
+                    const uint32_t q4 = (u + 4 <= t.P[rr + 1]) ? staged_src<G>(t, rr, w, 4) : ~0u;
+                    if (q4 != ~0u) {
+                        dw[i] = funnel(L->w[q4 >> 2], L->w[(q4 >> 2) + 1], q4);
+                    } else {
+                        uint32_t v = 0, rb = rr;
+                        for (uint32_t b = 0; b < 4; b++) {
+                            while (rb + 1 < cnt && t.P[rb + 1] <= u + b) rb++;
+                            v |= staged_byte<G>(*L, rb, u + b - t.P[rb]) << (8 * b);
+                        }
+                        dw[i] = v;
+                    }
+                }
+                out.x = dw[0]; out.y = dw[1]; out.z = dw[2]; out.w = dw[3];
+            }
+            dA[e] = out;
+        } else {
+            // chunk-edge segment: only this chunk's bytes, one at a time
+            uint8_t *db = reinterpret_cast<uint8_t *>(dA + e);
+            uint32_t rb = r;
+            for (uint32_t b = 0; b < 16; b++) {
+                const int32_t u = u0 + (int32_t)b;
+                if (u < 0 || (uint32_t)u >= tot) continue;
+                while (rb + 1 < cnt && t.P[rb + 1] <= (uint32_t)u) rb++;
+                db[b] = (uint8_t)staged_byte<G>(*L, rb, (uint32_t)u - t.P[rb]);
+            }
+        }
+    }
+    // The next chunk overwrites the stage: every lane's reads must be done.
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    return true;
+}
+
+// ---- DMA-gather chunk encoder (V and IDX: the .sst regions) ----------------
+//
+// A V record is [u32 vlen][value] and an IDX record [u32 klen][key][i64 off]:
+// one payload (value / key) plus fixed-size fields.  With chunk-relative
+// record starts P[r] = pre*r + (payload bytes before r) (pre = 4 / 12), the
+// payload byte at chunk position x of record r sits at source position
+// x - pre*r - 4 (relative to the chunk's first payload byte): a per-record
+// shift that is a multiple of 4.  So if the chunk image is laid out in LDS
+// with the source's dword phase, every LDS dword of the image is exactly one
+// aligned source dword, and the image is gathered by LDS-DMA (64 dwords per
+// wave instruction, each lane's source from a 6-step ds_bpermute binary
+// search for its record) -- no per-byte work and no divergence, whatever the
+// record sizes.  Bytes of the fixed fields receive neighbouring payload bytes
+// from the gather and are then overwritten by each record's lane (ds_write_b8;
+// a dword never reaches from one payload into the next one's payload, since
+// the 4-byte prefix sits between).  The image is stored with aligned 16-byte
+// stores (ds_read_b128 + funnel shift), chunk-edge bytes singly.
+constexpr uint32_t kGatherDwords = 1856;  // 7.25 KiB per wave
+
+template <int G>
+__device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint8_t *dst,
+                                    uint32_t *lds) {
+    static_assert(G != LSM_GRAMMAR_KV, "one payload per record");
+    constexpr uint32_t pre = G == LSM_GRAMMAR_V ? 4 : 12;
+    const uint32_t lane = lane_id();
+    const uint8_t *sbase = G == LSM_GRAMMAR_V ? S.vals : S.keys;
+    const uint64_t *soff = G == LSM_GRAMMAR_V ? S.voff : S.koff;
+    const uint64_t Sc = uni64(soff[c0]);
+    uint64_t len = 0, xo = 0;
+    if (lane < cnt) {
+        const uint64_t i = c0 + lane;
+        len = soff[i + 1] - soff[i];
+        if (G == LSM_GRAMMAR_IDX)
+            xo = S.idx_off ? (uint64_t)S.idx_off[i]
+                           : (uint64_t)(S.idx_base + (int64_t)(4 * (i - S.rs) + (S.voff[i] - S.vrs)));
+    }
+    uint64_t tot64;
+    const uint64_t P64 = wave_excl_scan64(lane < cnt ? pre + len : 0, &tot64);
+    const uint32_t ph = (uint32_t)(Sc & 3);
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
+    if (tot64 + 64 > 4ull * kGatherDwords) return false;
+    const uint32_t tot = (uint32_t)tot64, P = (uint32_t)P64;
+    const uint32_t nD = (tot + ph + 3) >> 2;
+    const int32_t T = (int32_t)ph - (int32_t)head;
+    const uint32_t sh = (uint32_t)T & 3;
+    const uint32_t OD = 8 + (((uint32_t)(-(T - (int32_t)sh)) >> 2) & 3);
+    if (OD + ((nD + 63) & ~63u) + 8 > kGatherDwords) return false;
+
+    // gather: image dword D covers chunk bytes [4D - ph, 4D - ph + 4)
+    const uint32_t Pl = lane < cnt ? P : 0xFFFFFFFFu;
+    const uint32_t sbytes = (uint32_t)(soff[c0 + cnt] - Sc);  // wave-uniform load below
+    const rsrc_t rs = make_rsrc(sbase + (Sc - ph), uni((sbytes + ph + 3) & ~3u));
+    for (uint32_t i = 0; i * kWave < nD; i++) {
+        const int32_t x0 = 4 * (int32_t)(i * kWave + lane) - (int32_t)ph;
+        const uint32_t x = x0 < 0 ? 0u : (uint32_t)x0;
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t st = 32; st; st >>= 1) {
+            const uint32_t Pc = __builtin_amdgcn_ds_bpermute((int)((r + st) << 2), (int)Pl);
+            if (Pc <= x) r += st;
+        }
+        const uint32_t voff = (uint32_t)(x0 - (int32_t)(pre * r) - 4 + (int32_t)ph);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void *)&lds[OD + i * kWave], 4, voff, 0, 0, 2);
+    }
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // fixed fields of this lane's record
+    uint8_t *ob = reinterpret_cast<uint8_t *>(lds) + 4 * OD + ph;
+    if (lane < cnt) {
+        const uint32_t l32 = (uint32_t)len;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; b++) ob[P + b] = (uint8_t)(l32 >> (8 * b));
+        if (G == LSM_GRAMMAR_IDX) {
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) ob[P + 4 + l32 + b] = (uint8_t)(xo >> (8 * b));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+
+    // store: segment e = global bytes [dA + 16e, +16) = chunk bytes [16e - head, +16)
+    u32x4 *dA = reinterpret_cast<u32x4 *>(reinterpret_cast<uintptr_t>(dst) - head);
+    const uint32_t nseg = (head + tot + 15) >> 4;
+    const uint32_t q0 = OD + (uint32_t)((T - (int32_t)sh) >> 2);  // dword of segment 0
+    for (uint32_t e = lane; e < nseg; e += kWave) {
+        const int32_t u0 = 16 * (int32_t)e - (int32_t)head;
+        if (u0 >= 0 && (uint32_t)u0 + 16 <= tot) {
+            const uint32_t q = q0 + 4 * e;
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(&lds[q]);
+            const uint32_t a4 = lds[q + 4];
+            u32x4 o;
+            o.x = funnel(a.x, a.y, sh);
+            o.y = funnel(a.y, a.z, sh);
+            o.z = funnel(a.z, a.w, sh);
+            o.w = funnel(a.w, a4, sh);
+            dA[e] = o;
+        } else {
+            uint8_t *db = reinterpret_cast<uint8_t *>(dA + e);
+            for (uint32_t b = 0; b < 16; b++) {
+                const int32_t u = u0 + (int32_t)b;
+                if (u >= 0 && (uint32_t)u < tot) db[b] = ob[u];
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    return true;
+}
+
+// Per-wave LDS: the staged encoder, or the global-source fallback's table.
+union EncodeLds {
+    StageLds st;
+    ChunkTable ct;
+    uint32_t gather[kGatherDwords];
+};
+union RegionLds {  // V / IDX only: no KV stage
+    ChunkTable ct;
+    uint32_t gather[kGatherDwords];
+};
+
+// Chunk encoder dispatch: DMA gather (V / IDX), LDS-staged (KV), then the
+// global-source fallback for chunks too large for LDS.  The three LDS views
+// alias one per-wave buffer.
+template <int G>
+__device__ __forceinline__ void encode_chunk_any(const RegionSrc &S, uint64_t c0, uint32_t cnt,
+                                                 uint8_t *dst, uint32_t *gather, StageLds *st,
+                                                 ChunkTable *ct) {
+    if (G == LSM_GRAMMAR_KV) {
+        if (encode_chunk_staged<LSM_GRAMMAR_KV>(S, c0, cnt, dst, st)) return;
+    } else {
+        if (encode_chunk_gather<G == LSM_GRAMMAR_KV ? LSM_GRAMMAR_V : G>(S, c0, cnt, dst, gather))
+            return;
+    }
+    encode_chunk<G>(S, c0, cnt, dst, ct);
+}
+
 // ---- lsm_encode_blocks ----------------------------------------------------
 
 struct EncodeBlocksArgs {
@@ -173,7 +518,7 @@ constexpr int kEncWaves = 4;
 template <int G>
 __global__ __launch_bounds__(256) void encode_blocks_kernel(EncodeBlocksArgs a) {
     using T = GrammarTraits<G>;
-    __shared__ ChunkTable tables[kEncWaves];
+    __shared__ EncodeLds lds[kEncWaves];
     const uint32_t b = blockIdx.x;
     const uint32_t wave = uni(threadIdx.x / kWave);
     const uint64_t rs = uni64(a.rec_start[b]);
@@ -186,11 +531,62 @@ __global__ __launch_bounds__(256) void encode_blocks_kernel(EncodeBlocksArgs a) 
         uint64_t rel = T::pre * (c0 - rs);
         if (T::K) rel += uni64(a.S.koff[c0]) - Krs;
         if (T::V) rel += uni64(a.S.voff[c0]) - Vrs;
-        encode_chunk<G>(a.S, c0, cnt, out + rel, &tables[wave]);
+        encode_chunk_any<G>(a.S, c0, cnt, out + rel, lds[wave].gather, &lds[wave].st, &lds[wave].ct);
     }
 }
 
 // ---- fused bloom build (LDS slices) --------------------------------------
+
+// Header bytes of the .sst holding records [s, e): u32 kl | min key | u32 kl |
+// max key (header.go:25-37; Builder.Finalize sets min/max = first/last key).
+__device__ __forceinline__ uint64_t sst_header_bytes(const uint64_t *koff, uint64_t s, uint64_t e) {
+    if (e <= s) return 8;
+    return 8 + (uni64(koff[s + 1]) - uni64(koff[s])) + (uni64(koff[e]) - uni64(koff[e - 1]));
+}
+
+// Big-endian stream dword q of the filter words held in LDS as native u32
+// pairs (word w = bits[2w] | bits[2w+1] << 32; bitset.WriteTo writes words
+// big-endian, so stream dword 2w is bswap(hi), 2w+1 is bswap(lo)).
+__device__ __forceinline__ uint32_t be_dword(const uint32_t *bits, uint64_t q) {
+    return bswap32(bits[(q & ~1ull) + ((q & 1) ^ 1)]);
+}
+
+// Store an LDS slice holding native filter words [wlo, whi) (bits[0] = word
+// wlo's low half).  Image mode (img_words != null, pointing at filter word 0
+// inside the .sst): big-endian bytes, whole dwords inside the slice's byte
+// range and single bytes at its edges (the neighbouring bytes belong to the
+// other slice or to the filter prefix).  Native mode: u64 words to native.
+__device__ void store_filter_slice(const uint32_t *bits, uint64_t wlo, uint64_t whi,
+                                   uint8_t *img_words, uint64_t *native) {
+    const uint32_t nthr = blockDim.x;
+    if (!img_words) {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(native + wlo);
+        for (uint64_t i = threadIdx.x; i < 2 * (whi - wlo); i += nthr) dst[i] = bits[i];
+        return;
+    }
+    const uint64_t len = 8 * (whi - wlo);
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(img_words + 8 * wlo);
+    const uint32_t head = (uint32_t)(p0 & 3);
+    uint32_t *dA = reinterpret_cast<uint32_t *>(p0 - head);
+    const uint64_t ndw = (head + len + 3) / 4;
+    for (uint64_t d = threadIdx.x; d < ndw; d += nthr) {
+        const int64_t u0 = (int64_t)(4 * d) - head;
+        if (u0 >= 0 && (uint64_t)u0 + 4 <= len) {
+            const uint64_t q = (uint64_t)u0 >> 2;
+            const uint32_t sh = (uint32_t)u0 & 3;
+            const uint32_t lo = be_dword(bits, q);
+            const uint32_t hi = sh ? be_dword(bits, q + 1) : 0;
+            dA[d] = funnel(lo, hi, sh);
+        } else {
+            uint8_t *db = reinterpret_cast<uint8_t *>(dA + d);
+            for (uint32_t b = 0; b < 4; b++) {
+                const int64_t u = u0 + b;
+                if (u < 0 || (uint64_t)u >= len) continue;
+                db[b] = (uint8_t)(be_dword(bits, (uint64_t)u >> 2) >> (8 * ((uint32_t)u & 3)));
+            }
+        }
+    }
+}
 
 struct BloomArgs {
     const uint8_t *keys;
@@ -200,10 +596,16 @@ struct BloomArgs {
     uint32_t k;
     uint64_t slice_bits;   // multiple of 64
     uint64_t nwords;       // ceil(m/64)
-    uint64_t *bitmap;      // nfile * nwords native u64 words
+    uint64_t *bitmap;      // native mode: nfile * nwords u64 words
     uint64_t nkeys;        // keys of the single filter when file_start == null
+    uint8_t *out;          // image mode (bitmap == null): .sst images
+    const uint64_t *file_off;
 };
 
+// One workgroup per (filter, slice): hashes every key of the filter (sum256 +
+// k locations + Barrett modulo) and ds_or's the bits inside its slice.  Used
+// for single filters (lsm_bloom_build) and for filters whose slice count the
+// binned path below does not cover.
 __global__ __launch_bounds__(1024) void bloom_slices_kernel(BloomArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
     const uint32_t f = blockIdx.x;
@@ -220,7 +622,7 @@ __global__ __launch_bounds__(1024) void bloom_slices_kernel(BloomArgs a) {
         uint64_t h[4];
         sum256(a.keys + k0, a.koff[i + 1] - k0, h);
         for (uint32_t j = 0; j < a.k; j++) {
-            uint64_t p = mod_barrett(location(h, j), a.m, a.mrecip);
+            uint64_t p = mod_barrett(location(h[0], h[1], h[2], h[3], j), a.m, a.mrecip);
             if (p >= lo && p < hi) {
                 uint32_t q = (uint32_t)(p - lo);
                 atomicOr(&lds_bits[q >> 5], 1u << (q & 31));
@@ -228,8 +630,131 @@ __global__ __launch_bounds__(1024) void bloom_slices_kernel(BloomArgs a) {
         }
     }
     __syncthreads();
-    uint32_t *dst = reinterpret_cast<uint32_t *>(a.bitmap + (uint64_t)f * a.nwords + lo / 64);
-    for (uint32_t i = threadIdx.x; i < nw32; i += blockDim.x) dst[i] = lds_bits[i];
+    const uint64_t wlo = lo / 64, whi = (hi + 63) / 64;
+    if (a.bitmap) {
+        store_filter_slice(lds_bits, wlo, whi, nullptr, a.bitmap + (uint64_t)f * a.nwords);
+    } else {
+        const uint64_t hdr = sst_header_bytes(a.koff, s, e);
+        store_filter_slice(lds_bits, wlo, whi, a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+    }
+}
+
+// ---- binned bloom build (two slices, m < 2^32) ------------------------------
+//
+// go-lsm's 1.6 Mbit filter needs two 100 KiB LDS slices.  Instead of hashing
+// every key once per slice, bloom_bin_kernel hashes each key once (a grid
+// over all keys: full occupancy for the compute-bound sum256 + 16 Barrett
+// moduli) and writes its bit positions binned by slice: slice 0 fills the
+// file's k*n position area from the front, slice 1 from the back, so the two
+// bins never collide and need no capacity planning.  Each wave compacts its
+// positions in LDS (ballot + mbcnt) and reserves room with one atomicAdd per
+// bin.  bloom_apply_kernel then ORs each bin into its LDS slice and stores the
+// slice straight into the image as big-endian words.
+struct BloomBinArgs {
+    const uint8_t *keys;
+    const uint64_t *koff;
+    const uint64_t *file_start;
+    uint64_t m, mrecip;
+    uint32_t k;
+    uint32_t split;  // bit positions < split -> slice 0
+    uint32_t *pos;   // file f's k * (records of f) positions at f * k * maxr
+    uint32_t maxr;   // max_file_records
+    uint32_t *cnt;   // per file: {front count, back count}
+    uint8_t *out;
+    const uint64_t *file_off;
+    uint64_t nwords;
+};
+
+constexpr uint32_t kBinWaves = 4;
+constexpr uint32_t kBinBatch = 16;  // locations per staging round
+
+struct BinLds {
+    uint32_t s0[kBinBatch * kWave], s1[kBinBatch * kWave];
+};
+
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+__global__ __launch_bounds__(64 * kBinWaves) void bloom_bin_kernel(BloomBinArgs a) {
+    __shared__ BinLds lds[kBinWaves];
+    const uint32_t f = blockIdx.x;
+    const uint32_t wave = uni(threadIdx.x / kWave);
+    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
+    const uint64_t c0 = s + (uint64_t)blockIdx.y * (kBinWaves * kWave) + (uint64_t)wave * kWave;
+    if (c0 >= e) return;
+    const uint32_t lane = lane_id();
+    const uint64_t i = c0 + lane;
+    const bool act = i < e;
+    uint64_t h[4] = {0, 0, 0, 0};
+    if (act) {
+        const uint64_t k0 = a.koff[i];
+        sum256(a.keys + k0, a.koff[i + 1] - k0, h);
+    }
+    const uint64_t base = (uint64_t)f * a.k * a.maxr;
+    const uint64_t cap = (uint64_t)a.k * (e - s);
+    BinLds &L = lds[wave];
+    for (uint32_t j0 = 0; j0 < a.k; j0 += kBinBatch) {
+        const uint32_t jn = a.k - j0 < kBinBatch ? a.k - j0 : kBinBatch;
+        uint32_t n0 = 0, n1 = 0;
+        for (uint32_t j = 0; j < jn; j++) {
+            const uint32_t p =
+                act ? (uint32_t)mod_barrett(location(h[0], h[1], h[2], h[3], j0 + j), a.m, a.mrecip) : 0;
+            const bool in1 = p >= a.split;
+            const uint64_t b1 = __ballot(act && in1), b0 = __ballot(act && !in1);
+            if (act) {
+                if (in1) L.s1[n1 + mbcnt(b1)] = p;
+                else L.s0[n0 + mbcnt(b0)] = p;
+            }
+            n0 += (uint32_t)__builtin_popcountll(b0);
+            n1 += (uint32_t)__builtin_popcountll(b1);
+        }
+        uint32_t o0 = 0, o1 = 0;
+        if (lane == 0) {
+            if (n0) o0 = atomicAdd(&a.cnt[2 * f], n0);
+            if (n1) o1 = atomicAdd(&a.cnt[2 * f + 1], n1);
+        }
+        o0 = uni(o0);
+        o1 = uni(o1);
+        __builtin_amdgcn_wave_barrier();
+        __asm__ __volatile__("" ::: "memory");
+        for (uint32_t t = lane; t < n0; t += kWave) a.pos[base + o0 + t] = L.s0[t];
+        for (uint32_t t = lane; t < n1; t += kWave) a.pos[base + cap - o1 - n1 + t] = L.s1[t];
+        __builtin_amdgcn_wave_barrier();
+        __asm__ __volatile__("" ::: "memory");
+    }
+}
+
+__global__ __launch_bounds__(1024) void bloom_apply_kernel(BloomBinArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    const uint32_t f = blockIdx.x, sl = blockIdx.y;
+    const uint64_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
+    const uint32_t nw32 = (uint32_t)((hi - lo + 63) / 64) * 2;
+    for (uint32_t i = threadIdx.x; i < nw32; i += blockDim.x) lds_bits[i] = 0;
+    __syncthreads();
+    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
+    const uint64_t base = (uint64_t)f * a.k * a.maxr;
+    const uint64_t cap = (uint64_t)a.k * (e - s);
+    const uint32_t n = a.cnt[2 * f + sl];
+    const uint32_t *src = a.pos + (sl ? base + cap - n : base);
+    // 16 independent loads per thread in flight per round (the loop would
+    // otherwise pay one memory latency per position).
+    constexpr uint32_t kU = 16;
+    for (uint32_t t0 = threadIdx.x; t0 < n; t0 += kU * blockDim.x) {
+        uint32_t q[kU];
+#pragma unroll
+        for (uint32_t j = 0; j < kU; j++) {
+            const uint32_t t = t0 + j * blockDim.x;
+            q[j] = t < n ? __builtin_nontemporal_load(&src[t]) - (uint32_t)lo : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kU; j++)
+            if (q[j] != 0xFFFFFFFFu) atomicOr(&lds_bits[q[j] >> 5], 1u << (q[j] & 31));
+    }
+    __syncthreads();
+    const uint64_t hdr = sst_header_bytes(a.koff, s, e);
+    store_filter_slice(lds_bits, lo / 64, (hi + 63) / 64, a.out + uni64(a.file_off[f]) + hdr + 32,
+                       nullptr);
 }
 
 // ---- .sst image writer ------------------------------------------------------
@@ -243,7 +768,6 @@ struct SstArgs {
     uint8_t *out;
     const uint64_t *file_off;
     int64_t *footer;
-    const uint64_t *bitmap;
     uint64_t m, nwords;
     uint32_t k;
 };
@@ -280,7 +804,7 @@ constexpr uint32_t kSstChunkRecs = kSstWaves * kWave;  // records per workgroup
 // Data region (V grammar) and index region (IDX grammar) of file blockIdx.x,
 // records chunk blockIdx.y.
 __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
-    __shared__ ChunkTable tables[kSstWaves];
+    __shared__ RegionLds lds[kSstWaves];
     const uint32_t f = blockIdx.x;
     const SstLayout L = sst_layout(a, f);
     const uint32_t wave = uni(threadIdx.x / kWave);
@@ -296,73 +820,45 @@ __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
     S.idx_base = (int64_t)L.data_off;
     S.rs = L.s;
     S.vrs = Vs;
-    encode_chunk<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
-                                 &tables[wave]);
-    encode_chunk<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
-                                   &tables[wave]);
+    encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
+                                    lds[wave].gather, nullptr, &lds[wave].ct);
+    encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
+                                      lds[wave].gather, nullptr, &lds[wave].ct);
 }
 
-// Header | filter block | footer of file blockIdx.x.  The header+filter
-// prefix [0, data_off) is cut into 4 KiB tiles over blockIdx.y; tile 0 also
-// writes the footer.
-constexpr uint32_t kMetaTile = 4096;
-
-__device__ __forceinline__ uint32_t meta_byte(const SstArgs &a, const SstLayout &L,
-                                              uint64_t fwords, uint64_t q) {
-    // Header: u32 kl0 | key[s] | u32 kl1 | key[e-1]   (header.go:25-37)
-    if (q < 4) return (L.kl0 >> (8 * q)) & 0xff;
-    if (q < 4 + (uint64_t)L.kl0) return a.keys[a.koff[L.s] + q - 4];
-    if (q < 8 + (uint64_t)L.kl0) return (L.kl1 >> (8 * (q - 4 - L.kl0))) & 0xff;
-    if (q < L.hdr) return a.keys[a.koff[L.e - 1] + q - 8 - L.kl0];
-    // Filter block (bloom.go:472-491): u64le L | u64be m | u64be k | u64be nbits | words be
-    uint64_t r = q - L.hdr;
-    uint64_t v;
-    uint32_t be;
-    if (r < 8) { v = 24 + 8 * a.nwords; return (uint32_t)(v >> (8 * r)) & 0xff; }
-    r -= 8;
-    uint64_t fi = r / 8, fb = r % 8;
-    if (fi == 0) v = a.m;
-    else if (fi == 1) v = a.k ? a.k : 1;
-    else if (fi == 2) v = a.m;
-    else v = a.bitmap[fwords + fi - 3];
-    be = (uint32_t)(v >> (8 * (7 - fb))) & 0xff;
-    return be;
-}
-
-__global__ __launch_bounds__(256) void sst_meta_kernel(SstArgs a) {
+// Header, filter-block prefix and footer of file blockIdx.x (one wave; byte
+// stores, since the neighbouring bytes belong to other kernels).  The filter
+// words themselves are stored by the bloom kernels.
+__global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) {
     const uint32_t f = blockIdx.x;
     const SstLayout L = sst_layout(a, f);
     uint8_t *img = a.out + uni64(a.file_off[f]);
-    const uint64_t fwords = (uint64_t)f * a.nwords;
-    const uint64_t t0 = (uint64_t)blockIdx.y * kMetaTile;
-    if (t0 < L.data_off) {
-        const uint64_t t1 = t0 + kMetaTile < L.data_off ? t0 + kMetaTile : L.data_off;
-        const uintptr_t base = reinterpret_cast<uintptr_t>(img) + t0;
-        const uint32_t head = (uint32_t)(base & 3);
-        uint32_t *dA = reinterpret_cast<uint32_t *>(base - head);
-        const uint64_t len = t1 - t0;
-        const uint64_t ndw = (head + len + 3) / 4;
-        for (uint64_t d = threadIdx.x; d < ndw; d += blockDim.x) {
-            const int64_t u0 = (int64_t)(4 * d) - head;
-            const bool full = u0 >= 0 && (uint64_t)u0 + 4 <= len;
-            uint32_t v = 0;
-            uint8_t *db = reinterpret_cast<uint8_t *>(dA + d);
-            for (uint32_t t = 0; t < 4; t++) {
-                int64_t u = u0 + t;
-                if (u < 0 || (uint64_t)u >= len) continue;
-                uint32_t byte = meta_byte(a, L, fwords, t0 + (uint64_t)u);
-                if (full) v |= byte << (8 * t);
-                else db[t] = (uint8_t)byte;
-            }
-            if (full) dA[d] = v;
-        }
+    const uint32_t lane = lane_id();
+    // Header (header.go:25-37): u32 kl0 | key[s] | u32 kl1 | key[e-1]
+    const uint64_t k0 = L.e > L.s ? uni64(a.koff[L.s]) : 0;
+    const uint64_t k1 = L.e > L.s ? uni64(a.koff[L.e - 1]) : 0;
+    for (uint64_t q = lane; q < L.hdr; q += kWave) {
+        uint32_t b;
+        if (q < 4) b = (L.kl0 >> (8 * q)) & 0xff;
+        else if (q < 4 + (uint64_t)L.kl0) b = a.keys[k0 + q - 4];
+        else if (q < 8 + (uint64_t)L.kl0) b = (L.kl1 >> (8 * (q - 4 - L.kl0))) & 0xff;
+        else b = a.keys[k1 + q - 8 - L.kl0];
+        img[q] = (uint8_t)b;
     }
-    if (blockIdx.y == 0 && threadIdx.x < 32) {
+    // Filter prefix (bloom.go:472-491): u64le 24+8*nwords | u64be m | u64be k | u64be nbits
+    if (lane < 32) {
+        const uint32_t fi = lane / 8, fb = lane % 8;
+        uint32_t b;
+        if (fi == 0) b = (uint32_t)((24 + 8 * a.nwords) >> (8 * fb)) & 0xff;
+        else {
+            const uint64_t v = fi == 2 ? (uint64_t)a.k : a.m;
+            b = (uint32_t)(v >> (8 * (7 - fb))) & 0xff;
+        }
+        img[L.hdr + lane] = (uint8_t)b;
         // Footer (footer.go:43-55): dataOff, dataSize, idxOff, idxSize (i64le)
-        const uint32_t t = threadIdx.x;
         const uint64_t vals[4] = {L.data_off, L.data_size, L.idx_off, L.idx_size};
-        img[L.img - 32 + t] = (uint8_t)(vals[t / 8] >> (8 * (t % 8)));
-        if (a.footer && t < 4) a.footer[4 * (uint64_t)f + t] = (int64_t)vals[t];
+        img[L.img - 32 + lane] = (uint8_t)(vals[lane / 8] >> (8 * (lane % 8)));
+        if (a.footer && lane < 4) a.footer[4 * (uint64_t)f + lane] = (int64_t)vals[lane];
     }
 }
 
@@ -390,7 +886,7 @@ __global__ __launch_bounds__(256) void bloom_probe_kernel(const uint64_t *words,
     sum256(keys + k0, koff[i + 1] - k0, h);
     uint8_t ok = 1;
     for (uint32_t j = 0; j < k && ok; j++) {
-        uint64_t p = mod_barrett(location(h, j), m, mrecip);
+        uint64_t p = mod_barrett(location(h[0], h[1], h[2], h[3], j), m, mrecip);
         if (!((words[p >> 6] >> (p & 63)) & 1)) ok = 0;
     }
     hit[i] = ok;
@@ -496,9 +992,19 @@ extern "C" uint64_t lsm_sst_image_size_host(const uint64_t *koff, const uint64_t
            lsm_encoded_size_host(LSM_GRAMMAR_IDX, koff, voff, r0, r1) + 32;
 }
 
-extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint64_t m) {
-    uint64_t nw = (m + 63) / 64;
-    return (size_t)(nfile ? nfile : 1) * (nw ? nw : 1) * 8;
+// The binned bloom path covers filters of exactly two LDS slices with 32-bit
+// bit positions (go-lsm's 1.6 Mbit default); anything else hashes per slice.
+static bool binned_bloom(uint64_t m) {
+    const uint64_t sb = slice_bits_for(m);
+    return m < (1ull << 32) && (m + sb - 1) / sb == 2;
+}
+
+extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
+                                                uint64_t m, uint32_t k) {
+    if (!binned_bloom(m)) return 16;
+    const uint64_t kk = k ? k : 1;
+    const uint64_t cnt = ((uint64_t)(nfile ? nfile : 1) * 2 * 4 + 255) & ~255ull;
+    return (size_t)(cnt + kk * nfile * (uint64_t)max_file_records * 4 + 16);
 }
 
 static uint64_t barrett_recip(uint64_t m) { return ~0ull / m; }
@@ -513,26 +1019,57 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
     if (nfile == 0) return 0;
     if (!d_keys || !d_koff || !d_vals || !d_voff || !d_file_start || !d_out || !d_file_off)
         return LSM_EINVAL;
-    if (ws_bytes < lsm_build_sst_workspace_bytes(nfile, m) || !d_workspace) return LSM_ESPACE;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint64_t nwords = (m + 63) / 64;
     const uint32_t kk = k ? k : 1;  // NewBloomFilter max(1, k) bloom.go:95-101
+    const uint32_t chunks = (max_file_records + kSstChunkRecs - 1) / kSstChunkRecs;
 
-    BloomArgs b;
-    b.keys = d_keys;
-    b.koff = d_koff;
-    b.file_start = d_file_start;
-    b.m = m;
-    b.mrecip = barrett_recip(m);
-    b.k = kk;
-    b.slice_bits = slice_bits_for(m);
-    b.nwords = nwords;
-    b.bitmap = static_cast<uint64_t *>(d_workspace);
-    b.nkeys = 0;
-    const uint32_t nslices = (uint32_t)((m + b.slice_bits - 1) / b.slice_bits);
-    const size_t lds = (size_t)(b.slice_bits / 8);
-    hipLaunchKernelGGL(bloom_slices_kernel, dim3(nfile, nslices), dim3(1024), lds, s, b);
-    LSM_HIP_CHECK(hipGetLastError());
+    // Bloom: filter words go straight into each image (big-endian).
+    const uint64_t sb = slice_bits_for(m);
+    if (binned_bloom(m)) {
+        const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
+        if (!d_workspace || ws_bytes < need) return LSM_ESPACE;
+        BloomBinArgs b;
+        b.keys = d_keys;
+        b.koff = d_koff;
+        b.file_start = d_file_start;
+        b.m = m;
+        b.mrecip = barrett_recip(m);
+        b.k = kk;
+        b.split = (uint32_t)sb;
+        b.maxr = max_file_records;
+        const size_t cnt_bytes = ((size_t)nfile * 2 * 4 + 255) & ~(size_t)255;
+        b.cnt = static_cast<uint32_t *>(d_workspace);
+        b.pos = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) + cnt_bytes);
+        b.out = d_out;
+        b.file_off = d_file_off;
+        b.nwords = nwords;
+        LSM_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)nfile * 2 * 4, s));
+        const uint32_t bchunks = (max_file_records + kBinWaves * kWave - 1) / (kBinWaves * kWave);
+        if (bchunks) {
+            hipLaunchKernelGGL(bloom_bin_kernel, dim3(nfile, bchunks), dim3(kBinWaves * kWave), 0, s, b);
+            LSM_HIP_CHECK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(bloom_apply_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, b);
+        LSM_HIP_CHECK(hipGetLastError());
+    } else {
+        BloomArgs b;
+        b.keys = d_keys;
+        b.koff = d_koff;
+        b.file_start = d_file_start;
+        b.m = m;
+        b.mrecip = barrett_recip(m);
+        b.k = kk;
+        b.slice_bits = sb;
+        b.nwords = nwords;
+        b.bitmap = nullptr;
+        b.nkeys = 0;
+        b.out = d_out;
+        b.file_off = d_file_off;
+        const uint32_t nslices = (uint32_t)((m + sb - 1) / sb);
+        hipLaunchKernelGGL(bloom_slices_kernel, dim3(nfile, nslices), dim3(1024), (size_t)(sb / 8), s, b);
+        LSM_HIP_CHECK(hipGetLastError());
+    }
 
     SstArgs a;
     a.keys = d_keys;
@@ -543,22 +1080,14 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
     a.out = d_out;
     a.file_off = d_file_off;
     a.footer = d_footer;
-    a.bitmap = b.bitmap;
     a.m = m;
     a.nwords = nwords;
     a.k = kk;
-    const uint32_t chunks = (max_file_records + kSstChunkRecs - 1) / kSstChunkRecs;
     if (chunks) {
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, chunks), dim3(256), 0, s, a);
         LSM_HIP_CHECK(hipGetLastError());
     }
-    // header + filter tiles: the key lengths of the header are data-dependent;
-    // bound the prefix by the max header (2 keys <= 2 * 2^20 + 8 is the
-    // decode cap, but in practice keys are short) -- use the filter size plus
-    // a generous header allowance and let tiles past data_off exit.
-    const uint64_t prefix_max = lsm_filter_block_size(m) + 8 + 2 * 65536;
-    const uint32_t tiles = (uint32_t)((prefix_max + kMetaTile - 1) / kMetaTile);
-    hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile, tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -605,6 +1134,8 @@ extern "C" int lsm_bloom_build(lsm_ctx *ctx, const uint8_t *d_keys, const uint64
     b.nwords = (m + 63) / 64;
     b.bitmap = d_words;
     b.nkeys = nkeys;
+    b.out = nullptr;
+    b.file_off = nullptr;
     const uint32_t nslices = (uint32_t)((m + b.slice_bits - 1) / b.slice_bits);
     hipLaunchKernelGGL(bloom_slices_kernel, dim3(1, nslices), dim3(1024),
                        (size_t)(b.slice_bits / 8), static_cast<hipStream_t>(stream), b);

@@ -92,11 +92,14 @@ __device__ __forceinline__ void sum256(const uint8_t *key, uint64_t len, uint64_
     }
 }
 
-// location(h, i) before the modulo (bloom.go:133-136).
-__device__ __forceinline__ uint64_t location(const uint64_t h[4], uint32_t i) {
-    uint32_t m4 = i & 3;
-    uint64_t a = (m4 & 1) ? h[1] : h[0];
-    uint64_t b = (m4 == 0 || m4 == 3) ? h[2] : h[3];
+// location(h, i) before the modulo (bloom.go:133-136).  Scalar arguments:
+// selecting among array elements by a runtime index would spill the digest
+// to scratch.
+__device__ __forceinline__ uint64_t location(uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3,
+                                             uint32_t i) {
+    const uint32_t m4 = i & 3;
+    const uint64_t a = (m4 & 1) ? h1 : h0;
+    const uint64_t b = (m4 == 0 || m4 == 3) ? h2 : h3;
     return a + (uint64_t)i * b;
 }
 

@@ -531,7 +531,7 @@ Error SSTable::EncodeImage(Bytes *out) {
         void *d_fo = d.Dev(5, 8);
         void *d_out = d.Dev(6, pad16(size));
         void *d_foot = d.Dev(7, 32);
-        const size_t ws = lsm_build_sst_workspace_bytes(1, m);
+        const size_t ws = lsm_build_sst_workspace_bytes(1, (uint32_t)n, m, (uint32_t)k);
         void *d_ws = d.Dev(8, ws);
         if (!keys.empty()) d.H2D(d_keys, keys.data(), keys.size());
         d.H2D(d_koff, koff.data(), koff.size() * 8);
@@ -755,7 +755,7 @@ std::vector<Bytes> BuildImages(const std::vector<kv::KeyValuePair> &sorted, uint
     void *d_fs = d.Dev(4, fs.size() * 8);
     void *d_fo = d.Dev(5, fo.size() * 8);
     void *d_out = d.Dev(6, pad16(total));
-    const size_t ws = lsm_build_sst_workspace_bytes((uint32_t)nf, m);
+    const size_t ws = lsm_build_sst_workspace_bytes((uint32_t)nf, (uint32_t)maxr, m, (uint32_t)k);
     void *d_ws = d.Dev(8, ws);
     if (!keys.empty()) d.H2D(d_keys, keys.data(), keys.size());
     d.H2D(d_koff, koff.data(), koff.size() * 8);

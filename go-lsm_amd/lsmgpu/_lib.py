@@ -57,7 +57,8 @@ SIGNATURES = {
     "lsm_sst_image_size_host": (ctypes.c_uint64, [c_u64p, c_u64p, ctypes.c_uint64,
                                                   ctypes.c_uint64, ctypes.c_uint64]),
     "lsm_filter_block_size": (ctypes.c_uint64, [ctypes.c_uint64]),
-    "lsm_build_sst_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint64]),
+    "lsm_build_sst_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint32,
+                                                         ctypes.c_uint64, ctypes.c_uint32]),
     "lsm_build_sst": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u8p, c_u64p, c_u64p,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                      ctypes.c_uint32, c_u8p, c_u64p, ctypes.c_void_p,

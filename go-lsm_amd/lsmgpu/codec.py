@@ -359,8 +359,8 @@ def prepare_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
     if nf:
         file_off[1:] = np.cumsum(padded)[:-1]
     total = int(padded.sum())
-    ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nf, m))
     max_recs = int(np.diff(file_start.astype(np.int64)).max()) if nf else 0
+    ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nf, max_recs, m, k))
     return SstBuild(
         out=torch.zeros(pad16(total), dtype=torch.uint8, device=dev),
         file_start=file_start, file_off=file_off, file_size=sizes,

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 1
+#define LSM_ABI_VERSION 2
 
 /* Record grammars (all fixed-width little-endian). */
 enum lsm_grammar {
@@ -177,7 +177,12 @@ uint64_t lsm_sst_image_size_host(const uint64_t *koff, const uint64_t *voff, uin
                                  uint64_t r1, uint64_t m);
 /* Filter block bytes for m bits: 8 + 24 + 8*ceil(m/64) (bloom.go:472-491). */
 uint64_t lsm_filter_block_size(uint64_t m);
-size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint64_t m);
+/* Device workspace lsm_build_sst needs for nfile files of at most
+ * max_file_records records each: the bloom's binned bit positions (k u32 per
+ * record) when the filter splits into two LDS slices (go-lsm's default m),
+ * else a token 16 bytes. */
+size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records, uint64_t m,
+                                     uint32_t k);
 
 /* Build nfile .sst images: file f holds records [file_start[f], file_start[f+1])
  * and its image (Header | Filter | V data | IDX index | Footer) is written at
@@ -185,9 +190,10 @@ size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint64_t m);
  * SSTable.Add (sstable.go:322-326), bloom Filter.Add (bloom.go:175-181,
  * murmur.go:245-275) and SSTable.EncodeTo (sstable.go:131-193).  The bloom
  * (m bits, k hashes; go-lsm default 1,600,000 / 16, bloom.go:79-82) is
- * built in LDS slices and fused into the image.  d_footer (optional) gets
- * {dataOff, dataSize, idxOff, idxSize} per file.  max_file_records bounds
- * the grid (largest file_start[f+1]-file_start[f]).  Requires m >= 1. */
+ * built in LDS slices and its words are stored straight into each image.
+ * d_footer (optional) gets {dataOff, dataSize, idxOff, idxSize} per file.
+ * max_file_records must be >= every file_start[f+1]-file_start[f] (it sizes
+ * the grid and the workspace).  Requires m >= 1. */
 int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
                   const uint8_t *d_vals, const uint64_t *d_voff, const uint64_t *d_file_start,
                   uint32_t nfile, uint32_t max_file_records, uint64_t m, uint32_t k,

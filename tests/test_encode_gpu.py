@@ -155,7 +155,8 @@ def test_sst_reference_fixtures(ctx):
     assert np.array_equal(sb.out.cpu().numpy()[: ORV["sst_iter"].size], ORV["sst_iter"])
 
 
-@pytest.mark.parametrize("m,k", [(1, 1), (63, 3), (64, 0), (65, 5), (1000, 4), (1_600_000, 16),
+@pytest.mark.parametrize("m,k", [(1, 1), (63, 3), (64, 0), (65, 5), (1000, 4), (819_200, 2),
+                                 (819_201, 3), (1_000_003, 20), (1_600_000, 16), (1_638_400, 33),
                                  (1_638_401, 7)])
 def test_sst_random_params(ctx, m, k):
     rng = np.random.default_rng(m + k)

@@ -54,3 +54,89 @@ extern "C" int probe_copy(const void *in, void *out, uint64_t nbytes, int grid, 
                        (const u32x4 *)in, (u32x4 *)out, nbytes / 16);
     return (int)hipGetLastError();
 }
+
+// ---- block-shaped probes (decode4k's memory pattern without the parse) ------
+// Each wave stages one 4 KiB block into LDS by four 1 KiB LDS-DMAs, waits,
+// and writes 33 x 16 B descriptors (the DESC output of a 33-record block).
+template <int WPG, bool META, int LAUX = 0, bool NTST = false>
+__global__ __launch_bounds__(64 * WPG) void blocks_dma(const uint8_t *in, const uint64_t *off,
+                                                      const uint32_t *len, uint32_t nblk, u32x4 *out) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[WPG][1024];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x * WPG + wave;
+    if (b >= nblk) return;
+    uint64_t o = (uint64_t)b * 4096;
+    uint32_t n = 4096;
+    if (META) {
+        o = __builtin_amdgcn_readfirstlane((uint32_t)off[b]) |
+            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off[b] >> 32)) << 32;
+        n = __builtin_amdgcn_readfirstlane(len[b]);
+    }
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(in + o), 0, n, 0x00020000);
+    for (int k = 0; k < 4; k++)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)&buf[wave][k * 256], 16, k * 1024 + lane * 16, 0, 0, LAUX);
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t v = buf[wave][lane * 31 % 1024];
+    if (lane < 33) {
+        u32x4 d = {v, (uint32_t)o, lane, 100};
+        if (NTST) __builtin_nontemporal_store(d, &out[(uint64_t)b * 33 + lane]);
+        else out[(uint64_t)b * 33 + lane] = d;
+    }
+}
+
+// Persistent, double-buffered: wave w walks blocks w, w+W, ...; block k+1's
+// DMAs are in flight while block k is "processed".
+template <int WPG>
+__global__ __launch_bounds__(64 * WPG) void blocks_dma_db(const uint8_t *in, uint32_t nblk, u32x4 *out) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[WPG][2][1024];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t W = gridDim.x * WPG;
+    uint32_t b = blockIdx.x * WPG + wave;
+    if (b >= nblk) return;
+    auto stage = [&](uint32_t bb, uint32_t slot) {
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(in + (uint64_t)bb * 4096), 0, 4096, 0x00020000);
+        for (int k = 0; k < 4; k++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)&buf[wave][slot][k * 256], 16, k * 1024 + lane * 16, 0, 0, 0);
+    };
+    stage(b, 0);
+    for (uint32_t k = 0;; k++) {
+        const uint32_t nb = b + W;
+        if (nb < nblk) {
+            stage(nb, (k + 1) & 1);
+            __asm__ __volatile__("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint32_t v = buf[wave][k & 1][lane * 31 % 1024];
+        if (lane < 33) {
+            u32x4 d = {v, b, lane, 100};
+            out[(uint64_t)b * 33 + lane] = d;
+        }
+        if (nb >= nblk) break;
+        b = nb;
+    }
+}
+
+extern "C" int probe_blocks(int mode, const void *in, const uint64_t *off, const uint32_t *len,
+                            uint32_t nblk, void *out, int grid, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    u32x4 *o = (u32x4 *)out;
+    const uint8_t *i = (const uint8_t *)in;
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((blocks_dma<4, false>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    case 1: hipLaunchKernelGGL((blocks_dma<4, true>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    case 2: hipLaunchKernelGGL((blocks_dma<1, true>), dim3(nblk), dim3(64), 0, s, i, off, len, nblk, o); break;
+    case 3: hipLaunchKernelGGL((blocks_dma<8, true>), dim3((nblk + 7) / 8), dim3(512), 0, s, i, off, len, nblk, o); break;
+    case 4: hipLaunchKernelGGL((blocks_dma_db<4>), dim3(grid), dim3(256), 0, s, i, nblk, o); break;
+    case 5: hipLaunchKernelGGL((blocks_dma_db<1>), dim3(grid), dim3(64), 0, s, i, nblk, o); break;
+    case 6: hipLaunchKernelGGL((blocks_dma<4, true, 0, true>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    case 7: hipLaunchKernelGGL((blocks_dma<4, true, 2, false>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    case 8: hipLaunchKernelGGL((blocks_dma<4, true, 2, true>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    case 9: hipLaunchKernelGGL((blocks_dma<4, true, 1, false>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    case 10: hipLaunchKernelGGL((blocks_dma<4, true, 17, true>), dim3((nblk + 3) / 4), dim3(256), 0, s, i, off, len, nblk, o); break;
+    default: return -1;
+    }
+    return (int)hipGetLastError();
+}
