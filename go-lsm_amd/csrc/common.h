@@ -54,6 +54,11 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t s)
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// Number of set bits of m in the lanes below this one.
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
 // Exclusive wave prefix sum (64 lanes) of a 32-bit value.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
     uint32_t lane = lane_id();

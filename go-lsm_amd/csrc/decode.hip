@@ -436,8 +436,8 @@ __global__ __launch_bounds__(64 * WPG) void decode_spec_kernel(DecodeArgs a) {
     for (uint32_t k = 0; k < K; k++) {
         const uint32_t b = b0 + k;
         if (b >= a.nblk) break;
-        const uint64_t off = uni64(__builtin_amdgcn_readlane((uint32_t)moff, k) |
-                                   (uint64_t)__builtin_amdgcn_readlane((uint32_t)(moff >> 32), k) << 32);
+        const uint64_t off = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)moff, k) |
+                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(moff >> 32), k) << 32);
         const uint32_t n = __builtin_amdgcn_readlane(mlen, k);
         decode_block_spec<G>(a, b, ring[wave], off, n);
     }
@@ -479,8 +479,8 @@ __global__ __launch_bounds__(64) void decode_group_kernel(DecodeArgs a) {
     const uint64_t small_mask = __ballot(small);
     for (uint32_t j = 0; j < NB; j++) {
         if (!((small_mask >> (j * H)) & 1)) continue;
-        const uint64_t offj = uni64(__builtin_amdgcn_readlane((uint32_t)off, j * H) |
-                                    (uint64_t)__builtin_amdgcn_readlane((uint32_t)(off >> 32), j * H) << 32);
+        const uint64_t offj = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)off, j * H) |
+                                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(off >> 32), j * H) << 32);
         const uint32_t nj = __builtin_amdgcn_readlane(n, j * H);
         const uint64_t a0 = offj & ~(uint64_t)15;
         const uint32_t tot = (uint32_t)(((offj - a0) + nj + 15) & ~(uint64_t)15);

@@ -16,6 +16,8 @@
 // hashes every key of the file (sum256 + 16 locations + Barrett modulo) and
 // ds_or's the bits that fall in its slice; the slice is then stored once.
 // No global atomics.
+#include <stdlib.h>
+
 #include "common.h"
 #include "murmur.h"
 
@@ -289,6 +291,7 @@ __device__ bool encode_chunk_staged(const RegionSrc &S, uint64_t c0, uint32_t cn
     }
     uint32_t tot;
     const uint32_t P = wave_excl_scan(sz, &tot);
+    tot = uni(tot);
     if (lane < cnt) {
         L->tb.P[lane] = P;
         L->tb.ks[lane] = ks;
@@ -384,6 +387,7 @@ __device__ bool encode_chunk_staged(const RegionSrc &S, uint64_t c0, uint32_t cn
 // the 4-byte prefix sits between).  The image is stored with aligned 16-byte
 // stores (ds_read_b128 + funnel shift), chunk-edge bytes singly.
 constexpr uint32_t kGatherDwords = 1856;  // 7.25 KiB per wave
+constexpr uint32_t kGatherMaskWords = kWave;  // one per lane; >= 2 * ceil(kGatherDwords / 64)
 
 template <int G>
 __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint8_t *dst,
@@ -404,6 +408,7 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
     }
     uint64_t tot64;
     const uint64_t P64 = wave_excl_scan64(lane < cnt ? pre + len : 0, &tot64);
+    tot64 = uni64(tot64);  // wave-uniform: keeps the loops below scalar
     const uint32_t ph = (uint32_t)(Sc & 3);
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
     if (tot64 + 64 > 4ull * kGatherDwords) return false;
@@ -415,18 +420,33 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
     if (OD + ((nD + 63) & ~63u) + 8 > kGatherDwords) return false;
 
     // gather: image dword D covers chunk bytes [4D - ph, 4D - ph + 4)
-    const uint32_t Pl = lane < cnt ? P : 0xFFFFFFFFu;
     const uint32_t sbytes = (uint32_t)(soff[c0 + cnt] - Sc);  // wave-uniform load below
     const rsrc_t rs = make_rsrc(sbase + (Sc - ph), uni((sbytes + ph + 3) & ~3u));
+    // Record of image dword D (its first byte x0 = 4D - ph): the number of
+    // record starts t >= 1 with P[t] <= x0, i.e. with e_t = ceil((P[t]+ph)/4)
+    // <= D.  Records are >= 4 bytes, so the e_t are distinct: one bit each
+    // in an LDS mask, and window i (dwords [64i, 64i+64)) reads its 64-bit
+    // word once -- a lane's record is the running count plus a masked
+    // popcount (mbcnt), no search.
+    uint32_t *mask = lds + kGatherDwords;  // kGatherMaskWords after the image
+    for (uint32_t w = lane; w < kGatherMaskWords; w += kWave) mask[w] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    if (lane >= 1 && lane < cnt) {
+        const uint32_t et = (P + ph + 3) >> 2;
+        atomicOr(&mask[et >> 5], 1u << (et & 31));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    uint32_t rb = 0;
+    const uint32_t mv = mask[lane];  // lane w holds mask word w (64 words)
     for (uint32_t i = 0; i * kWave < nD; i++) {
-        const int32_t x0 = 4 * (int32_t)(i * kWave + lane) - (int32_t)ph;
-        const uint32_t x = x0 < 0 ? 0u : (uint32_t)x0;
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t st = 32; st; st >>= 1) {
-            const uint32_t Pc = __builtin_amdgcn_ds_bpermute((int)((r + st) << 2), (int)Pl);
-            if (Pc <= x) r += st;
-        }
+        const int32_t x0 = 256 * (int32_t)i + 4 * (int32_t)lane - (int32_t)ph;
+        // (readlane returns int: cast to u32 before widening, no sign extension)
+        const uint64_t M = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(mv, 2 * i + 1) << 32 |
+                           (uint32_t)__builtin_amdgcn_readlane(mv, 2 * i);
+        const uint32_t r = rb + mbcnt(M) + (uint32_t)((M >> lane) & 1);
+        rb += (uint32_t)__builtin_popcountll(M);
         const uint32_t voff = (uint32_t)(x0 - (int32_t)(pre * r) - 4 + (int32_t)ph);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rs, (__attribute__((address_space(3))) void *)&lds[OD + i * kWave], 4, voff, 0, 0, 2);
@@ -480,11 +500,11 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
 union EncodeLds {
     StageLds st;
     ChunkTable ct;
-    uint32_t gather[kGatherDwords];
+    uint32_t gather[kGatherDwords + kGatherMaskWords];
 };
 union RegionLds {  // V / IDX only: no KV stage
     ChunkTable ct;
-    uint32_t gather[kGatherDwords];
+    uint32_t gather[kGatherDwords + kGatherMaskWords];
 };
 
 // Chunk encoder dispatch: DMA gather (V / IDX), LDS-staged (KV), then the
@@ -672,9 +692,6 @@ struct BinLds {
     uint32_t s0[kBinBatch * kWave], s1[kBinBatch * kWave];
 };
 
-__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-}
 
 __global__ __launch_bounds__(64 * kBinWaves) void bloom_bin_kernel(BloomBinArgs a) {
     __shared__ BinLds lds[kBinWaves];
@@ -686,10 +703,11 @@ __global__ __launch_bounds__(64 * kBinWaves) void bloom_bin_kernel(BloomBinArgs 
     const uint32_t lane = lane_id();
     const uint64_t i = c0 + lane;
     const bool act = i < e;
-    uint64_t h[4] = {0, 0, 0, 0};
-    if (act) {
-        const uint64_t k0 = a.koff[i];
-        sum256(a.keys + k0, a.koff[i + 1] - k0, h);
+    uint64_t h[4];
+    {
+        const uint64_t ii = act ? i : e - 1;  // unconditional loads (no per-load drain)
+        const uint64_t k0 = a.koff[ii];
+        sum256(a.keys + k0, a.koff[ii + 1] - k0, h);
     }
     const uint64_t base = (uint64_t)f * a.k * a.maxr;
     const uint64_t cap = (uint64_t)a.k * (e - s);
@@ -737,24 +755,124 @@ __global__ __launch_bounds__(1024) void bloom_apply_kernel(BloomBinArgs a) {
     const uint64_t cap = (uint64_t)a.k * (e - s);
     const uint32_t n = a.cnt[2 * f + sl];
     const uint32_t *src = a.pos + (sl ? base + cap - n : base);
-    // 16 independent loads per thread in flight per round (the loop would
-    // otherwise pay one memory latency per position).
+    // 16 independent loads per thread in flight per round.  Loads past the
+    // bin are clamped to its last position (OR-ing a bit twice is harmless):
+    // an unconditional load needs no per-load wait, a guarded one would make
+    // the compiler drain vmcnt after each.
     constexpr uint32_t kU = 16;
     for (uint32_t t0 = threadIdx.x; t0 < n; t0 += kU * blockDim.x) {
         uint32_t q[kU];
 #pragma unroll
         for (uint32_t j = 0; j < kU; j++) {
             const uint32_t t = t0 + j * blockDim.x;
-            q[j] = t < n ? __builtin_nontemporal_load(&src[t]) - (uint32_t)lo : 0xFFFFFFFFu;
+            q[j] = __builtin_nontemporal_load(&src[t < n ? t : n - 1]) - (uint32_t)lo;
         }
 #pragma unroll
-        for (uint32_t j = 0; j < kU; j++)
-            if (q[j] != 0xFFFFFFFFu) atomicOr(&lds_bits[q[j] >> 5], 1u << (q[j] & 31));
+        for (uint32_t j = 0; j < kU; j++) atomicOr(&lds_bits[q[j] >> 5], 1u << (q[j] & 31));
     }
     __syncthreads();
     const uint64_t hdr = sst_header_bytes(a.koff, s, e);
     store_filter_slice(lds_bits, lo / 64, (hi + 63) / 64, a.out + uni64(a.file_off[f]) + hdr + 32,
                        nullptr);
+}
+
+// ---- per-file bloom build, hash once (one or two slices, m < 2^32) -----------
+//
+// One 1024-thread workgroup per filter holds slice 0 (the first <= 100 KiB of
+// bits) in LDS.  It hashes each key of its filter exactly once: bits in slice
+// 0 are ds_or'ed at once, bits in slice 1 are appended to the filter's own
+// workspace list (wave-aggregated: one LDS counter add per location index
+// and a coalesced store).  Slice 0 is then stored, the LDS re-zeroed, and
+// the list -- just written by this workgroup, read back through L2 with nt
+// loads -- OR'ed in as slice 1.  No cross-workgroup dependency, no global
+// atomics, and the hash (the VALU-bound part) is done once per key.
+struct BloomFileArgs {
+    const uint8_t *keys;
+    const uint64_t *koff;
+    const uint64_t *file_start;  // null: one filter over keys [0, nkeys)
+    uint64_t nkeys;
+    uint64_t m, mrecip;
+    uint32_t k;
+    uint32_t split;   // slice 0 = bits [0, split); split >= m: one slice
+    uint32_t *pos;    // slice-1 list of filter f at f * k * maxr (two slices only)
+    uint32_t maxr;
+    uint64_t nwords;
+    uint8_t *out;     // image mode
+    const uint64_t *file_off;
+    uint64_t *bitmap; // native mode (out == null)
+};
+
+__global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    __shared__ uint32_t n1;
+    const uint32_t f = blockIdx.x;
+    const uint32_t lane = lane_id();
+    const uint64_t s = a.file_start ? uni64(a.file_start[f]) : 0;
+    const uint64_t e = a.file_start ? uni64(a.file_start[f + 1]) : a.nkeys;
+    const bool two = a.split < a.m;
+    const uint64_t lo1 = two ? a.split : a.m;  // end of slice 0
+    const uint32_t nw0 = (uint32_t)((lo1 + 63) / 64) * 2;
+    for (uint32_t i = threadIdx.x; i < nw0; i += blockDim.x) lds_bits[i] = 0;
+    if (threadIdx.x == 0) n1 = 0;
+    __syncthreads();
+    uint32_t *list = two ? a.pos + (uint64_t)f * a.k * a.maxr : nullptr;
+    for (uint64_t i0 = s + (threadIdx.x & ~63u); i0 < e; i0 += blockDim.x) {
+        const uint64_t i = i0 + lane;
+        const bool act = i < e;
+        uint64_t h[4];
+        {
+            const uint64_t ii = act ? i : e - 1;  // unconditional loads
+            const uint64_t k0 = a.koff[ii];
+            sum256(a.keys + k0, a.koff[ii + 1] - k0, h);
+        }
+        for (uint32_t j = 0; j < a.k; j++) {
+            const uint32_t p = (uint32_t)mod_barrett(location(h[0], h[1], h[2], h[3], j), a.m, a.mrecip);
+            const bool in1 = act && p >= lo1;
+            if (act && !in1) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
+            if (two) {
+                const uint64_t b1 = __ballot(in1);
+                if (b1) {
+                    uint32_t o = 0;
+                    if (lane == 0) o = atomicAdd(&n1, (uint32_t)__builtin_popcountll(b1));
+                    o = uni(o);
+                    if (in1) list[o + mbcnt(b1)] = p;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (a.out) {
+        const uint64_t hdr = sst_header_bytes(a.koff, s, e);
+        store_filter_slice(lds_bits, 0, (lo1 + 63) / 64, a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+    } else {
+        store_filter_slice(lds_bits, 0, (lo1 + 63) / 64, nullptr, a.bitmap + (uint64_t)f * a.nwords);
+    }
+    if (!two) return;
+    // slice 1 from this workgroup's own list
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t nw1 = (uint32_t)((a.m - lo1 + 63) / 64) * 2;
+    for (uint32_t i = threadIdx.x; i < nw1; i += blockDim.x) lds_bits[i] = 0;
+    __syncthreads();
+    const uint32_t n = n1;
+    constexpr uint32_t kU = 16;
+    for (uint32_t t0 = threadIdx.x; t0 < n; t0 += kU * blockDim.x) {
+        uint32_t q[kU];
+#pragma unroll
+        for (uint32_t j = 0; j < kU; j++) {
+            const uint32_t t = t0 + j * blockDim.x;
+            q[j] = __builtin_nontemporal_load(&list[t < n ? t : n - 1]) - (uint32_t)lo1;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kU; j++) atomicOr(&lds_bits[q[j] >> 5], 1u << (q[j] & 31));
+    }
+    __syncthreads();
+    if (a.out) {
+        const uint64_t hdr = sst_header_bytes(a.koff, s, e);
+        store_filter_slice(lds_bits, lo1 / 64, a.nwords, a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+    } else {
+        store_filter_slice(lds_bits, lo1 / 64, a.nwords, nullptr, a.bitmap + (uint64_t)f * a.nwords);
+    }
 }
 
 // ---- .sst image writer ------------------------------------------------------
@@ -770,6 +888,7 @@ struct SstArgs {
     int64_t *footer;
     uint64_t m, nwords;
     uint32_t k;
+    uint32_t dbg;  // diagnostics only: bit 0 skips the V region, bit 1 the IDX region
 };
 
 struct SstLayout {
@@ -820,10 +939,12 @@ __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
     S.idx_base = (int64_t)L.data_off;
     S.rs = L.s;
     S.vrs = Vs;
-    encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
-                                    lds[wave].gather, nullptr, &lds[wave].ct);
-    encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
-                                      lds[wave].gather, nullptr, &lds[wave].ct);
+    if (!(a.dbg & 1))
+        encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
+                                        lds[wave].gather, nullptr, &lds[wave].ct);
+    if (!(a.dbg & 2))
+        encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
+                                          lds[wave].gather, nullptr, &lds[wave].ct);
 }
 
 // Header, filter-block prefix and footer of file blockIdx.x (one wave; byte
@@ -992,16 +1113,17 @@ extern "C" uint64_t lsm_sst_image_size_host(const uint64_t *koff, const uint64_t
            lsm_encoded_size_host(LSM_GRAMMAR_IDX, koff, voff, r0, r1) + 32;
 }
 
-// The binned bloom path covers filters of exactly two LDS slices with 32-bit
-// bit positions (go-lsm's 1.6 Mbit default); anything else hashes per slice.
-static bool binned_bloom(uint64_t m) {
+// Filters of one or two LDS slices with 32-bit bit positions (go-lsm's 1.6
+// Mbit default is two) hash each key once; larger ones hash per slice.
+static uint32_t bloom_slices(uint64_t m) {
     const uint64_t sb = slice_bits_for(m);
-    return m < (1ull << 32) && (m + sb - 1) / sb == 2;
+    return (uint32_t)((m + sb - 1) / sb);
 }
+static bool hash_once_bloom(uint64_t m) { return m < (1ull << 32) && bloom_slices(m) <= 2; }
 
 extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
                                                 uint64_t m, uint32_t k) {
-    if (!binned_bloom(m)) return 16;
+    if (!hash_once_bloom(m) || bloom_slices(m) < 2) return 16;
     const uint64_t kk = k ? k : 1;
     const uint64_t cnt = ((uint64_t)(nfile ? nfile : 1) * 2 * 4 + 255) & ~255ull;
     return (size_t)(cnt + kk * nfile * (uint64_t)max_file_records * 4 + 16);
@@ -1026,32 +1148,57 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
 
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
-    if (binned_bloom(m)) {
+    if (hash_once_bloom(m)) {
         const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
-        if (!d_workspace || ws_bytes < need) return LSM_ESPACE;
-        BloomBinArgs b;
-        b.keys = d_keys;
-        b.koff = d_koff;
-        b.file_start = d_file_start;
-        b.m = m;
-        b.mrecip = barrett_recip(m);
-        b.k = kk;
-        b.split = (uint32_t)sb;
-        b.maxr = max_file_records;
-        const size_t cnt_bytes = ((size_t)nfile * 2 * 4 + 255) & ~(size_t)255;
-        b.cnt = static_cast<uint32_t *>(d_workspace);
-        b.pos = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) + cnt_bytes);
-        b.out = d_out;
-        b.file_off = d_file_off;
-        b.nwords = nwords;
-        LSM_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)nfile * 2 * 4, s));
-        const uint32_t bchunks = (max_file_records + kBinWaves * kWave - 1) / (kBinWaves * kWave);
-        if (bchunks) {
-            hipLaunchKernelGGL(bloom_bin_kernel, dim3(nfile, bchunks), dim3(kBinWaves * kWave), 0, s, b);
+        if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
+        // LSM_BLOOM_PATH=1 selects the two-kernel binned variant (A/B only).
+        static const int path = [] {
+            const char *e = getenv("LSM_BLOOM_PATH");
+            return e ? atoi(e) : 0;
+        }();
+        if (path == 0 || bloom_slices(m) < 2) {
+            BloomFileArgs b;
+            b.keys = d_keys;
+            b.koff = d_koff;
+            b.file_start = d_file_start;
+            b.nkeys = 0;
+            b.m = m;
+            b.mrecip = barrett_recip(m);
+            b.k = kk;
+            b.split = (uint32_t)sb;
+            b.pos = static_cast<uint32_t *>(d_workspace);
+            b.maxr = max_file_records;
+            b.nwords = nwords;
+            b.out = d_out;
+            b.file_off = d_file_off;
+            b.bitmap = nullptr;
+            hipLaunchKernelGGL(bloom_file_kernel, dim3(nfile), dim3(1024), (size_t)(sb / 8), s, b);
+            LSM_HIP_CHECK(hipGetLastError());
+        } else {
+            BloomBinArgs b;
+            b.keys = d_keys;
+            b.koff = d_koff;
+            b.file_start = d_file_start;
+            b.m = m;
+            b.mrecip = barrett_recip(m);
+            b.k = kk;
+            b.split = (uint32_t)sb;
+            b.maxr = max_file_records;
+            const size_t cnt_bytes = ((size_t)nfile * 2 * 4 + 255) & ~(size_t)255;
+            b.cnt = static_cast<uint32_t *>(d_workspace);
+            b.pos = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) + cnt_bytes);
+            b.out = d_out;
+            b.file_off = d_file_off;
+            b.nwords = nwords;
+            LSM_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)nfile * 2 * 4, s));
+            const uint32_t bchunks = (max_file_records + kBinWaves * kWave - 1) / (kBinWaves * kWave);
+            if (bchunks) {
+                hipLaunchKernelGGL(bloom_bin_kernel, dim3(nfile, bchunks), dim3(kBinWaves * kWave), 0, s, b);
+                LSM_HIP_CHECK(hipGetLastError());
+            }
+            hipLaunchKernelGGL(bloom_apply_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, b);
             LSM_HIP_CHECK(hipGetLastError());
         }
-        hipLaunchKernelGGL(bloom_apply_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, b);
-        LSM_HIP_CHECK(hipGetLastError());
     } else {
         BloomArgs b;
         b.keys = d_keys;
@@ -1071,6 +1218,7 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
         LSM_HIP_CHECK(hipGetLastError());
     }
 
+
     SstArgs a;
     a.keys = d_keys;
     a.koff = d_koff;
@@ -1083,6 +1231,11 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
     a.m = m;
     a.nwords = nwords;
     a.k = kk;
+    static const uint32_t dbg = [] {
+        const char *e = getenv("LSM_SST_DBG");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    a.dbg = dbg;
     if (chunks) {
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, chunks), dim3(256), 0, s, a);
         LSM_HIP_CHECK(hipGetLastError());
