@@ -800,6 +800,7 @@ struct BloomFileArgs {
     uint8_t *out;     // image mode
     const uint64_t *file_off;
     uint64_t *bitmap; // native mode (out == null)
+    uint32_t dbg;     // diagnostics only: bit 2 skips slice 1, bit 3 the slice-0 ORs
 };
 
 __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
@@ -816,26 +817,72 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
     if (threadIdx.x == 0) n1 = 0;
     __syncthreads();
     uint32_t *list = two ? a.pos + (uint64_t)f * a.k * a.maxr : nullptr;
-    for (uint64_t i0 = s + (threadIdx.x & ~63u); i0 < e; i0 += blockDim.x) {
+    // Two-stage load pipeline across rounds (a wave takes 64 keys per round,
+    // rounds 1024 keys apart): while round r hashes, the first 16 key bytes
+    // of round r+1 and the offsets of round r+2 are in flight.  Indices past
+    // the filter are clamped to its last key (unconditional loads).
+    const uint32_t stride = blockDim.x;
+    auto clampi = [&](uint64_t i) { return i < e ? i : e - 1; };
+    uint64_t i0 = s + (threadIdx.x & ~63u);
+    uint64_t ka = 0, la = 0, fa0 = 0, fa1 = 0, kb = 0, lb = 0;
+    if (i0 < e) {
+        const uint64_t ii = clampi(i0 + lane);
+        ka = a.koff[ii];
+        la = a.koff[ii + 1] - ka;
+        fa0 = ldg_u64_unaligned(a.keys + ka);
+        fa1 = ldg_u64_unaligned(a.keys + ka + 8);
+        const uint64_t jn = clampi(i0 + stride + lane);
+        kb = a.koff[jn];
+        lb = a.koff[jn + 1] - kb;
+    }
+    for (; i0 < e; i0 += stride) {
         const uint64_t i = i0 + lane;
         const bool act = i < e;
+        // prefetch: key bytes of the next round, offsets of the one after
+        const uint64_t fb0 = ldg_u64_unaligned(a.keys + kb);
+        const uint64_t fb1 = ldg_u64_unaligned(a.keys + kb + 8);
+        const uint64_t jc = clampi(i0 + 2 * stride + lane);
+        const uint64_t kc = a.koff[jc];
+        const uint64_t lc = a.koff[jc + 1] - kc;
         uint64_t h[4];
-        {
-            const uint64_t ii = act ? i : e - 1;  // unconditional loads
-            const uint64_t k0 = a.koff[ii];
-            sum256(a.keys + k0, a.koff[ii + 1] - k0, h);
-        }
-        for (uint32_t j = 0; j < a.k; j++) {
-            const uint32_t p = (uint32_t)mod_barrett(location(h[0], h[1], h[2], h[3], j), a.m, a.mrecip);
-            const bool in1 = act && p >= lo1;
-            if (act && !in1) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
+        sum256_pre(a.keys + ka, la, fa0, fa1, h);
+        ka = kb; la = lb; fa0 = fb0; fa1 = fb1;
+        kb = kc; lb = lc;
+        // 16 locations per round; a lane keeps its slice-1 positions in
+        // registers and the wave reserves list space once per round.
+        // location(j) = h[j%2] + j*h[2 + ((j + j%2) % 4)/2] (bloom.go:133-136):
+        // by class c = j%4 the multiplier is h2, h3, h3, h2, so each class is
+        // an arithmetic progression with step 4*h2 or 4*h3 -- additions only
+        // (64-bit multiplies are quarter-rate).
+        uint64_t loc[4] = {h[0], h[1] + h[3], h[0] + (h[3] << 1), h[1] + h[2] + (h[2] << 1)};
+        const uint64_t st2 = h[2] << 2, st3 = h[3] << 2;
+        for (uint32_t j0 = 0; j0 < a.k; j0 += kBinBatch) {
+            uint32_t pp[kBinBatch];
+            uint32_t c1 = 0;
+#pragma unroll
+            for (uint32_t jj = 0; jj < kBinBatch; jj++) {
+                const uint32_t j = j0 + jj;
+                const bool valid = act && j < a.k;
+                const uint32_t c = jj & 3;  // j0 is a multiple of 4
+                const uint32_t p = mod_small(loc[c], (uint32_t)a.m, (uint32_t)a.mrecip,
+                                             (uint32_t)(a.mrecip >> 32));
+                loc[c] += (c == 0 || c == 3) ? st2 : st3;
+                const bool in1 = p >= (uint32_t)lo1;  // lo1 <= m <= 2^30
+                if (valid && !in1 && !(a.dbg & 8)) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
+                pp[jj] = valid && in1 ? p : 0xFFFFFFFFu;
+                c1 += (uint32_t)(valid && in1);
+            }
             if (two) {
-                const uint64_t b1 = __ballot(in1);
-                if (b1) {
+                uint32_t tot1;
+                const uint32_t ex = wave_excl_scan(c1, &tot1);
+                tot1 = uni(tot1);
+                if (tot1) {
                     uint32_t o = 0;
-                    if (lane == 0) o = atomicAdd(&n1, (uint32_t)__builtin_popcountll(b1));
-                    o = uni(o);
-                    if (in1) list[o + mbcnt(b1)] = p;
+                    if (lane == 0) o = atomicAdd(&n1, tot1);
+                    uint32_t w = uni(o) + ex;
+#pragma unroll
+                    for (uint32_t jj = 0; jj < kBinBatch; jj++)
+                        if (pp[jj] != 0xFFFFFFFFu) list[w++] = pp[jj];
                 }
             }
         }
@@ -847,7 +894,7 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
     } else {
         store_filter_slice(lds_bits, 0, (lo1 + 63) / 64, nullptr, a.bitmap + (uint64_t)f * a.nwords);
     }
-    if (!two) return;
+    if (!two || (a.dbg & 4)) return;
     // slice 1 from this workgroup's own list
     __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1119,7 +1166,7 @@ static uint32_t bloom_slices(uint64_t m) {
     const uint64_t sb = slice_bits_for(m);
     return (uint32_t)((m + sb - 1) / sb);
 }
-static bool hash_once_bloom(uint64_t m) { return m < (1ull << 32) && bloom_slices(m) <= 2; }
+static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slices(m) <= 2; }
 
 extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
                                                 uint64_t m, uint32_t k) {
@@ -1130,6 +1177,15 @@ extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_fil
 }
 
 static uint64_t barrett_recip(uint64_t m) { return ~0ull / m; }
+
+// Diagnostics only (LSM_SST_DBG): skip parts of lsm_build_sst to time the rest.
+static uint32_t sst_dbg() {
+    static const uint32_t v = [] {
+        const char *e = getenv("LSM_SST_DBG");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    return v;
+}
 
 extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
                              const uint8_t *d_vals, const uint64_t *d_voff,
@@ -1172,6 +1228,7 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
             b.out = d_out;
             b.file_off = d_file_off;
             b.bitmap = nullptr;
+            b.dbg = sst_dbg();
             hipLaunchKernelGGL(bloom_file_kernel, dim3(nfile), dim3(1024), (size_t)(sb / 8), s, b);
             LSM_HIP_CHECK(hipGetLastError());
         } else {
@@ -1231,11 +1288,7 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
     a.m = m;
     a.nwords = nwords;
     a.k = kk;
-    static const uint32_t dbg = [] {
-        const char *e = getenv("LSM_SST_DBG");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    a.dbg = dbg;
+    a.dbg = sst_dbg();
     if (chunks) {
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, chunks), dim3(256), 0, s, a);
         LSM_HIP_CHECK(hipGetLastError());

@@ -62,21 +62,25 @@ __device__ __forceinline__ uint64_t ldg_u64_unaligned(const uint8_t *p) {
     return (uint64_t)funnel(x1, x2, s) << 32 | funnel(x0, x1, s);
 }
 
-// sum256 (murmur.go:245-275) of key[0..len).
-__device__ __forceinline__ void sum256(const uint8_t *key, uint64_t len, uint64_t h[4]) {
+// sum256 (murmur.go:245-275) of key[0..len), with the key's first 16 bytes
+// already loaded as (f0, f1) (callers prefetch them; bytes past len are
+// ignored).  Longer keys load their remaining blocks here.
+__device__ __forceinline__ void sum256_pre(const uint8_t *key, uint64_t len, uint64_t f0,
+                                           uint64_t f1, uint64_t h[4]) {
     uint64_t h1 = 0, h2 = 0;
-    uint64_t nb = len / 16;
-    for (uint64_t i = 0; i < nb; i++)
+    const uint64_t nb = len / 16;
+    if (nb) mmh3_block(h1, h2, f0, f1);
+    for (uint64_t i = 1; i < nb; i++)
         mmh3_block(h1, h2, ldg_u64_unaligned(key + 16 * i), ldg_u64_unaligned(key + 16 * i + 8));
-    uint32_t tl = (uint32_t)(len & 15);
-    const uint8_t *tail = key + 16 * nb;
+    const uint32_t tl = (uint32_t)(len & 15);
     uint64_t k1 = 0, k2 = 0;
     if (tl) {
         // Gather the tail bytes; bytes beyond tl are masked off.
-        uint64_t w0 = ldg_u64_unaligned(tail);
-        uint64_t w1 = tl > 8 ? ldg_u64_unaligned(tail + 8) : 0;
+        const uint8_t *tail = key + 16 * nb;
+        const uint64_t w0 = nb ? ldg_u64_unaligned(tail) : f0;
+        const uint64_t w1 = tl > 8 ? (nb ? ldg_u64_unaligned(tail + 8) : f1) : 0;
         k1 = tl >= 8 ? w0 : (w0 & ((1ull << (8 * tl)) - 1));
-        k2 = tl > 8 ? (tl == 16 ? w1 : (w1 & ((1ull << (8 * (tl - 8))) - 1))) : 0;
+        k2 = tl > 8 ? (w1 & ((1ull << (8 * (tl - 8))) - 1)) : 0;
     }
     mmh3_final(h1, h2, k1, k2, tl, len, h[0], h[1]);
     // Second digest: virtually append 0x01 at tail position tl.
@@ -90,6 +94,12 @@ __device__ __forceinline__ void sum256(const uint8_t *key, uint64_t len, uint64_
         else kk2 |= 1ull << (8 * (tl - 8));
         mmh3_final(h1, h2, kk1, kk2, tl + 1, len + 1, h[2], h[3]);
     }
+}
+
+// sum256 of key[0..len).  Reads up to 16 bytes past short keys (batches are
+// 16-byte padded, include/lsm_gpu.h).
+__device__ __forceinline__ void sum256(const uint8_t *key, uint64_t len, uint64_t h[4]) {
+    sum256_pre(key, len, ldg_u64_unaligned(key), ldg_u64_unaligned(key + 8), h);
 }
 
 // location(h, i) before the modulo (bloom.go:133-136).  Scalar arguments:
@@ -108,6 +118,22 @@ __device__ __forceinline__ uint64_t mod_barrett(uint64_t x, uint64_t m, uint64_t
     uint64_t q = __umul64hi(x, r);
     uint64_t rem = x - q * m;
     return rem >= m ? rem - m : rem;
+}
+
+// x mod m for m <= 2^30 in 32-bit arithmetic, r = floor((2^64-1)/m) split
+// as (rh, rl).  hi64(x*r) is in [q-1, q] (q = floor(x/m)); dropping the low
+// partial product and the carries of the middle ones costs at most 2 more,
+// so q' = the low 32 bits of xh*rh + hi(xh*rl) + hi(xl*rh) (mod 2^32) is in
+// [q-3, q] and x - q'*m, which is < 4m <= 2^32, is exact in 32 bits; three
+// conditional subtractions finish it (v_sub + v_min each).
+__device__ __forceinline__ uint32_t mod_small(uint64_t x, uint32_t m, uint32_t rl, uint32_t rh) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t q = xh * rh + __umulhi(xh, rl) + __umulhi(xl, rh);
+    uint32_t rem = xl - q * m;
+    rem = min(rem, rem - m);
+    rem = min(rem, rem - m);
+    rem = min(rem, rem - m);
+    return rem;
 }
 
 }  // namespace lsm
