@@ -203,7 +203,7 @@ def bench_decode(args, world, rank, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "decode_spec_kernel<KV>",
+            "kernel": "decode_spec_kernel<KV,1,1>",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

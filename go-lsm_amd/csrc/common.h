@@ -59,29 +59,57 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
-// Exclusive wave prefix sum (64 lanes) of a 32-bit value.
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
-    uint32_t lane = lane_id();
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, kWave);
-        if (lane >= (uint32_t)d) x += y;
+// Wave-64 inclusive prefix sums with DPP row shifts (1, 2, 4, 8 within a
+// 16-lane row) and the gfx9 row broadcasts (lane 15 -> next row, lane 31 ->
+// upper half): six VALU moves, no LDS round trip (a __shfl_up scan is six
+// ds_bpermute waits).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t l = lane_id(), rl = l & 15;
+    uint32_t t;
+    t = dpp_mov<0x111>(v); v += rl >= 1 ? t : 0;   // row_shr:1
+    t = dpp_mov<0x112>(v); v += rl >= 2 ? t : 0;   // row_shr:2
+    t = dpp_mov<0x114>(v); v += rl >= 4 ? t : 0;   // row_shr:4
+    t = dpp_mov<0x118>(v); v += rl >= 8 ? t : 0;   // row_shr:8
+    t = dpp_mov<0x142>(v); v += (l & 31) >= 16 ? t : 0;  // row_bcast:15
+    t = dpp_mov<0x143>(v); v += l >= 32 ? t : 0;   // row_bcast:31
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+    const uint32_t l = lane_id(), rl = l & 15;
+#define LSM_SCAN64_STEP(CTRL, COND)                                                     \
+    {                                                                                  \
+        const uint64_t t = (uint64_t)dpp_mov<CTRL>((uint32_t)(v >> 32)) << 32 |        \
+                           dpp_mov<CTRL>((uint32_t)v);                                 \
+        v += (COND) ? t : 0;                                                           \
     }
-    *total = __shfl(x, kWave - 1, kWave);
-    return x - v;
+    LSM_SCAN64_STEP(0x111, rl >= 1)
+    LSM_SCAN64_STEP(0x112, rl >= 2)
+    LSM_SCAN64_STEP(0x114, rl >= 4)
+    LSM_SCAN64_STEP(0x118, rl >= 8)
+    LSM_SCAN64_STEP(0x142, (l & 31) >= 16)
+    LSM_SCAN64_STEP(0x143, l >= 32)
+#undef LSM_SCAN64_STEP
+    return v;
+}
+
+// Exclusive wave prefix sum (64 lanes); *total = the sum over all lanes.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+    const uint32_t inc = wave_incl_scan(v);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+    return inc - v;
 }
 
 __device__ __forceinline__ uint64_t wave_excl_scan64(uint64_t v, uint64_t *total) {
-    uint32_t lane = lane_id();
-    uint64_t x = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint64_t y = __shfl_up(x, d, kWave);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    *total = __shfl(x, kWave - 1, kWave);
-    return x - v;
+    const uint64_t inc = wave_incl_scan64(v);
+    *total = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(inc >> 32), kWave - 1) << 32 |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)inc, kWave - 1);
+    return inc - v;
 }
 
 // Copy `len` bytes from buffer offset `src` (rsrc-relative, any alignment)
