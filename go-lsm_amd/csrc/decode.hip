@@ -1205,6 +1205,51 @@ extern "C" int lsm_plan_arena_base(lsm_ctx *ctx, const uint32_t *d_blk_len, uint
                      static_cast<hipStream_t>(stream));
 }
 
+// ---- compaction: decoded records -> one dense array -----------------------
+//
+// The decode writes block b's records at its capacity slots (rec_base or
+// offset-addressed), so the per-record arrays are sparse.  A consumer on the
+// host (or the next stage) wants them dense: out_base = exclusive scan of
+// nrec (plan_scan), then one wave per block copies its nrec descriptors
+// (16 B per lane, coalesced) and IDX values.
+__global__ __launch_bounds__(256) void compact_kernel(int grammar, const uint64_t *blk_off,
+                                                      uint32_t nblk, const u32x4 *desc,
+                                                      const int64_t *idx, const uint64_t *rec_base,
+                                                      const uint32_t *nrec, const uint64_t *out_base,
+                                                      u32x4 *dense, int64_t *dense_idx) {
+    const uint32_t b = uni(blockIdx.x * 4 + threadIdx.x / kWave);
+    if (b >= nblk) return;
+    const uint32_t R = grammar == LSM_GRAMMAR_V ? 4 : grammar == LSM_GRAMMAR_KV ? 8 : 12;
+    const uint64_t src = rec_base ? uni64(rec_base[b]) : uni64(blk_off[b]) / R;
+    const uint64_t dst = uni64(out_base[b]);
+    const uint32_t n = uni(nrec[b]);
+    for (uint32_t i = lane_id(); i < n; i += kWave) {
+        dense[dst + i] = __builtin_nontemporal_load(&desc[src + i]);
+        if (dense_idx) dense_idx[dst + i] = idx[src + i];
+    }
+}
+
+extern "C" int lsm_compact_records(lsm_ctx *ctx, int grammar, const uint64_t *d_blk_off,
+                                   uint32_t nblk, const lsm_decode_out *out, lsm_rec_desc *d_dense,
+                                   int64_t *d_dense_idx, uint64_t *d_dense_base, void *d_workspace,
+                                   size_t ws_bytes, void *stream) {
+    if (!ctx || !out || !d_dense_base) return LSM_EINVAL;
+    if (grammar < LSM_GRAMMAR_V || grammar > LSM_GRAMMAR_IDX) return LSM_EINVAL;
+    if (nblk && (!out->desc || !out->nrec || !d_dense || (!out->rec_base && !d_blk_off)))
+        return LSM_EINVAL;
+    if (d_dense_idx && (grammar != LSM_GRAMMAR_IDX || !out->idx_value)) return LSM_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int rc = plan_scan(3, out->nrec, nblk, d_dense_base, d_workspace, ws_bytes, s);
+    if (rc) return rc;
+    if (nblk == 0) return 0;
+    hipLaunchKernelGGL(compact_kernel, dim3((nblk + 3) / 4), dim3(256), 0, s, grammar, d_blk_off,
+                       nblk, reinterpret_cast<const u32x4 *>(out->desc), out->idx_value,
+                       out->rec_base, out->nrec, d_dense_base, reinterpret_cast<u32x4 *>(d_dense),
+                       d_dense_idx);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
                                  const uint64_t *d_blk_off, const uint32_t *d_blk_len,
                                  uint32_t nblk, const lsm_decode_out *out, void *stream) {

@@ -6,7 +6,8 @@ This package only moves buffers (PyTorch) and calls the C ABI (ctypes).
 from . import _lib  # noqa: F401
 from .codec import (  # noqa: F401
     DEFAULT_BLOOM_K, DEFAULT_BLOOM_M, DESC_DTYPE, GRAMMAR_IDX, GRAMMAR_KV, GRAMMAR_V,
-    MAX_SSTABLE_SIZE, STATUS_NAMES, Context, alloc_decode, alloc_decode_offset, batch_to_device, bloom_probe,
-    build_sst, build_sst_into, decode_blocks, decode_into, encode_blocks, pad16, plan,
-    prepare_sst, replan, segment_files, sum256, to_device_bytes)
+    MAX_SSTABLE_SIZE, STATUS_NAMES, Context, DenseRecords, alloc_decode, alloc_decode_offset,
+    alloc_dense, batch_to_device, bloom_probe, build_sst, build_sst_into, compact_into,
+    decode_blocks, decode_into, encode_blocks, pad16, plan, prepare_sst, replan, segment_files,
+    sum256, to_device_bytes)
 from . import synth  # noqa: F401

@@ -212,10 +212,8 @@ def alloc_decode_offset(ctx: Context, grammar: int, nblk: int, in_bytes: int,
     return r
 
 
-def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,
-                blk_len: torch.Tensor, r: DecodeResult, stream=None) -> None:
-    """lsm_decode_blocks into preallocated outputs (asynchronous)."""
-    out = _lib.DecodeOut(
+def _decode_out(r: DecodeResult):
+    return _lib.DecodeOut(
         desc=r.desc.data_ptr(),
         rec_base=r.rec_base.data_ptr() if r.rec_base is not None else None,
         nrec=r.nrec.data_ptr(),
@@ -227,6 +225,12 @@ def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.T
         key_arena_off=r.key_arena_off.data_ptr() if r.key_arena_off is not None else None,
         val_arena_off=r.val_arena_off.data_ptr() if r.val_arena_off is not None else None,
     )
+
+
+def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,
+                blk_len: torch.Tensor, r: DecodeResult, stream=None) -> None:
+    """lsm_decode_blocks into preallocated outputs (asynchronous)."""
+    out = _decode_out(r)
     _lib.check(ctx.lib.lsm_decode_blocks(ctx.handle, grammar, _ptr(d_in), _ptr(blk_off),
                                          _ptr(blk_len), int(blk_off.numel()), ctypes.byref(out),
                                          _stream_handle(stream)), "lsm_decode_blocks")
@@ -247,6 +251,36 @@ def decode_blocks(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch
     if nblk:
         decode_into(ctx, grammar, d_in, blk_off, blk_len, r, stream=stream)
     return r
+
+
+@dataclass
+class DenseRecords:
+    """lsm_compact_records output: block b's records at desc[base[b]:base[b+1]]."""
+    desc: torch.Tensor                # int32[cap, 4]
+    base: torch.Tensor                # int64[nblk+1]
+    idx_value: Optional[torch.Tensor]
+    workspace: torch.Tensor
+
+
+def alloc_dense(ctx: Context, grammar: int, nblk: int, cap: int) -> DenseRecords:
+    dev = ctx.torch_device
+    return DenseRecords(
+        desc=torch.empty((max(cap, 1), 4), dtype=torch.int32, device=dev),
+        base=torch.empty(nblk + 1, dtype=torch.int64, device=dev),
+        idx_value=torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        if grammar == GRAMMAR_IDX else None,
+        workspace=torch.empty(max(int(ctx.lib.lsm_plan_workspace_bytes(nblk)), 16),
+                              dtype=torch.uint8, device=dev))
+
+
+def compact_into(ctx: Context, grammar: int, blk_off: torch.Tensor, r: DecodeResult,
+                 d: DenseRecords, stream=None) -> None:
+    """lsm_compact_records (asynchronous): the decode's records, dense."""
+    out = _decode_out(r)
+    _lib.check(ctx.lib.lsm_compact_records(
+        ctx.handle, grammar, _ptr(blk_off), int(blk_off.numel()), ctypes.byref(out),
+        _ptr(d.desc), _ptr(d.idx_value), _ptr(d.base), _ptr(d.workspace), d.workspace.numel(),
+        _stream_handle(stream)), "lsm_compact_records")
 
 
 # ---- encode -----------------------------------------------------------------

@@ -146,6 +146,17 @@ int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in, const uint
                       const uint32_t *d_blk_len, uint32_t nblk, const lsm_decode_out *out,
                       void *stream);
 
+/* Compact the records of a finished lsm_decode_blocks into one dense array:
+ * d_dense_base[0..nblk] = exclusive scan of nrec (d_dense_base[nblk] = total)
+ * and block b's records land at d_dense[d_dense_base[b] ..] (and IDX values
+ * at d_dense_idx, optional).  `out` is the lsm_decode_out the decode used
+ * (its rec_base, or offset addressing with d_blk_off).  Workspace:
+ * lsm_plan_workspace_bytes(nblk).  This is the hand-off a host consumer
+ * copies back (GetKeyValuePairs' record list, sstable.go:248-268). */
+int lsm_compact_records(lsm_ctx *ctx, int grammar, const uint64_t *d_blk_off, uint32_t nblk,
+                        const lsm_decode_out *out, lsm_rec_desc *d_dense, int64_t *d_dense_idx,
+                        uint64_t *d_dense_base, void *d_workspace, size_t ws_bytes, void *stream);
+
 /* ---- encode ---------------------------------------------------------------- */
 
 /* Batch encode of a columnar record batch (CSR: record i's key is

@@ -71,14 +71,37 @@ def check_against_oracle(grammar, buf, blk_off, blk_len, r, arena=False):
                 assert va[ab[b]:ab[b] + ov.size].tobytes() == ov.tobytes(), b
 
 
-def run(ctx, grammar, blocks, arena=False, align_pad=None, seed=0, placement="plan"):
+def check_compaction(ctx, grammar, blk_off_host, d_off, r):
+    """lsm_compact_records: the same records, dense, in block order."""
+    nrec = r.nrec.cpu().numpy().astype(np.int64)[: d_off.numel()]
+    d = lsmgpu.alloc_dense(ctx, grammar, int(d_off.numel()), int(nrec.sum()))
+    lsmgpu.compact_into(ctx, grammar, d_off, r, d)
+    torch.cuda.synchronize()
+    base = d.base.cpu().numpy()
+    assert np.array_equal(base, np.concatenate([[0], np.cumsum(nrec)]))
+    dense = d.desc.cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+    sparse = r.desc_numpy()
+    rb = r.bases(blk_off_host).astype(np.int64)
+    for b in range(len(nrec)):
+        assert np.array_equal(dense[base[b]:base[b + 1]], sparse[rb[b]:rb[b] + nrec[b]]), b
+    if d.idx_value is not None:
+        iv, div = r.idx_value.cpu().numpy(), d.idx_value.cpu().numpy()
+        for b in range(len(nrec)):
+            assert np.array_equal(div[base[b]:base[b + 1]], iv[rb[b]:rb[b] + nrec[b]]), b
+
+
+def run(ctx, grammar, blocks, arena=False, align_pad=None, seed=0, placement="plan",
+        compact=False):
     rng = np.random.default_rng(seed)
     buf, d_in, d_off, d_len = dev_batch(ctx, blocks, align_pad=align_pad, rng=rng)
     r = lsmgpu.decode_blocks(ctx, grammar, d_in, d_off, d_len, arena=arena, arena_offsets=arena,
                              placement=placement)
     torch.cuda.synchronize()
-    check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
-                         d_len.cpu().numpy().view(np.uint32), r, arena=arena)
+    blk_off = d_off.cpu().numpy().view(np.uint64)
+    check_against_oracle(grammar, buf, blk_off, d_len.cpu().numpy().view(np.uint32), r,
+                         arena=arena)
+    if compact:
+        check_compaction(ctx, grammar, blk_off, d_off, r)
     return r
 
 
@@ -175,7 +198,8 @@ def test_fuzz_small_blocks(ctx, grammar, arena, placement):
     for i in range(300):
         b = rand_records(rng, grammar, int(rng.integers(0, 40)), kmax=24, vmax=120)
         blocks.append(corrupt(rng, b))
-    run(ctx, grammar, blocks, arena=arena, align_pad=19, seed=grammar, placement=placement)
+    run(ctx, grammar, blocks, arena=arena, align_pad=19, seed=grammar, placement=placement,
+        compact=not arena)
 
 
 @pytest.mark.parametrize("grammar", [0, 1, 2])
