@@ -59,24 +59,43 @@ struct DecodeArgs {
     const uint64_t *arena_base;
     uint64_t *key_arena_off;
     uint64_t *val_arena_off;
+    uint32_t split;  // 1: blocks larger than the 4 KiB ring are left to decode_large_kernel
+    uint32_t dbg;    // diagnostics only (LSM_DECODE_DBG): bit 0 no speculative runs,
+                     // bit 1 no global verification, bit 2 stop after one record
 };
 
 // Streams one block through this wave's LDS ring and serves u32 length
 // fields at wave-uniform block positions.
 //
-// Ring: 4 x 1 KiB chunks, filled by LDS-DMA (buffer_load_dwordx4 ... lds:
-// no VGPR staging, one s_waitcnt for all chunks of a refill).  Window: each
-// lane holds 16 raw bytes of a 1 KiB, 16-byte aligned slice of the stream
-// (one ds_read_b128); a field at stream byte s is two v_readlane of the
-// lanes/dwords covering [s, s+4) plus a scalar funnel shift.  A 4 KiB block
-// costs ~5 LDS round trips instead of one per record.
-struct BlockReader {
+// Ring: NCH x 1 KiB chunks, filled by LDS-DMA (buffer_load_dwordx4 ... lds:
+// no VGPR staging).  Window: each lane holds 16 raw bytes of a 1 KiB, 16-byte
+// aligned slice of the stream (one ds_read_b128); a field at stream byte s is
+// two v_readlane of the lanes/dwords covering [s, s+4) plus a scalar funnel
+// shift, so a 4 KiB block costs ~5 LDS round trips instead of one per record.
+// NCH = 4 (4 KiB) for blocks that fit whole; blocks larger than that stream
+// through a 16 KiB ring (decode_large_kernel) with up to 15 KiB in flight.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(uint32_t k) {
+    // s_waitcnt takes an immediate: one arm per count (N <= 16).
+#define LSM_VMW(i) case i: __asm__ __volatile__("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+    switch (k < N ? k : N - 1) {
+    LSM_VMW(0) LSM_VMW(1) LSM_VMW(2) LSM_VMW(3) LSM_VMW(4) LSM_VMW(5) LSM_VMW(6) LSM_VMW(7)
+    LSM_VMW(8) LSM_VMW(9) LSM_VMW(10) LSM_VMW(11) LSM_VMW(12) LSM_VMW(13) LSM_VMW(14)
+    default: __asm__ __volatile__("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+#undef LSM_VMW
+}
+
+template <uint32_t NCH>
+struct BlockReaderT {
+    static constexpr uint32_t kBytes = NCH * kChunk;
     uint32_t *ring;
     rsrc_t rsrc;
     uint32_t h;        // block start inside its first 16-byte line
     uint32_t total;    // loadable stream bytes: round_up16(h + n)
     uint32_t nchunks;  // chunks covering [0, total)
-    uint32_t hi_c;     // chunks [.., hi_c) have been loaded into the ring
+    uint32_t hi_c;     // chunks [.., hi_c) have been issued into the ring
+    uint32_t landed;   // chunks [.., landed) are known to be in LDS
     uint32_t wb;       // window base (stream byte, 16-aligned)
     u32x4 raw;         // lane j: stream bytes [wb + 16j, wb + 16j + 16)
     bool have_win;
@@ -90,40 +109,49 @@ struct BlockReader {
         nchunks = (total + kChunk - 1) / kChunk;
         rsrc = make_rsrc(in + a0, total);
         hi_c = 0;
+        landed = 0;
         have_win = false;
         wb = 0;
     }
 
-    // Make stream bytes [s0, s0 + kChunk) resident (clamped to the block),
-    // loading every missing chunk up to 3 chunks past s0's chunk.
-    __device__ __forceinline__ void ensure(uint32_t s0) {
-        uint32_t need_end = s0 + kChunk;
-        if (need_end > total) need_end = total;
-        const uint32_t need_hi = (need_end + kChunk - 1) / kChunk;
-        if (need_hi <= hi_c) return;
+    // Make stream bytes [s0, s0 + want) resident (clamped to the block and
+    // to the ring's reach from s0's chunk).  Every free ring slot is refilled,
+    // but the wait is counted: only the chunks asked for must have landed, the
+    // younger ones stay in flight while the chase runs.  vmcnt retires in
+    // issue order across loads, stores and LDS-DMA, so descriptor stores
+    // issued after a prefetch only make the count conservative.  (A plain
+    // vmcnt(0) here streams a block larger than the ring at one HBM round
+    // trip per refill.)
+    __device__ __forceinline__ void ensure(uint32_t s0, uint32_t want = kChunk) {
         const uint32_t c0 = s0 / kChunk;
-        const uint32_t first = hi_c > c0 ? hi_c : c0;
-        uint32_t last = c0 + kNChunk;
+        // Top up: every slot whose chunk lies behind s0 is free; refill it now
+        // (even when the bytes asked for are already resident), so a chunk is
+        // issued NCH - 1 chunks before the chase reaches it.
+        uint32_t last = c0 + NCH;
         if (last > nchunks) last = nchunks;
-        const uint32_t voff = lane_id() * 16;
-#pragma unroll
-        for (uint32_t i = 0; i < kNChunk; i++) {
-            const uint32_t c = first + i;
-            if (c < last)
+        if (last > hi_c) {
+            const uint32_t voff = lane_id() * 16;
+            for (uint32_t c = hi_c > c0 ? hi_c : c0; c < last; c++)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rsrc, (__attribute__((address_space(3))) void *)&ring[(c % kNChunk) * (kChunk / 4)],
+                    rsrc, (__attribute__((address_space(3))) void *)&ring[(c % NCH) * (kChunk / 4)],
                     16, voff + c * kChunk, 0, 0, kBlockLoadAux);
+            hi_c = last;
         }
-        hi_c = last;
+        uint64_t need_end = (uint64_t)s0 + want;
+        if (need_end > total) need_end = total;
+        if (need_end > (uint64_t)last * kChunk) need_end = (uint64_t)last * kChunk;
+        const uint32_t need_hi = (uint32_t)((need_end + kChunk - 1) / kChunk);
+        if (need_hi <= landed) return;
         // The DMA writes are invisible to the compiler's waitcnt tracking of
-        // ds_read; wait for them explicitly before the window read.
-        __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+        // ds_read; wait for them explicitly before any LDS read of them.
+        wait_vmcnt_le<NCH>(hi_c - need_hi);
+        landed = need_hi;
     }
 
     __device__ __forceinline__ void load_window(uint32_t s) {
         wb = s & ~15u;
         ensure(wb);
-        const uint32_t w = ((wb + lane_id() * 16) % kRingBytes) / 4;
+        const uint32_t w = ((wb + lane_id() * 16) % kBytes) / 4;
         raw = *reinterpret_cast<const u32x4 *>(&ring[w]);
         have_win = true;
     }
@@ -151,6 +179,7 @@ struct BlockReader {
         return lo;
     }
 };
+using BlockReader = BlockReaderT<kNChunk>;
 
 // Records staged one per lane until 64 are ready, then stored coalesced.
 struct RecordStage {
@@ -302,18 +331,19 @@ __device__ void decode_block_wave(const DecodeArgs &a, uint32_t b, uint32_t *rin
 // The first mismatching record is re-decoded by the exact scalar step, which
 // also produces the precise error status.  A block of equal-size records
 // (the common LSM case) costs one exact step and one run per 64 records.
-template <int G>
+template <int G, uint32_t NCH = kNChunk>
 __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
                                   uint32_t n, bool staged = false) {
+    constexpr uint32_t kWords = NCH * kChunk / 4;
     uint64_t base, cap;
     record_slots<G>(a, b, off, n, base, cap);
     base = uni64(base);
     cap = uni64(cap);
     const uint32_t lane = lane_id();
 
-    BlockReader rd;
+    BlockReaderT<NCH> rd;
     rd.init(ring, a.in, off, n);
-    if (staged) rd.hi_c = rd.nchunks < kNChunk ? rd.nchunks : kNChunk;  // DMA'd and landed
+    if (staged) rd.hi_c = rd.landed = rd.nchunks < NCH ? rd.nchunks : NCH;  // DMA'd and landed
 #ifdef LSM_STAMPS
     rd.ensure(rd.h);
     stamp(1);
@@ -321,13 +351,44 @@ __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *rin
     auto lds_u32 = [&](uint32_t p) -> uint32_t {  // per-lane read, block position p
         const uint32_t sb = rd.h + p;
         const uint32_t w = sb >> 2;
-        return funnel(ring[w % kRingWords], ring[(w + 1) % kRingWords], sb);
+        return funnel(ring[w % kWords], ring[(w + 1) % kWords], sb);
     };
 
-    uint32_t pos = 0, nr = 0;
+    // Wave-uniform field at block position p: two LDS dwords (a broadcast
+    // read), a funnel shift and one readfirstlane.  The bytes must be landed.
+    auto ufield = [&](uint32_t p) -> uint32_t {
+        const uint32_t sb = rd.h + p;
+        const uint32_t w = sb >> 2;
+        return uni(funnel(ring[w % kWords], ring[(w + 1) % kWords], sb));
+    };
+
+    // Exact-step records are staged one per lane and stored 64 at a time: a
+    // store between a ring refill and its counted wait is younger than the
+    // chunks in flight, so one store per record would make every wait drain
+    // the whole prefetch (vmcnt counts stores too).  Staged records occupy
+    // consecutive slots s_first.. (the stage is flushed before a run).
+    uint32_t s_pos = 0, s_k = 0, s_v = 0, s_xlo = 0, s_xhi = 0, ns = 0, s_first = 0;
+    auto flush_stage = [&]() {
+        if (ns && lane < ns) {
+            const uint64_t ro = off + s_pos;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = s_k;
+            d.w = s_v;
+            a.desc[base + s_first + lane] = d;
+            if (G == LSM_GRAMMAR_IDX && a.idx_value)
+                a.idx_value[base + s_first + lane] = (int64_t)((uint64_t)s_xhi << 32 | s_xlo);
+        }
+        ns = 0;
+    };
+    uint32_t pos = 0, nr = 0, miss = 0, skip = 0, kprev = 0;
     int32_t status = LSM_OK;
     for (;;) {
         // ---- exact step at pos (same checks and order as the reference) ----
+        // Fields are read straight from the ring; the value length is read
+        // speculatively at the previous record's key length, in the same LDS
+        // round trip as the key length (keys of one length are the norm).
         const uint32_t rem = n - pos;
         uint32_t klen = 0, vlen = 0, vp = pos;
         uint64_t xval = 0;
@@ -336,47 +397,70 @@ __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *rin
             status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
             break;
         }
+        rd.ensure(rd.h + pos);  // [pos, pos + 1 KiB) landed (and the ring topped up)
         if (G == LSM_GRAMMAR_V) {
-            vlen = rd.field(pos);
+            vlen = ufield(pos);
             if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
         } else if (G == LSM_GRAMMAR_KV) {
-            klen = rd.field(pos);
+            const bool spec_v = kprev <= kChunk - 12 && rem >= 8 + kprev;
+            klen = ufield(pos);
+            const uint32_t vguess = spec_v ? ufield(pos + 4 + kprev) : 0;
             if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; break; }
             if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; break; }
             vp = pos + 4 + klen;
             const uint32_t rem2 = n - vp;
             if (rem2 < 4) { status = LSM_ST_TRUNC_VLEN; break; }
-            vlen = rd.field(vp);
+            if (spec_v && klen == kprev) {
+                vlen = vguess;
+            } else {
+                if (vp + 4 - pos > kChunk) rd.ensure(rd.h + vp);
+                vlen = ufield(vp);
+            }
             if (vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; break; }
             if (rem2 - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
+            kprev = klen;
         } else {
-            klen = rd.field(pos);
+            klen = ufield(pos);
             if ((uint64_t)rem < 12ull + klen) { status = LSM_ST_IDX_OVERRUN; break; }
             vp = pos + 4 + klen;
-            xval = (uint64_t)rd.field(vp + 4) << 32 | rd.field(vp);
+            if (vp + 8 - pos > kChunk) rd.ensure(rd.h + vp);
+            xval = (uint64_t)ufield(vp + 4) << 32 | ufield(vp);
             vlen = 8;
         }
         if (nr >= cap) { status = LSM_ST_CAPACITY; break; }
-        if (lane == 0) {
-            const uint64_t ro = off + pos;
-            u32x4 d;
-            d.x = (uint32_t)ro;
-            d.y = (uint32_t)(ro >> 32);
-            d.z = klen;
-            d.w = vlen;
-            a.desc[base + nr] = d;
-            if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr] = (int64_t)xval;
+        if (ns == 0) s_first = nr;
+        if (lane == ns) {
+            s_pos = pos;
+            s_k = klen;
+            s_v = vlen;
+            if (G == LSM_GRAMMAR_IDX) {
+                s_xlo = (uint32_t)xval;
+                s_xhi = (uint32_t)(xval >> 32);
+            }
         }
+        if (++ns == kWave) flush_stage();
         nr++;
         const uint32_t S = G == LSM_GRAMMAR_V ? 4 + vlen : G == LSM_GRAMMAR_KV ? 8 + klen + vlen
                                                                               : 12 + klen;
         pos += S;
 
         // ---- speculative runs of records shaped like the last one ----
-        for (;;) {
+        // Back off after runs that verified nothing (blocks of varied record
+        // shapes, config 5): skip the next 1, 3, 7, 15 attempts.
+        if (skip || (a.dbg & 1)) {
+            if (skip) skip--;
+            continue;
+        }
+        flush_stage();
+        for (bool first = true;; first = false) {
             if (pos >= n) break;
-            rd.ensure(rd.h + pos);
-            uint32_t res = rd.hi_c * kChunk;  // resident stream end
+            // wait for the span the run can verify (64 records): all of a block
+            // that fits the ring (its chunks were issued together), at most
+            // half the ring otherwise, so the younger half stays in flight
+            const uint32_t kSpanMax = (rd.nchunks <= NCH ? NCH : NCH / 2) * kChunk;
+            const uint64_t span = (uint64_t)S * kWave + 8;
+            rd.ensure(rd.h + pos, span < kSpanMax ? (uint32_t)span : kSpanMax);
+            uint32_t res = rd.landed * kChunk;  // resident stream end
             if (res > rd.total) res = rd.total;
             const uint32_t lim = (res - rd.h) < n ? (res - rd.h) : n;
             const uint64_t pe = (uint64_t)pos + (uint64_t)(lane + 1) * S;  // record end
@@ -407,13 +491,352 @@ __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *rin
             }
             nr += j;
             pos += j * S;
+            if (first) {
+                if (j == 0) {
+                    miss = miss < 4 ? miss + 1 : 4;
+                    skip = (1u << miss) - 1;
+                } else {
+                    miss = 0;
+                }
+            }
             if (j < 64) break;
         }
     }
+    flush_stage();
     if (lane == 0) {
         a.nrec[b] = nr;
         a.status[b] = status;
     }
+}
+
+// ---- v2: the chase with the fewest scalar instructions -------------------
+//
+// The exact step is a serial chain, and a wave-uniform chain runs on the CU's
+// one scalar unit, shared by all 32 resident waves: PMC on config 5 (record
+// shapes vary, so speculative runs rarely verify) counted 107 SALU
+// instructions per record for decode_block_spec, 74% of the kernel time at one
+// SALU issue per cycle.  v2 keeps the same semantics with a leaner step:
+//  * one compare decides whether the bytes are landed (`lim`), the ring
+//    bookkeeping only runs when a step crosses it;
+//  * blocks that fit the ring are read without modulo arithmetic (LIN);
+//  * the value length is read at the previous key length in the same LDS
+//    round trip as the key length;
+//  * descriptors are staged branch-free (v_cndmask) and stored 64 at a time;
+//  * error statuses are only computed on the (one) failing record.
+// Speculative runs are unchanged.
+// A wave-uniform value moved into a VGPR, so the arithmetic that depends on
+// it stays on the vector ALU (the compiler would otherwise keep a uniform
+// chain on the CU's single scalar unit).
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
+    uint32_t v;
+    __asm__ __volatile__("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+    return v;
+}
+
+template <int G, uint32_t NCH, bool LIN>
+__device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
+                                uint32_t n) {
+    constexpr uint32_t kWords = NCH * kChunk / 4;
+    uint64_t base, cap;
+    record_slots<G>(a, b, off, n, base, cap);
+    base = uni64(base);
+    const uint32_t ncap = uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu);
+    const uint32_t lane = lane_id();
+    BlockReaderT<NCH> rd;
+    rd.init(ring, a.in, off, n);
+
+    // Block bytes below `lim` (and at or above the last anchor) are landed.
+    uint32_t lim = 0;
+    auto need = [&](uint32_t p, uint32_t len) {
+        if ((uint64_t)p + len <= lim) return;
+        rd.ensure(rd.h + p, LIN ? rd.total : len);
+        lim = rd.landed >= rd.nchunks ? n : rd.landed * kChunk - rd.h;
+    };
+    auto word = [&](uint32_t w) -> uint32_t { return LIN ? ring[w] : ring[w % kWords]; };
+    auto fld = [&](uint32_t p) -> uint32_t {  // wave-uniform u32 at block position p
+        const uint32_t sb = rd.h + p;
+        const uint32_t w = sb >> 2;
+        return uni(funnel(word(w), word(w + 1), sb));
+    };
+    auto lds_u32 = [&](uint32_t p) -> uint32_t {  // per-lane u32 at block position p
+        const uint32_t sb = rd.h + p;
+        const uint32_t w = sb >> 2;
+        return funnel(word(w), word(w + 1), sb);
+    };
+
+    uint32_t s_pos = 0, s_k = 0, s_v = 0, s_xlo = 0, s_xhi = 0, ns = 0, s_first = 0;
+    uint32_t pos = 0, nr = 0, kprev = 0xFFFFFFFFu, miss = 0, skip = 0;
+    auto flush = [&]() {
+        if (ns) {
+            if (lane < ns) {
+                const uint64_t ro = off + s_pos;
+                u32x4 d;
+                d.x = (uint32_t)ro;
+                d.y = (uint32_t)(ro >> 32);
+                d.z = s_k;
+                d.w = s_v;
+                a.desc[base + s_first + lane] = d;
+                if (G == LSM_GRAMMAR_IDX && a.idx_value)
+                    a.idx_value[base + s_first + lane] = (int64_t)((uint64_t)s_xhi << 32 | s_xlo);
+            }
+            ns = 0;
+        }
+    };
+    auto gverify = [&](uint32_t K, uint32_t V, uint32_t S) {
+        constexpr uint32_t T = 8;  // 64-record rounds per batch (a 64 KiB block of 124 B records in one)
+        const uint32_t cnt = (n - pos) / S;  // candidates wholly inside the block
+        uint32_t i0 = 0;
+        while (i0 < cnt) {
+            uint32_t kw0[T], kw1[T], vw0[T], vw1[T], sb[T];
+#pragma unroll
+            for (uint32_t t = 0; t < T; t++) {
+                const uint32_t i = i0 + t * kWave + lane;
+                sb[t] = rd.h + pos + i * S;  // no wrap: i < cnt keeps it inside the block
+                const uint32_t sk = (i < cnt ? sb[t] : 0u) & ~3u;
+                const uint32_t svv = (i < cnt ? sb[t] + (G == LSM_GRAMMAR_KV ? 4 + K : 0u) : 0u) & ~3u;
+                kw0[t] = ld_b32(rd.rsrc, sk);
+                kw1[t] = ld_b32(rd.rsrc, sk + 4);
+                if (G == LSM_GRAMMAR_KV) {
+                    vw0[t] = ld_b32(rd.rsrc, svv);
+                    vw1[t] = ld_b32(rd.rsrc, svv + 4);
+                }
+            }
+            uint32_t f = T * kWave;
+#pragma unroll
+            for (uint32_t t = 0; t < T; t++) {
+                const uint32_t i = i0 + t * kWave + lane;
+                const uint32_t k = funnel(kw0[t], kw1[t], sb[t]);
+                bool ok = i < cnt && nr + i < ncap;
+                if (G == LSM_GRAMMAR_KV) {
+                    const uint32_t v = funnel(vw0[t], vw1[t], sb[t] + 4 + K);
+                    ok = ok && k == K && v == V;
+                } else {
+                    ok = ok && k == V;
+                }
+                const uint64_t m = __ballot(ok);
+                const uint32_t jt = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+                if (f == T * kWave && jt < 64) f = t * kWave + jt;
+                if (ok && t * kWave + lane < f) {
+                    const uint64_t ro = off + (sb[t] - rd.h);
+                    u32x4 d;
+                    d.x = (uint32_t)ro;
+                    d.y = (uint32_t)(ro >> 32);
+                    d.z = K;
+                    d.w = V;
+                    a.desc[base + nr + i] = d;
+                }
+            }
+            const uint32_t take = f < cnt - i0 ? f : cnt - i0;
+            i0 += take;
+            if (take < T * kWave) break;
+        }
+        const uint32_t got = i0 < cnt ? i0 : cnt;
+        nr += got;
+        pos += got * S;
+    };
+    int32_t status = LSM_OK;
+    for (;;) {
+        // ---- exact step at pos (same checks and order as the reference) ----
+        const uint32_t rem = n - pos;
+        if (rem == 0) break;
+        if (rem < 4) {
+            status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
+            break;
+        }
+        need(pos, rem < kChunk ? rem : kChunk);
+        uint32_t K = 0, V, S;
+        uint64_t x = 0;
+        if (G == LSM_GRAMMAR_V) {
+            V = fld(pos);  // data.go:58-76
+            if (rem - 4 < V) { status = LSM_ST_TRUNC_VAL; break; }
+            S = 4 + V;
+        } else if (G == LSM_GRAMMAR_KV) {
+            // kv.go:77-115; the guess at kprev lies inside the landed KiB
+            const bool sv = kprev <= kChunk - 8;
+            K = fld(pos);
+            const uint32_t vg = sv ? fld(pos + 4 + kprev) : 0u;
+            if (K > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; break; }
+            if (rem - 4 < K) { status = LSM_ST_TRUNC_KEY; break; }
+            const uint32_t vp = pos + 4 + K;
+            const uint32_t rem2 = n - vp;
+            if (rem2 < 4) { status = LSM_ST_TRUNC_VLEN; break; }
+            if (sv && K == kprev) {
+                V = vg;
+            } else {
+                need(vp, rem2 < kChunk ? rem2 : kChunk);
+                V = fld(vp);
+            }
+            if (V > kValCap) { status = LSM_ST_VAL_TOO_LONG; break; }
+            if (rem2 - 4 < V) { status = LSM_ST_TRUNC_VAL; break; }
+            kprev = K;
+            S = 8 + K + V;
+        } else {
+            K = fld(pos);  // index.go:70-98
+            if ((uint64_t)rem < 12ull + K) { status = LSM_ST_IDX_OVERRUN; break; }
+            const uint32_t vp = pos + 4 + K;
+            need(vp, 8);
+            x = (uint64_t)fld(vp + 4) << 32 | fld(vp);
+            V = 8;
+            S = 12 + K;
+        }
+        if (nr >= ncap) { status = LSM_ST_CAPACITY; break; }
+        if (ns == 0) s_first = nr;
+        {
+            const bool me = lane == ns;
+            s_pos = me ? pos : s_pos;
+            s_k = me ? K : s_k;
+            s_v = me ? V : s_v;
+            if (G == LSM_GRAMMAR_IDX) {
+                s_xlo = me ? (uint32_t)x : s_xlo;
+                s_xhi = me ? (uint32_t)(x >> 32) : s_xhi;
+            }
+        }
+        if (++ns == kWave) flush();
+        nr++;
+        pos += S;
+        if (a.dbg & 4) break;
+
+        // ---- records of varying shape: the VALU chain ----
+        // After a failed run (skip > 0) the following records are chased with
+        // the cursor in a VGPR: all lanes compute the same step, the checks
+        // combine into one ballot and the scalar unit only counts.  The step
+        // assumes the key length of the previous record and reads the value
+        // length at that offset in the same LDS round trip; any record it
+        // cannot vouch for (other key length, not yet landed, an error, the
+        // block end, capacity) drops back to the exact step above.
+        if (skip) {
+            skip--;
+            if (G == LSM_GRAMMAR_KV && kprev <= kChunk - 8) {
+                uint32_t vpos = to_vgpr(pos);
+                const uint32_t need8 = 8 + kprev;
+                while (nr < ncap) {
+                    const uint32_t sb = rd.h + vpos, sv = sb + 4 + kprev;
+                    const uint32_t k = funnel(word(sb >> 2), word((sb >> 2) + 1), sb);
+                    const uint32_t v = funnel(word(sv >> 2), word((sv >> 2) + 1), sv);
+                    const uint32_t rem = n - vpos;
+                    const bool ok = (vpos <= lim) & (lim - vpos >= need8) & (k == kprev) &
+                                    (v <= kValCap) & (rem - need8 >= v);
+                    if (!__ballot(ok)) break;
+                    if (ns == 0) s_first = nr;
+                    const bool me = lane == ns;
+                    s_pos = me ? vpos : s_pos;
+                    s_k = me ? kprev : s_k;
+                    s_v = me ? v : s_v;
+                    if (++ns == kWave) flush();
+                    nr++;
+                    vpos += need8 + v;
+                }
+                pos = uni(vpos);
+            } else if (G == LSM_GRAMMAR_V) {
+                uint32_t vpos = to_vgpr(pos);
+                while (nr < ncap) {
+                    const uint32_t sb = rd.h + vpos;
+                    const uint32_t v = funnel(word(sb >> 2), word((sb >> 2) + 1), sb);
+                    const uint32_t rem = n - vpos;
+                    const bool ok = (vpos <= lim) & (lim - vpos >= 4u) & (rem - 4 >= v);
+                    if (!__ballot(ok)) break;
+                    if (ns == 0) s_first = nr;
+                    const bool me = lane == ns;
+                    s_pos = me ? vpos : s_pos;
+                    s_k = me ? 0u : s_k;
+                    s_v = me ? v : s_v;
+                    if (++ns == kWave) flush();
+                    nr++;
+                    vpos += 4 + v;
+                }
+                pos = uni(vpos);
+            }
+            continue;
+        }
+        if (a.dbg & 1) continue;
+        flush();
+        for (bool first = true;; first = false) {
+            if (pos >= n) break;
+            // wait for the span the run can verify (64 records): all of a
+            // block that fits the ring, at most half the ring otherwise
+            const uint32_t span_max = (LIN ? NCH : NCH / 2) * kChunk;
+            const uint64_t span = (uint64_t)S * kWave + 8;
+            const uint32_t want = span < span_max ? (uint32_t)span : span_max;
+            need(pos, n - pos < want ? n - pos : want);
+            const uint64_t pe = (uint64_t)pos + (uint64_t)(lane + 1) * S;  // record end
+            const uint32_t p = pos + lane * S;
+            bool ok = pe <= lim && nr + lane < ncap;
+            uint64_t xx = 0;
+            if (ok) {
+                if (G == LSM_GRAMMAR_V) {
+                    ok = lds_u32(p) == V;
+                } else if (G == LSM_GRAMMAR_KV) {
+                    ok = (int)(lds_u32(p) == K) & (int)(lds_u32(p + 4 + K) == V);
+                } else {
+                    ok = lds_u32(p) == K;
+                    xx = (uint64_t)lds_u32(p + 8 + K) << 32 | lds_u32(p + 4 + K);
+                }
+            }
+            const uint64_t m = __ballot(ok);
+            const uint32_t j = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+            if (lane < j) {
+                const uint64_t ro = off + p;
+                u32x4 d;
+                d.x = (uint32_t)ro;
+                d.y = (uint32_t)(ro >> 32);
+                d.z = K;
+                d.w = V;
+                a.desc[base + nr + lane] = d;
+                if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + lane] = (int64_t)xx;
+            }
+            // the run ended at the landed limit, not at a mismatch
+            const bool at_lim = j == 64 || (uint64_t)pos + (uint64_t)(j + 1) * S > lim;
+            nr += j;
+            pos += j * S;
+            if (first) {
+                if (j == 0) {
+                    miss = miss < 4 ? miss + 1 : 4;
+                    skip = (1u << miss) - 1;
+                } else {
+                    miss = 0;
+                }
+            }
+            if (!LIN && at_lim && j >= 4 && G != LSM_GRAMMAR_IDX && !(a.dbg & 2)) {
+                // A full run in a streamed block: test the same hypothesis on
+                // the rest of the block straight from global memory, 256
+                // records per batch with all their loads in flight (the ring
+                // keeps ~2 KiB in flight per wave, too little for 64 KiB
+                // blocks at 25 waves per CU).  Verified records are exactly
+                // the chase's records (each check reads the record's own
+                // fields); the first mismatch goes back to the exact step.
+                gverify(K, V, S);
+                break;
+            }
+            if (j < 64) break;
+        }
+    }
+    flush();
+    if (lane == 0) {
+        a.nrec[b] = nr;
+        a.status[b] = status;
+    }
+}
+
+// One wave (and one workgroup) per block; NCH x 1 KiB ring plus a guard
+// dword so linear reads of a block's last field stay inside the array.
+template <int G, uint32_t NCH>
+__global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = uni64(a.blk_off[b]);
+    const uint32_t n = uni(a.blk_len[b]);
+    if (a.split && (off & 15) + (uint64_t)n > NCH * kChunk) return;
+    if (((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk)
+        decode_block_v2<G, NCH, true>(a, b, ring, off, n);
+    else
+        decode_block_v2<G, NCH, false>(a, b, ring, off, n);
+}
+
+template <int G, uint32_t NCH>
+int launch_v2(const DecodeArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((decode_v2_kernel<G, NCH>), dim3(a.nblk), dim3(kWave), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 // Each wave decodes K consecutive blocks one after the other; the metadata of
@@ -439,9 +862,62 @@ __global__ __launch_bounds__(64 * WPG) void decode_spec_kernel(DecodeArgs a) {
         const uint64_t off = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)moff, k) |
                                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(moff >> 32), k) << 32);
         const uint32_t n = __builtin_amdgcn_readlane(mlen, k);
+        if (a.split && (off & 15) + (uint64_t)n > kRingBytes) continue;
         decode_block_spec<G>(a, b, ring[wave], off, n);
     }
     stamp(3);
+}
+
+// ---- blocks larger than the 4 KiB ring ------------------------------------
+//
+// A 4 KiB ring keeps at most 3 KiB in flight per wave, which streams a 64 KiB
+// block at a fraction of the HBM rate (decode64k 0.56 of peak, config 5
+// 0.35).  Blocks with h + n > 4 KiB are therefore left by the small-block
+// kernel (a.split) to this persistent one: W one-wave workgroups, each with a
+// 16 KiB ring (up to 15 KiB in flight, 10 waves per CU by LDS), walk the
+// block list with stride W.  Lane l of wave w looks at block r0 + l*W and a
+// ballot picks the large ones, so a batch without large blocks costs one
+// metadata load per wave.
+constexpr uint32_t kLargeNCH = 16;
+
+template <int G, uint32_t NCH>
+__global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
+    const uint64_t W = gridDim.x;
+    const uint32_t lane = lane_id();
+    for (uint64_t r0 = blockIdx.x; r0 < a.nblk; r0 += W * kWave) {
+        const uint64_t b = r0 + lane * W;
+        uint64_t off = 0;
+        uint32_t n = 0;
+        bool big = false;
+        if (b < a.nblk) {
+            off = a.blk_off[b];
+            n = a.blk_len[b];
+            big = (off & 15) + (uint64_t)n > kRingBytes;
+        }
+        uint64_t m = __ballot(big);
+        while (m) {
+            const uint32_t l = uni((uint32_t)__builtin_ctzll(m));
+            m &= m - 1;
+            const uint64_t offj = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)off, l) |
+                                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(off >> 32), l) << 32);
+            const uint32_t nj = uni(__builtin_amdgcn_readlane(n, l));
+            decode_block_v2<G, NCH, false>(a, (uint32_t)(r0 + (uint64_t)l * W), ring, offj, nj);
+        }
+    }
+}
+
+template <int G, uint32_t NCH>
+int launch_large(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
+    // resident one-wave workgroups per CU: the 160 KiB LDS over the ring
+    constexpr uint32_t per_cu = 160 / NCH;
+    const uint32_t cus = ctx ? (uint32_t)lsm_ctx_num_cus(ctx) : 256u;
+    uint64_t grid = (uint64_t)cus * per_cu;
+    if (grid > a.nblk) grid = a.nblk;
+    if (grid == 0) return 0;
+    hipLaunchKernelGGL((decode_large_kernel<G, NCH>), dim3((uint32_t)grid), dim3(kWave), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 // ---- group-per-block speculative path (DESC mode, blocks <= 4 KiB) --------
@@ -1115,6 +1591,9 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             if (!strcmp(e, "stream32x32")) return 4;
             if (!strcmp(e, "spec4")) return 10;
             if (!strcmp(e, "spec")) return 30;
+            if (!strcmp(e, "large8")) return 40;
+            if (!strcmp(e, "v2split")) return 41;
+            if (!strcmp(e, "v2r8")) return 42;
             if (!strcmp(e, "spec_w1")) return 31;
             if (!strcmp(e, "spec_w2")) return 32;
             if (!strcmp(e, "pipe")) return 33;
@@ -1127,7 +1606,22 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             return 0;
         }();
         switch (variant) {
-        case 0: return launch_spec<G, 1, 1>(a, s);  // one-wave workgroups: measured best
+        case 0: return launch_v2<G, kNChunk>(a, s);  // one wave per block, 4 KiB ring
+        case 41: {
+            // v2 for blocks that fit the 4 KiB ring, then the deep-ring
+            // persistent kernel for the larger ones
+            DecodeArgs b = a;
+            b.split = 1;
+            const int rc = launch_v2<G, kNChunk>(b, s);
+            return rc ? rc : launch_large<G, kLargeNCH>(ctx, b, s);
+        }
+        case 42: return launch_v2<G, 8>(a, s);
+        case 40: {
+            DecodeArgs b = a;
+            b.split = 1;
+            const int rc = launch_spec<G, 1, 1>(b, s);
+            return rc ? rc : launch_large<G, 8>(ctx, b, s);
+        }
         case 33: return launch_pipe<G>(ctx, a, s);
         case 30: return launch_spec<G, 1>(a, s);
         case 31: return launch_spec<G, 1, 1>(a, s);
@@ -1274,6 +1768,12 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
     a.arena_base = out->arena_base;
     a.key_arena_off = out->key_arena_off;
     a.val_arena_off = out->val_arena_off;
+    a.split = 0;
+    static const uint32_t dbg = [] {
+        const char *e = getenv("LSM_DECODE_DBG");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    a.dbg = dbg;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (grammar) {
     case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true>(ctx, a, s)

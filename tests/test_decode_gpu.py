@@ -213,8 +213,14 @@ def test_large_and_many_record_blocks(ctx, grammar):
         b"",
     ]
     blocks.append(corrupt(rng, blocks[1]))
+    # a mixed-shape block far larger than the 4 KiB ring, then a uniform one:
+    # the DESC path streams both through counted-wait ring refills
+    blocks.append(rand_records(rng, grammar, 400, kmax=30, vmax=700))
+    blocks.append(rand_records(np.random.default_rng(0), grammar, 1, kmax=16, vmax=100) * 900)
     run(ctx, grammar, blocks, arena=True, align_pad=13, seed=3)
     run(ctx, grammar, blocks, arena=True, align_pad=13, seed=3, placement="offset")
+    run(ctx, grammar, blocks, arena=False, align_pad=13, seed=3, compact=True)
+    run(ctx, grammar, blocks, arena=False, align_pad=13, seed=4, placement="offset")
 
 
 def test_capacity_status(ctx):
@@ -291,3 +297,28 @@ def test_config5_mixed_sample(ctx):
     assert int((r.status != 0).sum()) == 0
     assert np.array_equal(r.nrec.cpu().numpy(), nrec)
     check_against_oracle(lsmgpu.GRAMMAR_KV, buf, blk_off, blk_len, r, arena=True)
+    # DESC output, the bench's kernel and placement
+    r = lsmgpu.decode_blocks(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, placement="offset")
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0
+    check_against_oracle(lsmgpu.GRAMMAR_KV, buf, blk_off, blk_len, r)
+
+
+def test_decode64k_full_size(ctx):
+    """6,400 x 64 KiB uniform KV blocks (the bench's decode64k): closed-form
+    descriptors, every block's records streamed through the ring."""
+    nblk, recs = 6400, 528
+    buf, blk_off, blk_len = synth.uniform_kv_blocks(np.arange(nblk), recs=recs, slot=65536)
+    dev = ctx.torch_device
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.tensor(blk_off.view(np.int64), device=dev)
+    d_len = torch.tensor(blk_len.view(np.int32), device=dev)
+    r = lsmgpu.decode_blocks(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, placement="offset")
+    torch.cuda.synchronize()
+    assert int((r.status != 0).sum()) == 0 and bool((r.nrec == recs).all())
+    per = 65536 // 8
+    idx = (torch.arange(nblk, device=dev)[:, None] * per + torch.arange(recs, device=dev)[None, :]).reshape(-1)
+    d = r.desc.view(-1, 4)[idx].cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+    want = (np.arange(nblk)[:, None] * 65536 + np.arange(recs)[None, :] * 124).reshape(-1)
+    assert np.array_equal(d["rec_off"], want.astype(np.uint64))
+    assert (d["key_len"] == 16).all() and (d["val_len"] == 100).all()

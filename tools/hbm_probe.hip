@@ -140,3 +140,55 @@ extern "C" int probe_blocks(int mode, const void *in, const uint64_t *off, const
     }
     return (int)hipGetLastError();
 }
+
+// ---- long-block streaming probe (the large-block decode's memory pattern) --
+// Persistent one-wave workgroups; wave w streams blocks w, w+W, ... of
+// `blk` bytes each through an NCH x 1 KiB LDS ring: consuming chunk c waits
+// (counted vmcnt) for chunk c only and tops the ring up to c + NCH - 1.
+template <int N>
+__device__ __forceinline__ void probe_wait(uint32_t k) {
+#define PW(i) case i: __asm__ __volatile__("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+    switch (k < N ? k : N - 1) {
+    PW(0) PW(1) PW(2) PW(3) PW(4) PW(5) PW(6) PW(7) PW(8) PW(9) PW(10) PW(11) PW(12) PW(13) PW(14)
+    default: __asm__ __volatile__("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+#undef PW
+}
+
+template <int NCH, int AUX>
+__global__ __launch_bounds__(64) void stream_ring(const uint8_t *in, uint32_t nblk, uint32_t blk,
+                                                  uint32_t *sink) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * 256];
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t acc = 0;
+    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(in + (uint64_t)b * blk), 0, blk, 0x00020000);
+        const uint32_t nch = blk / 1024;
+        uint32_t hi = 0;
+        for (uint32_t c = 0; c < nch; c++) {
+            uint32_t last = c + NCH < nch ? c + NCH : nch;
+            for (; hi < last; hi++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)&ring[(hi % NCH) * 256], 16, hi * 1024 + lane * 16, 0, 0, AUX);
+            probe_wait<NCH>(hi - c - 1);
+            acc ^= ring[(c % NCH) * 256 + lane * 4];
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+extern "C" int probe_stream(int nch, const void *in, uint32_t nblk, uint32_t blk, void *sink,
+                            int grid, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t *i = (const uint8_t *)in;
+    uint32_t *k = (uint32_t *)sink;
+    switch (nch) {
+    case 2: hipLaunchKernelGGL((stream_ring<2, 2>), dim3(grid), dim3(64), 0, s, i, nblk, blk, k); break;
+    case 4: hipLaunchKernelGGL((stream_ring<4, 2>), dim3(grid), dim3(64), 0, s, i, nblk, blk, k); break;
+    case 8: hipLaunchKernelGGL((stream_ring<8, 2>), dim3(grid), dim3(64), 0, s, i, nblk, blk, k); break;
+    case 16: hipLaunchKernelGGL((stream_ring<16, 2>), dim3(grid), dim3(64), 0, s, i, nblk, blk, k); break;
+    case 116: hipLaunchKernelGGL((stream_ring<16, 0>), dim3(grid), dim3(64), 0, s, i, nblk, blk, k); break;
+    case 108: hipLaunchKernelGGL((stream_ring<8, 0>), dim3(grid), dim3(64), 0, s, i, nblk, blk, k); break;
+    default: return -1;
+    }
+    return (int)hipGetLastError();
+}
