@@ -61,7 +61,8 @@ struct DecodeArgs {
     uint64_t *val_arena_off;
     uint32_t split;  // 1: blocks larger than the 4 KiB ring are left to decode_large_kernel
     uint32_t dbg;    // diagnostics only (LSM_DECODE_DBG): bit 0 no speculative runs,
-                     // bit 1 no global verification, bit 2 stop after one record
+                     // bit 2 stop after one record, bit 3 global verification of
+                     // streamed uniform blocks (A/B; off by default)
 };
 
 // Streams one block through this wave's LDS ring and serves u32 length
@@ -692,6 +693,7 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
             }
         }
         if (++ns == kWave) flush();
+        if (nr == 0) stamp(1);
         nr++;
         pos += S;
         if (a.dbg & 4) break;
@@ -753,7 +755,8 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
         for (bool first = true;; first = false) {
             if (pos >= n) break;
             // wait for the span the run can verify (64 records): all of a
-            // block that fits the ring, at most half the ring otherwise
+            // block that fits the ring, half the ring otherwise (the other
+            // half stays in flight while the run is checked)
             const uint32_t span_max = (LIN ? NCH : NCH / 2) * kChunk;
             const uint64_t span = (uint64_t)S * kWave + 8;
             const uint32_t want = span < span_max ? (uint32_t)span : span_max;
@@ -796,7 +799,7 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
                     miss = 0;
                 }
             }
-            if (!LIN && at_lim && j >= 4 && G != LSM_GRAMMAR_IDX && !(a.dbg & 2)) {
+            if (!LIN && at_lim && j >= 4 && G != LSM_GRAMMAR_IDX && (a.dbg & 8)) {
                 // A full run in a streamed block: test the same hypothesis on
                 // the rest of the block straight from global memory, 256
                 // records per batch with all their loads in flight (the ring
@@ -805,9 +808,12 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
                 // the chase's records (each check reads the record's own
                 // fields); the first mismatch goes back to the exact step.
                 gverify(K, V, S);
+                stamp(2);
                 break;
             }
-            if (j < 64) break;
+            // a run cut short by the landed limit goes on once more bytes
+            // have landed (no exact step in between); a mismatch ends it
+            if (j < 64 && !(at_lim && j > 0)) break;
         }
     }
     flush();
@@ -823,6 +829,7 @@ template <int G, uint32_t NCH>
 __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
     const uint32_t b = blockIdx.x;
+    stamp(0);
     const uint64_t off = uni64(a.blk_off[b]);
     const uint32_t n = uni(a.blk_len[b]);
     if (a.split && (off & 15) + (uint64_t)n > NCH * kChunk) return;
@@ -830,6 +837,7 @@ __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
         decode_block_v2<G, NCH, true>(a, b, ring, off, n);
     else
         decode_block_v2<G, NCH, false>(a, b, ring, off, n);
+    stamp(3);
 }
 
 template <int G, uint32_t NCH>
@@ -1593,7 +1601,7 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             if (!strcmp(e, "spec")) return 30;
             if (!strcmp(e, "large8")) return 40;
             if (!strcmp(e, "v2split")) return 41;
-            if (!strcmp(e, "v2r8")) return 42;
+            if (!strcmp(e, "v2r4")) return 42;
             if (!strcmp(e, "spec_w1")) return 31;
             if (!strcmp(e, "spec_w2")) return 32;
             if (!strcmp(e, "pipe")) return 33;
@@ -1606,7 +1614,9 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             return 0;
         }();
         switch (variant) {
-        case 0: return launch_v2<G, kNChunk>(a, s);  // one wave per block, 4 KiB ring
+        // one wave per block, 8 KiB ring: decode4k equal to a 4 KiB ring,
+        // decode64k 0.71 vs 0.58 of HBM peak (more in flight per wave)
+        case 0: return launch_v2<G, 8>(a, s);
         case 41: {
             // v2 for blocks that fit the 4 KiB ring, then the deep-ring
             // persistent kernel for the larger ones
@@ -1615,7 +1625,7 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             const int rc = launch_v2<G, kNChunk>(b, s);
             return rc ? rc : launch_large<G, kLargeNCH>(ctx, b, s);
         }
-        case 42: return launch_v2<G, 8>(a, s);
+        case 42: return launch_v2<G, kNChunk>(a, s);
         case 40: {
             DecodeArgs b = a;
             b.split = 1;
