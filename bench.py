@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
-                    choices=["decode4k", "decode64k", "mixed", "sst"])
+                    choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -362,13 +362,20 @@ def main():
     if args.config == "sst":
         from bench_sst import bench_sst  # encode path (config 3)
         out, data = bench_sst(args, world, rank, local)
+    elif args.config in ("sstdec", "sstdec1"):
+        from bench_sstdec import bench_sst_decode  # whole-.sst decode (§8(f) f1; config 1)
+        out, data = bench_sst_decode(args, world, rank, local)
     else:
         out, data = bench_decode(args, world, rank, local)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "sst":
-        out["cpu_baseline"] = cpu_baseline(args, data)
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "sst":
-        from bench_sst import cpu_baseline_sst
-        out["cpu_baseline"] = cpu_baseline_sst(args, data)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if args.config == "sst":
+            from bench_sst import cpu_baseline_sst
+            out["cpu_baseline"] = cpu_baseline_sst(args, data)
+        elif args.config in ("sstdec", "sstdec1"):
+            from bench_sstdec import cpu_baseline_sst_decode
+            out["cpu_baseline"] = cpu_baseline_sst_decode(args, data)
+        else:
+            out["cpu_baseline"] = cpu_baseline(args, data)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1,0 +1,106 @@
+"""Whole-.sst decode bench (BASELINE config 1 at one
+image): `python bench.py --config sstdec` decodes the config-3 image set
+(208 .sst images per GPU, built on the GPU by lsm_build_sst) with
+lsm_decode_sst -- SSTable.DecodeFrom + DecodeDataBlock + GetKeyValuePairs in
+one call; `--config sstdec1` decodes one 2,297,320-byte image (config 1).
+Secondary bench lines; the headline is block decode (bench.py).
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "go-lsm_amd"))
+
+import lsmgpu  # noqa: E402
+from lsmgpu import synth  # noqa: E402
+
+GIB = float(1 << 30)
+
+
+def bench_sst_decode(args, world, rank, local):
+    from bench import barrier, max_over_ranks, sum_over_ranks, HBM_PEAK_GBS
+    ctx = lsmgpu.Context(local)
+    one = args.config == "sstdec1"
+    n = 15_888 if one else (args.blocks or 100_000) * 33
+    keys, koff, vals, voff = synth.kv_stream(n, first=rank * n)
+    batch = lsmgpu.batch_to_device(ctx, keys, koff, vals, voff)
+    starts = lsmgpu.segment_files(ctx, koff, voff, lsmgpu.MAX_SSTABLE_SIZE)
+    sb = lsmgpu.build_sst(ctx, batch, starts)
+    torch.cuda.synchronize()
+    del batch
+    nf = len(starts) - 1
+    r = lsmgpu.alloc_sst_decode(ctx, sb.file_off, sb.file_size, int(sb.out.numel()))
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        lsmgpu.decode_sst_into(ctx, sb.out, r, stream=stream)
+    torch.cuda.synchronize()
+    meta = r.meta_numpy()
+    assert (meta["stage"] == 0).all() and int(meta["nidx"].sum()) == n, "decode failed"
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        lsmgpu.decode_sst_into(ctx, sb.out, r, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(world, time.perf_counter() - t0)
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    parsed = float(meta["data_size"].astype(np.float64).sum() +
+                   meta["idx_size"].astype(np.float64).sum())
+    parsed_all = sum_over_ranks(world, parsed)
+    # algorithmic bytes: both regions read; per record a key view (16 B), its
+    # i64 offset (8 B) and a value view (16 B) written; 112 B meta per file
+    alg = parsed + 40.0 * n + 112.0 * nf
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    out = {
+        "metric": "GiB/s of .sst data+index region bytes decoded to KV records",
+        "value": round(parsed_all * args.steps / elapsed / GIB, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seed 0x5EED, keys k%015d, splitmix64 values); images built on the GPU",
+        "config": {"workload": f"decode {nf} whole .sst image(s) per GPU ({n} records, "
+                               f"16 B keys / 100 B values, 2 MiB flush)",
+                   "files_per_gpu": nf, "records_per_gpu": n,
+                   "parsed_bytes_per_gpu": int(parsed),
+                   "parallelism": f"dp{world} (files per rank, no collective)"},
+        "roofline": {"bound": "hbm", "kernel": "lsm_decode_sst (4 launches)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "alg_bytes_per_launch": int(alg), "kernel_ms": round(kern_ms, 5)},
+    }
+    return out, (sb.out.cpu().numpy(), sb.file_off, sb.file_size, meta)
+
+
+def cpu_baseline_sst_decode(args, data):
+    """The oracle's SSTable decode (ora_sst_decode: framing, both chases,
+    join counts; oracle/lsm_oracle.c) on the same images, 1 thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as ora
+    img, file_off, file_size, meta = data
+    t, done, parsed = 0.0, 0, 0.0
+    f = 0
+    while (t < args.cpu_seconds or done == 0) and done < 10_000:
+        o, n = int(file_off[f]), int(file_size[f])
+        t0 = time.perf_counter()
+        ora.sst_decode(img[o:o + n])
+        t += time.perf_counter() - t0
+        parsed += float(meta["data_size"][f] + meta["idx_size"][f])
+        done += 1
+        f = (f + 1) % len(file_off)
+    return {"value": round(parsed / t / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{done} image decodes by the C restatement in {t:.1f} s (1 thread)"}

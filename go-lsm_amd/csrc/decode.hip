@@ -534,14 +534,12 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
     return v;
 }
 
+// Decode the byte range [off, off + n) of a.in as one block whose records
+// go to slots base.. (capacity ncap); returns the record count and status.
 template <int G, uint32_t NCH, bool LIN>
-__device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
-                                uint32_t n) {
+__device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
+                                uint64_t base, uint32_t ncap, uint32_t &nr_out, int32_t &st_out) {
     constexpr uint32_t kWords = NCH * kChunk / 4;
-    uint64_t base, cap;
-    record_slots<G>(a, b, off, n, base, cap);
-    base = uni64(base);
-    const uint32_t ncap = uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu);
     const uint32_t lane = lane_id();
     BlockReaderT<NCH> rd;
     rd.init(ring, a.in, off, n);
@@ -817,10 +815,33 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
         }
     }
     flush();
-    if (lane == 0) {
+    nr_out = nr;
+    st_out = status;
+}
+
+template <int G, uint32_t NCH, bool LIN>
+__device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
+                                uint32_t n) {
+    uint64_t base, cap;
+    record_slots<G>(a, b, off, n, base, cap);
+    uint32_t nr;
+    int32_t st;
+    decode_range_v2<G, NCH, LIN>(a, ring, off, n, uni64(base),
+                                 uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr, st);
+    if (lane_id() == 0) {
         a.nrec[b] = nr;
-        a.status[b] = status;
+        a.status[b] = st;
     }
+}
+
+// Either form of the range decoder: linear when the range fits the ring.
+template <int G, uint32_t NCH>
+__device__ void decode_range_any(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
+                                 uint64_t base, uint32_t ncap, uint32_t &nr, int32_t &st) {
+    if (((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk)
+        decode_range_v2<G, NCH, true>(a, ring, off, n, base, ncap, nr, st);
+    else
+        decode_range_v2<G, NCH, false>(a, ring, off, n, base, ncap, nr, st);
 }
 
 // One wave (and one workgroup) per block; NCH x 1 KiB ring plus a guard
@@ -1672,6 +1693,281 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
     return 0;
 }
 
+// ---- whole .sst files: SSTable.DecodeFrom + DecodeDataBlock + join ---------
+//
+// SURVEY.md §8(f) row f1.  go-lsm decodes a file's index region and data
+// region by two serial chases (index.go:61-101, data.go:49-79) and joins
+// value i with index key i (sstable.go:248-268).  Here, per file:
+//   1. sst_index_kernel: every workgroup parses the framing (header, filter
+//      prefix, footer; sstable.go:87-128); then all threads test the stride
+//      hypothesis "every index entry has the first entry's key length" on
+//      the whole index region at once.  Entry i verified <=> its key length
+//      field holds K0, so the serial chase visits exactly these entries.
+//   2. sst_index_fixup_kernel: one wave chases the index from the first
+//      entry the hypothesis failed on (decode_range_v2, exact semantics).
+//   3. sst_data_verify_kernel: the values are located by the index offsets
+//      (SSTable.EncodeTo writes value i at Indexes[i].Offset,
+//      sstable.go:164-169); value i is verified when it starts where value
+//      i-1 ended (value 0 at DataHandle.Offset) and ends where value i+1
+//      starts (the last one at the end of the region).  The verified values
+//      are exactly the serial chase's.
+//   4. sst_data_fixup_kernel: one wave chases the data region from the first
+//      unverified value, then applies GetKeyValuePairs' count rules and
+//      writes the per-file lsm_sst_meta.
+// A well-formed file costs two parallel passes; a corrupted one falls back
+// to the exact chase only from the first entry that cannot be vouched for.
+
+// Range-checked little-endian reads at byte offsets of one file image.
+struct ImgReader {
+    rsrc_t r;
+    uint32_t h;  // image start inside its 4-byte aligned base
+    __device__ void init(const uint8_t *img, uint64_t foff, uint64_t n) {
+        const uint64_t a0 = foff & ~(uint64_t)3;
+        h = (uint32_t)(foff - a0);
+        uint64_t tot = (h + n + 7) & ~(uint64_t)3;
+        if (tot > 0xFFFFFFF0ull) tot = 0xFFFFFFF0ull;
+        r = make_rsrc(img + a0, (uint32_t)tot);
+    }
+    __device__ uint32_t u32(uint64_t p) const {
+        const uint32_t s = h + (uint32_t)p;
+        return funnel(ld_b32(r, s & ~3u), ld_b32(r, (s & ~3u) + 4), s);
+    }
+    __device__ uint64_t u64(uint64_t p) const { return (uint64_t)u32(p + 4) << 32 | u32(p); }
+    __device__ uint64_t u64be(uint64_t p) const { return __builtin_bswap64(u64(p)); }
+};
+
+struct SstWork {
+    lsm_sst_meta m;
+    uint64_t io, il, dof, dl;  // index / data regions to decode (image-relative)
+    uint64_t base, cap;        // record slots of the file
+    uint32_t k0, spec_cnt;     // index stride hypothesis: key length, entries to test
+    uint32_t idx_overrun;      // IndexHandle.Size runs past the end of the file
+    uint32_t data_neg;         // DataHandle.Offset < 0: the seek fails
+};
+
+// SSTable.DecodeFrom's framing (sstable.go:87-128) as the oracle restates it
+// (oracle/lsm_oracle.c ora_sst_decode); one thread.
+__device__ void sst_parse(const ImgReader &R, uint64_t n, SstWork &w) {
+    lsm_sst_meta &m = w.m;
+    uint64_t pos = 0;
+    for (int j = 0; j < 2; j++) {  // Header.DecodeFrom header.go:40-52 (Key: no cap)
+        if (n - pos < 4) { m.stage = LSM_SST_HEADER; return; }
+        const uint32_t kl = R.u32(pos);
+        if (n - pos - 4 < kl) { m.stage = LSM_SST_HEADER; return; }
+        if (j == 0) { m.min_key_off = pos + 4; m.min_key_len = kl; }
+        else { m.max_key_off = pos + 4; m.max_key_len = kl; }
+        pos += 4 + (uint64_t)kl;
+    }
+    // Filter.DecodeFrom bloom.go:453-469 -> ReadFrom :262-281 -> bitset ReadFrom
+    if (n - pos < 8) { m.stage = LSM_SST_FILTER; return; }
+    const uint64_t L = R.u64(pos);
+    if (L > n - pos - 8 || L < 24) { m.stage = LSM_SST_FILTER; return; }
+    const uint64_t fm = R.u64be(pos + 8), fk = R.u64be(pos + 16), nb = R.u64be(pos + 24);
+    if ((nb + 63) / 64 > (L - 24) / 8) { m.stage = LSM_SST_FILTER; return; }
+    m.filter_m = fm;
+    m.filter_k = fk;
+    m.filter_nbits = nb;
+    m.filter_words_off = pos + 32;
+    // DecodeFooterFrom sstable.go:195-212
+    if (n < 32) { m.stage = LSM_SST_FOOTER; return; }
+    m.data_off = (int64_t)R.u64(n - 32);
+    m.data_size = (int64_t)R.u64(n - 24);
+    m.idx_off = (int64_t)R.u64(n - 16);
+    m.idx_size = (int64_t)R.u64(n - 8);
+    // seek to IndexHandle.Offset; IndexBlock.DecodeFrom rejects a negative size
+    if (m.idx_off < 0 || m.idx_size < 0) { m.stage = LSM_SST_INDEX; return; }
+    const uint64_t io = (uint64_t)m.idx_off, avail = io <= n ? n - io : 0;
+    w.io = io;
+    w.il = (uint64_t)m.idx_size < avail ? (uint64_t)m.idx_size : avail;
+    w.idx_overrun = (uint64_t)m.idx_size > avail;  // the file ends before the limit
+    // DecodeDataBlock: DataBlock.DecodeFrom(file, DataHandle.Size), size <= 0 = to EOF
+    w.data_neg = m.data_off < 0;
+    const uint64_t dof = w.data_neg ? 0 : (uint64_t)m.data_off;
+    const uint64_t davail = dof <= n ? n - dof : 0;
+    w.dof = dof;
+    w.dl = (m.data_size > 0 && (uint64_t)m.data_size < davail) ? (uint64_t)m.data_size : davail;
+}
+
+struct SstArgs {
+    const uint8_t *img;
+    const uint64_t *file_off, *file_len;
+    uint32_t nfile;
+    const uint64_t *rec_base;
+    lsm_sst_meta *meta;
+    u32x4 *idx_desc;
+    int64_t *idx_value;
+    u32x4 *data_desc;
+    SstWork *work;
+    uint32_t *fail;  // [2f] first unverified index entry, [2f+1] first unverified value
+};
+
+__device__ __forceinline__ void sst_slots(const SstArgs &a, uint32_t f, uint64_t foff, uint64_t n,
+                                          uint64_t &base, uint64_t &cap) {
+    if (a.rec_base) {
+        base = a.rec_base[f];
+        cap = a.rec_base[f + 1] - base;
+    } else {
+        base = foff / 4;
+        cap = (foff + n) / 4 - base;
+    }
+}
+
+__global__ __launch_bounds__(256) void sst_index_kernel(SstArgs a) {
+    __shared__ SstWork W;
+    const uint32_t f = blockIdx.y;
+    const uint64_t foff = a.file_off[f], n = a.file_len[f];
+    ImgReader R;
+    R.init(a.img, foff, n);
+    if (threadIdx.x == 0) {
+        memset(&W, 0, sizeof(W));
+        sst_parse(R, n, W);
+        sst_slots(a, f, foff, n, W.base, W.cap);
+        if (W.m.stage == 0 && W.il >= 4) {
+            W.k0 = R.u32(W.io);
+            const uint64_t cnt = W.il / (12ull + W.k0);
+            const uint64_t lim = W.cap < 0xFFFFFFFFull ? W.cap : 0xFFFFFFFFull;
+            W.spec_cnt = (uint32_t)(cnt < lim ? cnt : lim);
+        }
+        if (blockIdx.x == 0) a.work[f] = W;
+    }
+    __syncthreads();
+    if (W.m.stage != 0) return;
+    const uint64_t S = 12ull + W.k0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W.spec_cnt;
+         i += gridDim.x * blockDim.x) {
+        const uint64_t p = W.io + (uint64_t)i * S;
+        if (R.u32(p) == W.k0) {
+            const uint64_t ro = foff + p;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = W.k0;
+            d.w = 8;
+            a.idx_desc[W.base + i] = d;
+            a.idx_value[W.base + i] = (int64_t)R.u64(p + 4 + W.k0);
+        } else {
+            atomicMin(&a.fail[2 * f], i);
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void sst_index_fixup_kernel(SstArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
+    const uint32_t f = blockIdx.x;
+    SstWork &W = a.work[f];
+    if (uni((uint32_t)W.m.stage) != 0) return;
+    const uint32_t spec = uni(W.spec_cnt);
+    const uint32_t fl = uni(a.fail[2 * f]);
+    const uint32_t i0 = fl < spec ? fl : spec;
+    const uint64_t S = 12ull + uni(W.k0), il = uni64(W.il);
+    const bool overrun = uni(W.idx_overrun) != 0;
+    uint32_t nidx;
+    int32_t st = LSM_OK;
+    if (i0 == spec && (uint64_t)spec * S == il && !overrun) {
+        nidx = spec;
+    } else {
+        DecodeArgs d = {};
+        d.in = a.img;
+        d.desc = a.idx_desc;
+        d.idx_value = a.idx_value;
+        const uint64_t start = (uint64_t)i0 * S, cap = uni64(W.cap);
+        uint32_t nr = 0;
+        decode_range_any<LSM_GRAMMAR_IDX, 8>(
+            d, ring, uni64(a.file_off[f]) + uni64(W.io) + start, (uint32_t)(il - start),
+            uni64(W.base) + i0, (uint32_t)(cap - i0 < 0xFFFFFFFFull ? cap - i0 : 0xFFFFFFFFull), nr, st);
+        nidx = i0 + nr;
+        if (overrun && st == LSM_OK) st = LSM_ST_IDX_OVERRUN;  // index.go:73-91 reads past EOF
+    }
+    if (lane_id() == 0) {
+        W.m.nidx = nidx;
+        if (st != LSM_OK) {
+            W.m.stage = LSM_SST_INDEX;
+            W.m.status = st;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void sst_data_verify_kernel(SstArgs a) {
+    __shared__ SstWork W;
+    const uint32_t f = blockIdx.y;
+    if (threadIdx.x == 0) W = a.work[f];
+    __syncthreads();
+    if (W.m.stage != 0 || W.data_neg) return;
+    const uint64_t foff = a.file_off[f];
+    ImgReader R;
+    R.init(a.img, foff, a.file_len[f]);
+    const uint64_t doff = (uint64_t)W.m.data_off, dl = W.dl;
+    const uint32_t nidx = W.m.nidx;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nidx;
+         i += gridDim.x * blockDim.x) {
+        const uint64_t pos = (uint64_t)a.idx_value[W.base + i] - doff;  // value i, region-relative
+        bool bad = dl < 4 || pos > dl - 4 || (i == 0 && pos != 0);
+        if (!bad) {
+            const uint32_t v = R.u32(W.dof + pos);
+            const uint64_t e = pos + 4 + v;  // where value i ends
+            const uint64_t next = i + 1 < nidx ? (uint64_t)a.idx_value[W.base + i + 1] - doff : dl;
+            bad = e > dl || e != next;
+            const uint64_t ro = foff + W.dof + pos;
+            u32x4 d;
+            d.x = (uint32_t)ro;
+            d.y = (uint32_t)(ro >> 32);
+            d.z = 0;
+            d.w = v;
+            a.data_desc[W.base + i] = d;
+        }
+        if (bad) atomicMin(&a.fail[2 * f + 1], i);
+    }
+}
+
+__global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
+    const uint32_t f = blockIdx.x;
+    SstWork &W = a.work[f];
+    int32_t stage = (int32_t)uni((uint32_t)W.m.stage);
+    int32_t status = (int32_t)uni((uint32_t)W.m.status);
+    const uint32_t nidx = uni(W.m.nidx);
+    uint32_t ndata = 0;
+    if (stage == LSM_SST_OK) {
+        if (uni(W.data_neg)) {
+            stage = LSM_SST_DATA;  // seek to a negative offset
+        } else {
+            const uint32_t fl = uni(a.fail[2 * f + 1]);
+            const uint32_t f0 = nidx == 0 ? 0u : (fl < nidx ? fl : nidx);
+            int32_t st = LSM_OK;
+            if (nidx > 0 && f0 == nidx) {
+                ndata = nidx;
+            } else {
+                const uint64_t doff = uni64((uint64_t)W.m.data_off), dl = uni64(W.dl);
+                const uint64_t start =
+                    f0 == 0 ? 0 : uni64((uint64_t)a.idx_value[uni64(W.base) + f0] - doff);
+                DecodeArgs d = {};
+                d.in = a.img;
+                d.desc = a.data_desc;
+                const uint64_t cap = uni64(W.cap);
+                uint32_t nr = 0;
+                decode_range_any<LSM_GRAMMAR_V, 8>(
+                    d, ring, uni64(a.file_off[f]) + uni64(W.dof) + start, (uint32_t)(dl - start),
+                    uni64(W.base) + f0,
+                    (uint32_t)(cap - f0 < 0xFFFFFFFFull ? cap - f0 : 0xFFFFFFFFull), nr, st);
+                ndata = f0 + nr;
+            }
+            if (st != LSM_OK) {
+                stage = LSM_SST_DATA;
+                status = st;
+            } else if (nidx && ndata && nidx != ndata) {
+                stage = LSM_SST_MISMATCH;  // GetKeyValuePairs sstable.go:254-257
+            }
+        }
+    }
+    if (lane_id() == 0) {
+        lsm_sst_meta m = W.m;
+        m.stage = stage;
+        m.status = status;
+        m.ndata = ndata;
+        a.meta[f] = m;
+    }
+}
+
 }  // namespace
 }  // namespace lsm
 
@@ -1793,6 +2089,49 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
     default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true>(ctx, a, s)
                           : launch_decode<LSM_GRAMMAR_IDX, false>(ctx, a, s);
     }
+}
+
+
+extern "C" size_t lsm_decode_sst_workspace_bytes(uint32_t nfile) {
+    return (size_t)nfile * (sizeof(SstWork) + 8) + 16;
+}
+
+extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                              const uint64_t *d_file_len, uint32_t nfile,
+                              const uint64_t *d_rec_base, lsm_sst_meta *d_meta,
+                              lsm_rec_desc *d_idx_desc, int64_t *d_idx_value,
+                              lsm_rec_desc *d_data_desc, void *d_workspace, size_t ws_bytes,
+                              void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nfile == 0) return 0;
+    if (nfile > 65535 || !d_img || !d_file_off || !d_file_len || !d_meta || !d_idx_desc ||
+        !d_idx_value || !d_data_desc || !d_workspace)
+        return LSM_EINVAL;
+    if (ws_bytes < lsm_decode_sst_workspace_bytes(nfile)) return LSM_ESPACE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    SstArgs a;
+    a.img = d_img;
+    a.file_off = d_file_off;
+    a.file_len = d_file_len;
+    a.nfile = nfile;
+    a.rec_base = d_rec_base;
+    a.meta = d_meta;
+    a.idx_desc = reinterpret_cast<u32x4 *>(d_idx_desc);
+    a.idx_value = d_idx_value;
+    a.data_desc = reinterpret_cast<u32x4 *>(d_data_desc);
+    a.work = static_cast<SstWork *>(d_workspace);
+    a.fail = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) +
+                                          (size_t)nfile * sizeof(SstWork));
+    LSM_HIP_CHECK(hipMemsetAsync(a.fail, 0xFF, (size_t)nfile * 8, s));
+    // parallel passes: ~2048 workgroups over the batch, at most 64 per file
+    uint32_t g = (2048 + nfile - 1) / nfile;
+    if (g > 64) g = 64;
+    hipLaunchKernelGGL(sst_index_kernel, dim3(g, nfile), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(sst_index_fixup_kernel, dim3(nfile), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(sst_data_verify_kernel, dim3(g, nfile), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(sst_data_fixup_kernel, dim3(nfile), dim3(kWave), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 #ifdef LSM_STAMPS

@@ -9,5 +9,6 @@ from .codec import (  # noqa: F401
     MAX_SSTABLE_SIZE, STATUS_NAMES, Context, DenseRecords, alloc_decode, alloc_decode_offset,
     alloc_dense, batch_to_device, bloom_probe, build_sst, build_sst_into, compact_into,
     decode_blocks, decode_into, encode_blocks, pad16, plan, prepare_sst, replan, segment_files,
-    sum256, to_device_bytes)
+    sum256, to_device_bytes, SST_META_DTYPE, SST_STAGE_NAMES, SstDecode, alloc_sst_decode,
+    decode_sst, decode_sst_into)
 from . import synth  # noqa: F401

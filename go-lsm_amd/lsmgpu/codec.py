@@ -283,6 +283,76 @@ def compact_into(ctx: Context, grammar: int, blk_off: torch.Tensor, r: DecodeRes
         _stream_handle(stream)), "lsm_compact_records")
 
 
+# ---- whole .sst files (lsm_decode_sst) ----------------------------------------
+
+SST_META_DTYPE = np.dtype([
+    ("min_key_off", "<u8"), ("min_key_len", "<u8"), ("max_key_off", "<u8"), ("max_key_len", "<u8"),
+    ("filter_m", "<u8"), ("filter_k", "<u8"), ("filter_nbits", "<u8"), ("filter_words_off", "<u8"),
+    ("data_off", "<i8"), ("data_size", "<i8"), ("idx_off", "<i8"), ("idx_size", "<i8"),
+    ("stage", "<i4"), ("status", "<i4"), ("nidx", "<u4"), ("ndata", "<u4")])
+assert SST_META_DTYPE.itemsize == 112
+
+SST_STAGE_NAMES = {0: "ok", 1: "header", 2: "filter", 3: "footer", 4: "index", 5: "data",
+                   6: "mismatch"}
+
+
+@dataclass
+class SstDecode:
+    """lsm_decode_sst outputs: file f's entries at slots base(f).. of the
+    per-record arrays (offset addressing: base(f) = file_off[f] // 4)."""
+    meta: torch.Tensor        # uint8[nfile * 112] = lsm_sst_meta
+    idx_desc: torch.Tensor    # int32[cap, 4]
+    idx_value: torch.Tensor   # int64[cap]
+    data_desc: torch.Tensor   # int32[cap, 4]
+    workspace: torch.Tensor
+    d_file_off: torch.Tensor
+    d_file_len: torch.Tensor
+    file_off: np.ndarray
+    nfile: int
+
+    def meta_numpy(self) -> np.ndarray:
+        return self.meta.cpu().numpy().view(SST_META_DTYPE).reshape(-1)
+
+    def bases(self) -> np.ndarray:
+        return self.file_off // 4
+
+
+def alloc_sst_decode(ctx: Context, file_off: np.ndarray, file_len: np.ndarray,
+                     img_bytes: int) -> SstDecode:
+    dev = ctx.torch_device
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
+    file_len = np.ascontiguousarray(file_len, dtype=np.uint64)
+    nf = file_off.size
+    cap = img_bytes // 4 + 1
+    ws = int(ctx.lib.lsm_decode_sst_workspace_bytes(nf))
+    return SstDecode(
+        meta=torch.zeros(max(nf, 1) * SST_META_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+        idx_desc=torch.zeros((cap, 4), dtype=torch.int32, device=dev),
+        idx_value=torch.zeros(cap, dtype=torch.int64, device=dev),
+        data_desc=torch.zeros((cap, 4), dtype=torch.int32, device=dev),
+        workspace=torch.empty(max(ws, 16), dtype=torch.uint8, device=dev),
+        d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
+        d_file_len=torch.from_numpy(file_len.view(np.int64)).to(dev),
+        file_off=file_off, nfile=nf)
+
+
+def decode_sst_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, stream=None) -> None:
+    _lib.check(ctx.lib.lsm_decode_sst(
+        ctx.handle, _ptr(d_img), _ptr(r.d_file_off), _ptr(r.d_file_len), r.nfile, None,
+        _ptr(r.meta), _ptr(r.idx_desc), _ptr(r.idx_value), _ptr(r.data_desc), _ptr(r.workspace),
+        r.workspace.numel(), _stream_handle(stream)), "lsm_decode_sst")
+
+
+def decode_sst(ctx: Context, d_img: torch.Tensor, file_off: np.ndarray, file_len: np.ndarray,
+               stream=None) -> SstDecode:
+    """Decode whole .sst images (SSTable.DecodeFrom + DecodeDataBlock +
+    GetKeyValuePairs) held in d_img at file_off[f], file_len[f] bytes each."""
+    r = alloc_sst_decode(ctx, file_off, file_len, int(d_img.numel()))
+    if r.nfile:
+        decode_sst_into(ctx, d_img, r, stream=stream)
+    return r
+
+
 # ---- encode -----------------------------------------------------------------
 
 @dataclass

@@ -157,6 +157,51 @@ int lsm_compact_records(lsm_ctx *ctx, int grammar, const uint64_t *d_blk_off, ui
                         const lsm_decode_out *out, lsm_rec_desc *d_dense, int64_t *d_dense_idx,
                         uint64_t *d_dense_base, void *d_workspace, size_t ws_bytes, void *stream);
 
+/* ---- whole .sst files ------------------------------------------------------ */
+
+/* Per-file result of lsm_decode_sst.  Offsets are relative to the file image. */
+typedef struct lsm_sst_meta {
+    uint64_t min_key_off, min_key_len, max_key_off, max_key_len; /* Header      header.go:40-52 */
+    uint64_t filter_m, filter_k, filter_nbits;                   /* Filter      bloom.go:453-469 */
+    uint64_t filter_words_off; /* first filter word (u64 big-endian, bitset v1.22.0 WriteTo)   */
+    int64_t data_off, data_size, idx_off, idx_size;              /* Footer      footer.go:58-70 */
+    int32_t stage;   /* enum lsm_sst_stage: the first step that failed, 0 = none               */
+    int32_t status;  /* lsm_status of a failing index (stage 4) or data (stage 5) decode       */
+    uint32_t nidx;   /* index entries decoded (those before an error are kept, index.go:94)  */
+    uint32_t ndata;  /* values decoded (those before an error are kept, data.go:75)          */
+} lsm_sst_meta;
+
+enum lsm_sst_stage {
+    LSM_SST_OK = 0,
+    LSM_SST_HEADER = 1,   /* sstable.go:101-104 "decode Header failed"                       */
+    LSM_SST_FILTER = 2,   /* sstable.go:106-109 "decode FilterBlock failed"                  */
+    LSM_SST_FOOTER = 3,   /* sstable.go:112-115 "decode Footer failed" (file < 32 bytes)     */
+    LSM_SST_INDEX = 4,    /* sstable.go:118-125 seek / "decode IndexBlock failed"            */
+    LSM_SST_DATA = 5,     /* sstable.go:214-225 seek / "decode DataBlock failed"             */
+    LSM_SST_MISMATCH = 6, /* sstable.go:254-257 "mismatched DataBlock and IndexBlock entries" */
+};
+
+size_t lsm_decode_sst_workspace_bytes(uint32_t nfile);
+
+/* Decode nfile whole .sst images [file_off[f], file_off[f] + file_len[f]) of
+ * d_img: SSTable.DecodeFrom (sstable.go:87-128: header, filter, footer, the
+ * IndexBlock chase), DecodeDataBlock (:214-225: the DataBlock chase over
+ * DataHandle, data.go:49-79) and GetKeyValuePairs (:248-268: the positional
+ * join) in one call.  Entry i of file f goes to slot base(f) + i of
+ * d_idx_desc / d_idx_value (key view + i64 offset) and of d_data_desc (value
+ * view); record i is (key of idx entry i, value i) for
+ * i < (stage == 0 && nidx && ndata ? nidx : 0).  base(f) = d_rec_base[f]
+ * with capacity d_rec_base[f+1] - base(f), or with d_rec_base == NULL,
+ * file_off[f] / 4 with capacity (file_off[f] + file_len[f]) / 4 - base(f).
+ * The results equal the reference's serial chases; the index and the values
+ * are verified in parallel (stride hypothesis, index offsets) and chased
+ * exactly from the first entry the verification cannot vouch for.
+ * Workspace: lsm_decode_sst_workspace_bytes(nfile). */
+int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                   const uint64_t *d_file_len, uint32_t nfile, const uint64_t *d_rec_base,
+                   lsm_sst_meta *d_meta, lsm_rec_desc *d_idx_desc, int64_t *d_idx_value,
+                   lsm_rec_desc *d_data_desc, void *d_workspace, size_t ws_bytes, void *stream);
+
 /* ---- encode ---------------------------------------------------------------- */
 
 /* Batch encode of a columnar record batch (CSR: record i's key is
