@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
-                    choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1"])
+                    choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -128,6 +128,18 @@ def make_workload(args, world, rank):
         total = (args.blocks or 1 << 30)
         buf, off, ln, _ = synth.mixed_kv_blocks(total, seed=synth.SEED + rank)
         return buf, off, ln, "decode mixed 4/16/64 KiB KV blocks, values log-uniform 8 B-4 KiB"
+    if args.config == "wal":
+        # §8(f) f4: wal.Recover of memtable-sized logs shaped by go-lsm's
+        # benchmark; 16 distinct logs generated, dealt 4x (generation is slow)
+        nlog = args.blocks or 64
+        b16, o16, l16, _ = synth.wal_logs(min(16, nlog), seed=synth.SEED + rank)
+        reps = (nlog + 15) // 16
+        span = b16.size
+        buf = np.tile(b16, reps)
+        off = np.concatenate([o16 + np.uint64(r * span) for r in range(reps)])[:nlog]
+        ln = np.tile(l16, reps)[:nlog]
+        return buf, off, ln, (f"replay {nlog} write-ahead logs per GPU (2 MiB memtables, "
+                              "benchmark.go-shaped records)")
     raise ValueError(args.config)
 
 
@@ -143,8 +155,14 @@ def bench_decode(args, world, rank, local):
                                    arena=args.arena)
     stream = torch.cuda.current_stream()
 
+    wal_max = int(blk_len.max()) if args.config == "wal" else 0
+    wal_ws = lsmgpu.wal_workspace(ctx, nblk, wal_max) if args.config == "wal" else None
+
     def step():
-        lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream)
+        if args.config == "wal":
+            lsmgpu.wal_replay_into(ctx, d_in, d_off, d_len, wal_max, r, wal_ws, stream=stream)
+        else:
+            lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -207,7 +225,7 @@ def bench_decode(args, world, rank, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "decode_spec_kernel<KV,1,1>",
+            "kernel": "decode_v2_kernel<KV,8>",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -535,10 +535,13 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
 }
 
 // Decode the byte range [off, off + n) of a.in as one block whose records
-// go to slots base.. (capacity ncap); returns the record count and status.
+// go to slots base.. (capacity ncap); returns the record count, the status
+// and the position where the chase stopped.  Records that start at or past
+// `stop` are not decoded (a clean stop; stop = n decodes the whole range).
 template <int G, uint32_t NCH, bool LIN>
 __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
-                                uint64_t base, uint32_t ncap, uint32_t &nr_out, int32_t &st_out) {
+                                uint64_t base, uint32_t ncap, uint32_t &nr_out, int32_t &st_out,
+                                uint32_t stop, uint32_t &pos_out) {
     constexpr uint32_t kWords = NCH * kChunk / 4;
     const uint32_t lane = lane_id();
     BlockReaderT<NCH> rd;
@@ -637,7 +640,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     for (;;) {
         // ---- exact step at pos (same checks and order as the reference) ----
         const uint32_t rem = n - pos;
-        if (rem == 0) break;
+        if (rem == 0 || pos >= stop) break;
         if (rem < 4) {
             status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
             break;
@@ -700,40 +703,49 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
         // After a failed run (skip > 0) the following records are chased with
         // the cursor in a VGPR: all lanes compute the same step, the checks
         // combine into one ballot and the scalar unit only counts.  The step
-        // assumes the key length of the previous record and reads the value
-        // length at that offset in the same LDS round trip; any record it
-        // cannot vouch for (other key length, not yet landed, an error, the
-        // block end, capacity) drops back to the exact step above.
+        // guesses the previous record's key length and reads the value length
+        // there in the same LDS round trip (re-read when the key length
+        // differs); any record it cannot vouch for (a key over 1 KiB, bytes
+        // not yet landed, an error, the block end, capacity) drops back to the
+        // exact step above.
         if (skip) {
             skip--;
             if (G == LSM_GRAMMAR_KV && kprev <= kChunk - 8) {
-                uint32_t vpos = to_vgpr(pos);
-                const uint32_t need8 = 8 + kprev;
+                uint32_t vpos = to_vgpr(pos), kp = to_vgpr(kprev);
                 while (nr < ncap) {
-                    const uint32_t sb = rd.h + vpos, sv = sb + 4 + kprev;
+                    const uint32_t sb = rd.h + vpos, sv = sb + 4 + kp;
                     const uint32_t k = funnel(word(sb >> 2), word((sb >> 2) + 1), sb);
-                    const uint32_t v = funnel(word(sv >> 2), word((sv >> 2) + 1), sv);
+                    uint32_t v = funnel(word(sv >> 2), word((sv >> 2) + 1), sv);
+                    // a key of another length: the value length is elsewhere
+                    // (one more LDS round trip, still on the vector ALU)
+                    if (!__ballot(k == kp) && __ballot(k <= kChunk - 8)) {
+                        const uint32_t sw = sb + 4 + k;
+                        v = funnel(word(sw >> 2), word((sw >> 2) + 1), sw);
+                    }
                     const uint32_t rem = n - vpos;
-                    const bool ok = (vpos <= lim) & (lim - vpos >= need8) & (k == kprev) &
-                                    (v <= kValCap) & (rem - need8 >= v);
+                    const bool ok = (k <= kChunk - 8) & (vpos <= lim) & (lim - vpos >= 8 + k) &
+                                    (v <= kValCap) & (rem - 8 - k >= v) & (vpos < stop);
                     if (!__ballot(ok)) break;
                     if (ns == 0) s_first = nr;
                     const bool me = lane == ns;
                     s_pos = me ? vpos : s_pos;
-                    s_k = me ? kprev : s_k;
+                    s_k = me ? k : s_k;
                     s_v = me ? v : s_v;
                     if (++ns == kWave) flush();
                     nr++;
-                    vpos += need8 + v;
+                    vpos += 8 + k + v;
+                    kp = k;
                 }
                 pos = uni(vpos);
+                kprev = uni(kp);
             } else if (G == LSM_GRAMMAR_V) {
                 uint32_t vpos = to_vgpr(pos);
                 while (nr < ncap) {
                     const uint32_t sb = rd.h + vpos;
                     const uint32_t v = funnel(word(sb >> 2), word((sb >> 2) + 1), sb);
                     const uint32_t rem = n - vpos;
-                    const bool ok = (vpos <= lim) & (lim - vpos >= 4u) & (rem - 4 >= v);
+                    const bool ok = (vpos <= lim) & (lim - vpos >= 4u) & (rem - 4 >= v) &
+                                    (vpos < stop);
                     if (!__ballot(ok)) break;
                     if (ns == 0) s_first = nr;
                     const bool me = lane == ns;
@@ -761,7 +773,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
             need(pos, n - pos < want ? n - pos : want);
             const uint64_t pe = (uint64_t)pos + (uint64_t)(lane + 1) * S;  // record end
             const uint32_t p = pos + lane * S;
-            bool ok = pe <= lim && nr + lane < ncap;
+            bool ok = pe <= lim && nr + lane < ncap && p < stop;
             uint64_t xx = 0;
             if (ok) {
                 if (G == LSM_GRAMMAR_V) {
@@ -797,7 +809,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                     miss = 0;
                 }
             }
-            if (!LIN && at_lim && j >= 4 && G != LSM_GRAMMAR_IDX && (a.dbg & 8)) {
+            if (!LIN && at_lim && j >= 4 && G != LSM_GRAMMAR_IDX && (a.dbg & 8) && stop >= n) {
                 // A full run in a streamed block: test the same hypothesis on
                 // the rest of the block straight from global memory, 256
                 // records per batch with all their loads in flight (the ring
@@ -817,6 +829,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     flush();
     nr_out = nr;
     st_out = status;
+    pos_out = pos;
 }
 
 template <int G, uint32_t NCH, bool LIN>
@@ -824,10 +837,11 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
                                 uint32_t n) {
     uint64_t base, cap;
     record_slots<G>(a, b, off, n, base, cap);
-    uint32_t nr;
+    uint32_t nr, end;
     int32_t st;
     decode_range_v2<G, NCH, LIN>(a, ring, off, n, uni64(base),
-                                 uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr, st);
+                                 uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr, st, n,
+                                 end);
     if (lane_id() == 0) {
         a.nrec[b] = nr;
         a.status[b] = st;
@@ -837,11 +851,14 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
 // Either form of the range decoder: linear when the range fits the ring.
 template <int G, uint32_t NCH>
 __device__ void decode_range_any(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
-                                 uint64_t base, uint32_t ncap, uint32_t &nr, int32_t &st) {
+                                 uint64_t base, uint32_t ncap, uint32_t &nr, int32_t &st,
+                                 uint32_t stop = 0xFFFFFFFFu, uint32_t *end = nullptr) {
+    uint32_t e;
     if (((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk)
-        decode_range_v2<G, NCH, true>(a, ring, off, n, base, ncap, nr, st);
+        decode_range_v2<G, NCH, true>(a, ring, off, n, base, ncap, nr, st, stop, e);
     else
-        decode_range_v2<G, NCH, false>(a, ring, off, n, base, ncap, nr, st);
+        decode_range_v2<G, NCH, false>(a, ring, off, n, base, ncap, nr, st, stop, e);
+    if (end) *end = e;
 }
 
 // One wave (and one workgroup) per block; NCH x 1 KiB ring plus a guard
@@ -1968,6 +1985,247 @@ __global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
     }
 }
 
+// ---- WAL replay: one long KV stream per log ----------
+//
+// wal.Recover chases a whole log (~1.7 MB, ~44k records for a 2 MiB
+// memtable) as one serial chain; one wave per log would take milliseconds.
+// The log is cut into 16 KiB segments, one wave each:
+//   wal_seg_kernel: two waves per segment guess where its first record starts
+//     (the first position from which three records in a row have plausible
+//     lengths).  A record is two length-prefixed fields, so a chain started
+//     at a value-length field looks just as plausible, one field out of
+//     phase, and never meets the true chain: wave 0 chases from the guess g,
+//     wave 1 from g + 4 + u32(g) (the record after the value if g was a
+//     value length).  Each chases to the first record starting in the next
+//     segment and writes its records to a scratch area of its own.
+//   wal_stitch_kernel: one wave per log walks the segments in order with the
+//     true chain position e (0 at the start).  A chain of the segment that
+//     starts at e is the serial chase's (same start, same deterministic
+//     chain); if neither does, the segment is chased again from e.  The
+//     first error ends the log, as it ends Recover.
+//   wal_compact_kernel: each segment's records move to their final slots.
+// The result equals one serial chase for any input; guesses only decide how
+// much is chased twice.
+constexpr uint32_t kWalSeg = 16 * 1024;
+constexpr uint32_t kWalSegSlots = kWalSeg / 8 + 1;  // records starting in a segment
+
+struct WalSeg {
+    uint32_t entry, exit, nrec;
+    int32_t status;
+};
+
+struct WalArgs {
+    const uint8_t *wal;
+    const uint64_t *wal_off;
+    const uint32_t *wal_len;
+    uint32_t nwal, segs, max_len;
+    lsm_decode_out out;
+    WalSeg *seg;      // nwal * segs * 2 (two phases)
+    uint32_t *fin;    // nwal * segs * 2: prefix, count | phase << 31
+    u32x4 *scratch;   // nwal * segs * 2 * kWalSegSlots
+};
+
+__device__ __forceinline__ void wal_slots(const WalArgs &a, uint32_t w, uint64_t &base,
+                                          uint64_t &cap) {
+    if (a.out.rec_base) {
+        base = a.out.rec_base[w];
+        cap = a.out.rec_base[w + 1] - base;
+    } else {
+        const uint64_t o = a.wal_off[w];
+        base = o / 8;
+        cap = (o + a.wal_len[w]) / 8 - base;
+    }
+}
+
+__global__ __launch_bounds__(64) void wal_seg_kernel(WalArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
+    const uint32_t s = blockIdx.x >> 1, ph = blockIdx.x & 1, w = blockIdx.y, lane = lane_id();
+    const uint32_t len = uni(a.wal_len[w]);
+    const uint64_t off = uni64(a.wal_off[w]);
+    const uint64_t q = ((uint64_t)w * a.segs + s) * 2 + ph;
+    WalSeg &T = a.seg[q];
+    const uint32_t start = s * kWalSeg;
+    if (start >= len || len > a.max_len) {
+        if (lane == 0) T = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+        return;
+    }
+    uint32_t g = start;
+    if (s > 0) {
+        // stage up to 4 KiB of the segment head, then test 64 candidate
+        // starts per round: records of plausible lengths in a row (key <=
+        // 1 KiB, value <= 1 MiB, inside the log), at least two of them read
+        // within the staged bytes or one that ends the log; a guess only
+        // decides what the stitch must re-chase, never the result
+        const uint64_t a0 = (off + start) & ~(uint64_t)15;
+        const uint32_t h = (uint32_t)(off + start - a0);
+        const uint32_t W = len - start < kRingBytes - 16 ? len - start : kRingBytes - 16;
+        const rsrc_t r = make_rsrc(a.wal + a0, (h + W + 15) & ~15u);
+#pragma unroll
+        for (uint32_t c = 0; c < kNChunk; c++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r, (__attribute__((address_space(3))) void *)&ring[c * (kChunk / 4)], 16,
+                c * kChunk + lane * 16, 0, 0, kBlockLoadAux);
+        __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+        auto rd = [&](uint32_t q) -> uint32_t {
+            const uint32_t sb = h + q;
+            return funnel(ring[sb >> 2], ring[(sb >> 2) + 1], sb);
+        };
+        const uint32_t rlen = W < 2048 ? W : 2048;
+        g = 0xFFFFFFFFu;
+        for (uint32_t t0 = 0; t0 < rlen && g == 0xFFFFFFFFu; t0 += kWave) {
+            const uint32_t p = t0 + lane;
+            bool ok = p < rlen;
+            uint32_t q = p, seen = 0;
+            for (int rec = 0; rec < 3 && ok; rec++) {
+                if ((uint64_t)start + q == len) { seen = 2; break; }  // ends the log exactly
+                if (q + 8 > W) break;
+                const uint32_t k = rd(q);
+                if (k > 1024 || (uint64_t)start + q + 8 + k > len) { ok = false; break; }
+                if (q + 8 + k > W) break;
+                const uint32_t v = rd(q + 4 + k);
+                if (v > (1u << 20) || (uint64_t)start + q + 8 + k + v > len) { ok = false; break; }
+                q += 8 + k + v;
+                seen++;
+            }
+            ok = ok && seen >= 2;
+            const uint64_t m = __ballot(ok);
+            if (m) g = start + t0 + (uint32_t)__builtin_ctzll(m);
+        }
+        if (g == 0xFFFFFFFFu) g = start;
+        if (ph == 1) {  // the other phase: g read as a value length
+            const uint32_t v = g - start + 4 <= W ? rd(g - start) : 0xFFFFFFFFu;
+            g = (uint64_t)g + 4 + v <= len ? g + 4 + v : len;
+        }
+    } else if (ph == 1) {
+        if (lane == 0) T = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};  // segment 0 starts at 0
+        return;
+    }
+    g = uni(g);
+    if (g >= len || g >= start + kWalSeg) {
+        if (lane == 0) T = WalSeg{g, g, 0, 0};
+        return;
+    }
+    const uint32_t stop = (start + kWalSeg < len ? start + kWalSeg : len) - g;
+    DecodeArgs d = {};
+    d.in = a.wal;
+    d.desc = a.scratch;
+    uint32_t nr = 0, endp = 0;
+    int32_t st = LSM_OK;
+    decode_range_any<LSM_GRAMMAR_KV, 8>(d, ring, off + g, len - g, q * kWalSegSlots, kWalSegSlots,
+                                        nr, st, stop, &endp);
+    if (lane == 0) T = WalSeg{g, g + endp, nr, st};
+}
+
+__global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
+    const uint32_t w = blockIdx.x, lane = lane_id();
+    const uint32_t len = uni(a.wal_len[w]);
+    const uint64_t off = uni64(a.wal_off[w]);
+    uint64_t base, cap;
+    wal_slots(a, w, base, cap);
+    base = uni64(base);
+    const uint32_t ocap = uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu);
+    if (len > a.max_len) {  // outside the segment grid: one exact chase, in place
+        DecodeArgs d = {};
+        d.in = a.wal;
+        d.desc = a.out.desc ? reinterpret_cast<u32x4 *>(a.out.desc) : nullptr;
+        uint32_t nr = 0;
+        int32_t st = LSM_OK;
+        decode_range_any<LSM_GRAMMAR_KV, 8>(d, ring, off, len, base, ocap, nr, st);
+        for (uint32_t s = lane; s < a.segs; s += kWave) {
+            a.fin[2 * ((uint64_t)w * a.segs + s)] = 0;
+            a.fin[2 * ((uint64_t)w * a.segs + s) + 1] = 0;
+        }
+        if (lane == 0) {
+            a.out.nrec[w] = nr;
+            a.out.status[w] = st;
+        }
+        return;
+    }
+    const uint32_t nseg = (len + kWalSeg - 1) / kWalSeg;
+    uint32_t e = 0, total = 0;
+    int32_t status = LSM_OK;
+    bool dead = false;
+    for (uint32_t s0 = 0; s0 < a.segs; s0 += kWave) {
+        const uint32_t sl = s0 + lane;
+        const uint64_t q0 = ((uint64_t)w * a.segs + sl) * 2;
+        const WalSeg T0 = sl < nseg ? a.seg[q0] : WalSeg{0, 0, 0, 0};
+        const WalSeg T1 = sl < nseg ? a.seg[q0 + 1] : WalSeg{0, 0, 0, 0};
+        uint32_t f_pre = 0, f_cnt = 0;
+        for (uint32_t j = 0; j < kWave && s0 + j < nseg; j++) {
+            const uint32_t s = s0 + j;
+            uint32_t pre = total, cnt = 0;
+            if (!dead && e < len && e < (s + 1) * kWalSeg) {
+                const uint32_t e0 = uni(__builtin_amdgcn_readlane(T0.entry, j));
+                const uint32_t e1 = uni(__builtin_amdgcn_readlane(T1.entry, j));
+                const uint32_t ph = e0 == e ? 0u : e1 == e ? 1u : 2u;
+                uint32_t ex, nr;
+                int32_t st;
+                if (ph == 0) {
+                    ex = uni(__builtin_amdgcn_readlane(T0.exit, j));
+                    nr = uni(__builtin_amdgcn_readlane(T0.nrec, j));
+                    st = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)T0.status, j));
+                } else if (ph == 1) {
+                    ex = uni(__builtin_amdgcn_readlane(T1.exit, j));
+                    nr = uni(__builtin_amdgcn_readlane(T1.nrec, j));
+                    st = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)T1.status, j));
+                } else {  // both guesses missed: chase from the true position
+                    DecodeArgs d = {};
+                    d.in = a.wal;
+                    d.desc = a.scratch;
+                    const uint32_t stop = ((s + 1) * kWalSeg < len ? (s + 1) * kWalSeg : len) - e;
+                    uint32_t endp = 0;
+                    nr = 0;
+                    st = LSM_OK;
+                    decode_range_any<LSM_GRAMMAR_KV, 8>(
+                        d, ring, off + e, len - e, ((uint64_t)w * a.segs + s) * 2 * kWalSegSlots,
+                        kWalSegSlots, nr, st, stop, &endp);
+                    ex = e + endp;
+                }
+                cnt = nr | (ph == 1 ? 0x80000000u : 0u);
+                total += nr;
+                e = ex;
+                if (st != LSM_OK) {
+                    status = st;
+                    dead = true;
+                }
+            } else if (e >= len) {
+                dead = true;
+            }
+            if (lane == j) {
+                f_pre = pre;
+                f_cnt = cnt;
+            }
+        }
+        if (sl < a.segs) {
+            a.fin[2 * ((uint64_t)w * a.segs + sl)] = f_pre;
+            a.fin[2 * ((uint64_t)w * a.segs + sl) + 1] = f_cnt;
+        }
+    }
+    if (lane == 0) {
+        if (total > ocap) {  // caller's record capacity (not a reference error)
+            total = ocap;
+            status = LSM_ST_CAPACITY;
+        }
+        a.out.nrec[w] = total;
+        a.out.status[w] = status;
+    }
+}
+
+__global__ __launch_bounds__(256) void wal_compact_kernel(WalArgs a) {
+    const uint32_t s = blockIdx.x, w = blockIdx.y;
+    const uint64_t q = (uint64_t)w * a.segs + s;
+    const uint32_t pre = a.fin[2 * q], cf = a.fin[2 * q + 1];
+    const uint32_t cnt = cf & 0x7FFFFFFFu;
+    if (cnt == 0) return;
+    uint64_t base, cap;
+    wal_slots(a, w, base, cap);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(a.out.desc);
+    const u32x4 *src = a.scratch + (q * 2 + (cf >> 31)) * kWalSegSlots;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
+        if ((uint64_t)pre + j < cap) dst[base + pre + j] = src[j];
+}
+
 }  // namespace
 }  // namespace lsm
 
@@ -2091,6 +2349,43 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
     }
 }
 
+
+extern "C" size_t lsm_wal_replay_workspace_bytes(uint32_t nwal, uint32_t max_wal_len) {
+    const uint64_t segs = max_wal_len ? ((uint64_t)max_wal_len + kWalSeg - 1) / kWalSeg : 1;
+    const uint64_t n = (uint64_t)nwal * segs;
+    return (size_t)(n * (2 * sizeof(WalSeg) + 8 + 2ull * kWalSegSlots * 16) + 64);
+}
+
+extern "C" int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t *d_wal_off,
+                              const uint32_t *d_wal_len, uint32_t nwal, uint32_t max_wal_len,
+                              const lsm_decode_out *out, void *d_workspace, size_t ws_bytes,
+                              void *stream) {
+    if (!ctx || !out) return LSM_EINVAL;
+    if (nwal == 0) return 0;
+    if (!d_wal || !d_wal_off || !d_wal_len || !out->desc || !out->nrec || !out->status ||
+        !d_workspace || out->key_arena || out->val_arena || nwal > 65535)
+        return LSM_EINVAL;
+    if (ws_bytes < lsm_wal_replay_workspace_bytes(nwal, max_wal_len)) return LSM_ESPACE;
+    WalArgs a;
+    a.wal = d_wal;
+    a.wal_off = d_wal_off;
+    a.wal_len = d_wal_len;
+    a.nwal = nwal;
+    a.max_len = max_wal_len;
+    a.segs = max_wal_len ? (max_wal_len + kWalSeg - 1) / kWalSeg : 1;
+    a.out = *out;
+    const uint64_t n = (uint64_t)nwal * a.segs;
+    uint8_t *ws = static_cast<uint8_t *>(d_workspace);
+    a.scratch = reinterpret_cast<u32x4 *>(ws);  // 16-byte aligned first
+    a.seg = reinterpret_cast<WalSeg *>(ws + n * 2 * kWalSegSlots * 16);
+    a.fin = reinterpret_cast<uint32_t *>(ws + n * 2 * (kWalSegSlots * 16 + sizeof(WalSeg)));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(wal_seg_kernel, dim3(2 * a.segs, nwal), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(wal_stitch_kernel, dim3(nwal), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(wal_compact_kernel, dim3(a.segs, nwal), dim3(256), 0, s, a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
 
 extern "C" size_t lsm_decode_sst_workspace_bytes(uint32_t nfile) {
     return (size_t)nfile * (sizeof(SstWork) + 8) + 16;

@@ -1060,6 +1060,129 @@ __global__ __launch_bounds__(256) void bloom_probe_kernel(const uint64_t *words,
     hit[i] = ok;
 }
 
+// ---- batched SSTable.MayContain ------------------------
+//
+// d_hit[i * nfile + f] = SSTable.MayContain(key i) on file f (sstable.go:300-
+// 305): the key range check against the header's min / max key in Go string
+// order, then Filter.Test (bloom.go:371-379) on the filter block as stored in
+// the image (u64 big-endian words, bitset v1.22.0 WriteTo; bit p -> word p>>6
+// bit p&63; bitset.Test is false past its length).  One thread per key
+// hashes it once (sum256) and walks the files; the files' key bounds are
+// staged in LDS as big-endian words (prefix compares in integer registers),
+// 256 files per pass.
+constexpr uint32_t kMcTile = 256;
+
+struct McFile {
+    uint32_t lo[4], hi[4];  // first 16 bytes of min / max key, big-endian, zero padded
+    uint32_t lo_len, hi_len;
+    uint32_t ok;            // header and filter decoded (lsm_sst_meta.stage not 1 or 2)
+    uint32_t pad;
+};
+
+__device__ __forceinline__ uint32_t be_word_at(const uint8_t *p, uint64_t len, uint32_t j) {
+    uint32_t w = 0;
+    for (uint32_t b = 0; b < 4; b++) {
+        const uint64_t at = 4ull * j + b;
+        w = (w << 8) | (at < len ? p[at] : 0u);
+    }
+    return w;
+}
+
+// Go string comparison of a and b (bytewise, then length): <0, 0, >0.
+__device__ __forceinline__ int go_cmp(const uint8_t *a, uint64_t la, const uint8_t *b,
+                                      uint64_t lb) {
+    const uint64_t n = la < lb ? la : lb;
+    for (uint64_t i = 0; i < n; i++)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
+
+// Compare the 16-byte big-endian prefixes, then (when both go on) the bytes.
+__device__ __forceinline__ int bound_cmp(const uint32_t bw[4], uint64_t blen, const uint8_t *bp,
+                                         const uint32_t kw[4], uint64_t klen, const uint8_t *kp) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (bw[j] != kw[j]) return bw[j] < kw[j] ? -1 : 1;
+    // equal over min(16, len) bytes with zero padding: decide by the rest
+    if (blen <= 16 || klen <= 16) {
+        // zero padding hides a real 0x00 byte only when one side ends first
+        return go_cmp(bp, blen, kp, klen);
+    }
+    return go_cmp(bp + 16, blen - 16, kp + 16, klen - 16);
+}
+
+__global__ __launch_bounds__(256) void may_contain_kernel(const uint8_t *img,
+                                                          const uint64_t *file_off,
+                                                          const lsm_sst_meta *meta,
+                                                          uint32_t nfile, const uint8_t *keys,
+                                                          const uint64_t *koff, uint64_t nkeys,
+                                                          uint8_t *hit) {
+    __shared__ McFile tile[kMcTile];
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = i < nkeys;
+    uint64_t k0 = 0, kl = 0;
+    uint64_t h[4] = {0, 0, 0, 0};
+    uint32_t kw[4] = {0, 0, 0, 0};
+    if (act) {
+        k0 = koff[i];
+        kl = koff[i + 1] - k0;
+        sum256(keys + k0, kl, h);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) kw[j] = be_word_at(keys + k0, kl, j);
+    }
+    const uint8_t *kp = keys + k0;
+    for (uint32_t f0 = 0; f0 < nfile; f0 += kMcTile) {
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < kMcTile && f0 + t < nfile; t += blockDim.x) {
+            const lsm_sst_meta &M = meta[f0 + t];
+            const uint8_t *base = img + file_off[f0 + t];
+            McFile F;
+            F.ok = M.stage != 1 && M.stage != 2;
+            F.lo_len = (uint32_t)M.min_key_len;
+            F.hi_len = (uint32_t)M.max_key_len;
+            for (uint32_t j = 0; j < 4; j++) {
+                F.lo[j] = F.ok ? be_word_at(base + M.min_key_off, M.min_key_len, j) : 0;
+                F.hi[j] = F.ok ? be_word_at(base + M.max_key_off, M.max_key_len, j) : 0;
+            }
+            F.pad = 0;
+            tile[t] = F;
+        }
+        __syncthreads();
+        if (!act) continue;
+        const uint32_t nt = nfile - f0 < kMcTile ? nfile - f0 : kMcTile;
+        for (uint32_t t = 0; t < nt; t++) {
+            const McFile &F = tile[t];
+            uint8_t r = 0;
+            if (F.ok) {
+                const lsm_sst_meta &M = meta[f0 + t];
+                const uint8_t *base = img + file_off[f0 + t];
+                // sstable.go:301: MinKey > key || MaxKey < key -> false
+                if (bound_cmp(F.lo, F.lo_len, base + M.min_key_off, kw, kl, kp) <= 0 &&
+                    bound_cmp(F.hi, F.hi_len, base + M.max_key_off, kw, kl, kp) >= 0) {
+                    const uint64_t m = M.filter_m;
+                    // k from the file (no max(1, k) on a decoded filter); a
+                    // corrupted k is capped so a probe always ends
+                    const uint64_t k = M.filter_k < 4096 ? M.filter_k : 4096;
+                    r = m != 0;  // m == 0: Go's location() divides by zero
+                    const uint64_t mr = m ? ~0ull / m : 0;
+                    for (uint64_t j = 0; j < k && r; j++) {
+                        const uint64_t x = location(h[0], h[1], h[2], h[3], (uint32_t)j);
+                        const uint64_t p = m < (1ull << 63) ? mod_barrett(x, m, mr) : x % m;
+                        if (p >= M.filter_nbits) {
+                            r = 0;
+                        } else {
+                            const uint8_t byte =
+                                base[M.filter_words_off + 8 * (p >> 6) + 7 - ((p & 63) >> 3)];
+                            r = (byte >> (p & 7)) & 1;
+                        }
+                    }
+                }
+            }
+            hit[i * nfile + f0 + t] = r;
+        }
+    }
+}
+
 template <int G>
 int launch_encode_blocks(const EncodeBlocksArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(encode_blocks_kernel<G>, dim3(a.nblk), dim3(kWave * kEncWaves), 0, s, a);
@@ -1308,6 +1431,22 @@ extern "C" int lsm_bloom_probe(lsm_ctx *ctx, const uint64_t *d_words, uint64_t m
     hipLaunchKernelGGL(bloom_probe_kernel, dim3(grid), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_words, m, barrett_recip(m), k ? k : 1,
                        d_keys, d_koff, nkeys, d_hit);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                               const lsm_sst_meta *d_meta, uint32_t nfile, const uint8_t *d_keys,
+                               const uint64_t *d_koff, uint64_t nkeys, uint8_t *d_hit,
+                               void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nkeys == 0 || nfile == 0) return 0;
+    if (!d_img || !d_file_off || !d_meta || !d_keys || !d_koff || !d_hit) return LSM_EINVAL;
+    const uint64_t grid = (nkeys + 255) / 256;
+    if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
+    hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_img, d_file_off, d_meta, nfile, d_keys,
+                       d_koff, nkeys, d_hit);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -10,5 +10,6 @@ from .codec import (  # noqa: F401
     alloc_dense, batch_to_device, bloom_probe, build_sst, build_sst_into, compact_into,
     decode_blocks, decode_into, encode_blocks, pad16, plan, prepare_sst, replan, segment_files,
     sum256, to_device_bytes, SST_META_DTYPE, SST_STAGE_NAMES, SstDecode, alloc_sst_decode,
-    decode_sst, decode_sst_into)
+    decode_sst, decode_sst_into, wal_replay, wal_replay_into, wal_workspace,
+    may_contain, may_contain_into)
 from . import synth  # noqa: F401

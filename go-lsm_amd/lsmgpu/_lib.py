@@ -74,11 +74,18 @@ SIGNATURES = {
     "lsm_bloom_build": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_uint64,
                                        ctypes.c_uint64, ctypes.c_uint32, c_u64p,
                                        ctypes.c_void_p]),
+    "lsm_wal_replay_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint32]),
+    "lsm_wal_replay": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u32p, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.POINTER(DecodeOut), ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_void_p]),
     "lsm_decode_sst_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32]),
     "lsm_decode_sst": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u64p, ctypes.c_uint32,
                                       c_u64p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_void_p]),
+    "lsm_may_contain": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_void_p,
+                                       ctypes.c_uint32, c_u8p, c_u64p, ctypes.c_uint64, c_u8p,
+                                       ctypes.c_void_p]),
     "lsm_dev_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_void_p)]),
     "lsm_dev_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -283,6 +283,34 @@ def compact_into(ctx: Context, grammar: int, blk_off: torch.Tensor, r: DecodeRes
         _stream_handle(stream)), "lsm_compact_records")
 
 
+def wal_workspace(ctx: Context, nwal: int, max_len: int) -> torch.Tensor:
+    n = int(ctx.lib.lsm_wal_replay_workspace_bytes(nwal, max_len))
+    return torch.empty(max(n, 16), dtype=torch.uint8, device=ctx.torch_device)
+
+
+def wal_replay_into(ctx: Context, d_wal: torch.Tensor, wal_off: torch.Tensor,
+                    wal_len: torch.Tensor, max_len: int, r: DecodeResult, ws: torch.Tensor,
+                    stream=None) -> None:
+    """lsm_wal_replay (wal.Recover, wal/wal.go:95-121) into preallocated outputs."""
+    out = _decode_out(r)
+    _lib.check(ctx.lib.lsm_wal_replay(ctx.handle, _ptr(d_wal), _ptr(wal_off), _ptr(wal_len),
+                                      int(wal_off.numel()), max_len, ctypes.byref(out), _ptr(ws),
+                                      ws.numel(), _stream_handle(stream)), "lsm_wal_replay")
+
+
+def wal_replay(ctx: Context, d_wal: torch.Tensor, wal_off: torch.Tensor, wal_len: torch.Tensor,
+               max_len: Optional[int] = None, stream=None) -> DecodeResult:
+    """Replay nwal logs; offset-addressed outputs (record slots wal_off/8..)."""
+    nwal = int(wal_off.numel())
+    if max_len is None:
+        max_len = int(wal_len.max().item()) if nwal else 0
+    r = alloc_decode_offset(ctx, GRAMMAR_KV, nwal, int(d_wal.numel()))
+    if nwal:
+        wal_replay_into(ctx, d_wal, wal_off, wal_len, max_len, r,
+                        wal_workspace(ctx, nwal, max_len), stream=stream)
+    return r
+
+
 # ---- whole .sst files (lsm_decode_sst) ----------------------------------------
 
 SST_META_DTYPE = np.dtype([
@@ -351,6 +379,24 @@ def decode_sst(ctx: Context, d_img: torch.Tensor, file_off: np.ndarray, file_len
     if r.nfile:
         decode_sst_into(ctx, d_img, r, stream=stream)
     return r
+
+
+def may_contain_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                     hit: torch.Tensor, stream=None) -> None:
+    """lsm_may_contain: SSTable.MayContain of every key of `batch` against
+    every file decoded into r; hit viewed as uint8[nkeys, nfile]."""
+    _lib.check(ctx.lib.lsm_may_contain(ctx.handle, _ptr(d_img), _ptr(r.d_file_off), _ptr(r.meta),
+                                       r.nfile, _ptr(batch.keys), _ptr(batch.koff), batch.n,
+                                       _ptr(hit), _stream_handle(stream)), "lsm_may_contain")
+
+
+def may_contain(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                stream=None) -> torch.Tensor:
+    hit = torch.zeros((max(batch.n, 1), max(r.nfile, 1)), dtype=torch.uint8,
+                      device=ctx.torch_device)
+    if batch.n and r.nfile:
+        may_contain_into(ctx, d_img, r, batch, hit, stream=stream)
+    return hit
 
 
 # ---- encode -----------------------------------------------------------------

@@ -136,3 +136,47 @@ def mixed_kv_blocks(total_bytes: int, seed: int = SEED, sizes=(4096, 16384, 6553
         nrec[b] = cnt
         g += cnt
     return buf, blk_off, blk_len, nrec
+
+
+TOMBSTONE = "～DELETED～".encode()  # kv.DeletedValue, kv/kv.go:30 (13 bytes)
+
+
+def wal_logs(nwal: int, seed: int = SEED, memtable_bytes: int = 2 * 1024 * 1024,
+             delete_every: int = 16):
+    """Write-ahead logs shaped by go-lsm's own benchmark (benchmark.go:30-43):
+    Put keys "k_<i>_<1-10 random letters>", values "v_<i>_<2-20 random
+    letters>", every delete_every-th record a Delete (the tombstone value,
+    memtable Delete -> WAL.Append).  Each log holds the records of one
+    memtable: appended until the EstimateSize sum (kv.go:118-121) reaches
+    memtable_bytes (memtable.go:119-121).  A log is KeyValuePair.EncodeTo of
+    each record (kv.go:46-74).
+
+    Returns (buf uint8, wal_off uint64[nwal], wal_len uint32[nwal], nrec[nwal])."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ", np.uint8)
+    logs, nrec = [], []
+    g = 0
+    for _ in range(nwal):
+        parts, est, cnt = [], 0, 0
+        while est < memtable_bytes:
+            k = b"k_%d_" % g + letters[rng.integers(0, 52, int(rng.integers(1, 11)))].tobytes()
+            if delete_every and g % delete_every == delete_every - 1:
+                v = TOMBSTONE
+            else:
+                v = b"v_%d_" % g + letters[rng.integers(0, 52, int(rng.integers(2, 21)))].tobytes()
+            parts.append(np.uint32(len(k)).tobytes() + k + np.uint32(len(v)).tobytes() + v)
+            est += 4 + len(k) + 4 + len(v) + 8
+            cnt += 1
+            g += 1
+        logs.append(b"".join(parts))
+        nrec.append(cnt)
+    # 16-byte aligned starts, as files read into one device buffer
+    off, pos = [], 0
+    for lg in logs:
+        off.append(pos)
+        pos += (len(lg) + 15) // 16 * 16
+    buf = np.zeros(pos, dtype=np.uint8)
+    for o, lg in zip(off, logs):
+        buf[o:o + len(lg)] = np.frombuffer(lg, np.uint8)
+    return (buf, np.array(off, dtype=np.uint64), np.array([len(x) for x in logs], dtype=np.uint32),
+            np.array(nrec, dtype=np.int64))

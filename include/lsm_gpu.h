@@ -157,6 +157,25 @@ int lsm_compact_records(lsm_ctx *ctx, int grammar, const uint64_t *d_blk_off, ui
                         const lsm_decode_out *out, lsm_rec_desc *d_dense, int64_t *d_dense_idx,
                         uint64_t *d_dense_base, void *d_workspace, size_t ws_bytes, void *stream);
 
+/* ---- WAL replay ------------------------------------------------------------ */
+
+/* wal.Recover (wal/wal.go:95-121) of nwal write-ahead logs, each read whole
+ * into device memory (io.ReadAll, :101) at [wal_off[w], wal_off[w]+wal_len[w]):
+ * KeyValuePair.DecodeFrom (kv/kv.go:77-115) looped while bytes remain
+ * (:107-118).  The records decoded before an error are delivered (Recover has
+ * already called back for them, :117) and status[w] names the error, which
+ * Recover returns as "failed to read wal <file>: <err>".  Outputs and
+ * placement as lsm_decode_blocks with LSM_GRAMMAR_KV, one block per log
+ * (descriptors only; no arenas).  A log is decoded by many waves (16 KiB
+ * segments, guessed entry points, an exact stitch), so the records are the
+ * serial chase's.  max_wal_len >= every wal_len[w] sizes the grid and the
+ * workspace (a longer log is chased by one wave); workspace:
+ * lsm_wal_replay_workspace_bytes(nwal, max_wal_len). */
+size_t lsm_wal_replay_workspace_bytes(uint32_t nwal, uint32_t max_wal_len);
+int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t *d_wal_off,
+                   const uint32_t *d_wal_len, uint32_t nwal, uint32_t max_wal_len,
+                   const lsm_decode_out *out, void *d_workspace, size_t ws_bytes, void *stream);
+
 /* ---- whole .sst files ------------------------------------------------------ */
 
 /* Per-file result of lsm_decode_sst.  Offsets are relative to the file image. */
@@ -201,6 +220,18 @@ int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_of
                    const uint64_t *d_file_len, uint32_t nfile, const uint64_t *d_rec_base,
                    lsm_sst_meta *d_meta, lsm_rec_desc *d_idx_desc, int64_t *d_idx_value,
                    lsm_rec_desc *d_data_desc, void *d_workspace, size_t ws_bytes, void *stream);
+
+/* Batched SSTable.MayContain (sstable.go:300-305) of nkeys keys (CSR, as in
+ * lsm_bloom_probe) against nfile .sst images: the key range check against
+ * the header's MinKey / MaxKey in Go string order, then Filter.Test
+ * (bloom.go:371-379) on the filter block as stored in the image.  d_meta is
+ * lsm_decode_sst's output for the same images; a file whose header or filter
+ * did not decode (stage 1 or 2) reports 0.  d_hit[i * nfile + f] = 1 when
+ * key i may be in file f.  Deviations on corrupted filters only: m == 0
+ * reports 0 (Go divides by zero) and k is capped at 4096 probes. */
+int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                    const lsm_sst_meta *d_meta, uint32_t nfile, const uint8_t *d_keys,
+                    const uint64_t *d_koff, uint64_t nkeys, uint8_t *d_hit, void *stream);
 
 /* ---- encode ---------------------------------------------------------------- */
 

@@ -1,0 +1,100 @@
+"""GPU parity of lsm_may_contain (batched SSTable.MayContain, sstable.go:300-305;
+SURVEY.md §8(f) row f3) against the oracle: the range check in Go string
+order (Python bytes order is the same) and Filter.Test (bloom.go:371-379) of
+the filter block decoded by the oracle (ora_filter_decode + ora_bloom_test).
+"""
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+import lsmgpu
+import pyoracle as ora
+
+pytestmark = pytest.mark.gpu
+
+
+def csr(items):
+    data = b"".join(items)
+    off = np.zeros(len(items) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in items])
+    return np.frombuffer(data, np.uint8) if data else np.zeros(0, np.uint8), off
+
+
+def build(keys, m, k):
+    kb, ko = csr(keys)
+    vb, vo = csr([b"v" * (len(x) % 7) for x in keys])
+    img, _ = ora.build_sst(kb, ko, vb, vo, 0, len(keys), m=m, k=k)
+    return img
+
+
+def expected(img, key):
+    rc, meta, *_ = ora.sst_decode(img)
+    if meta.stage in (1, 2):
+        return 0
+    mn = img[meta.min_key_off:meta.min_key_off + meta.min_key_len].tobytes()
+    mx = img[meta.max_key_off:meta.max_key_off + meta.max_key_len].tobytes()
+    if mn > key or mx < key:
+        return 0
+    hdr = 8 + meta.min_key_len + meta.max_key_len
+    f, nbits, _ = ora.Bloom.decode(img[hdr:])
+    if meta.filter_m == 0:
+        return 0
+    if meta.filter_k == 0:
+        return 1
+    return int(f.test(key)) if nbits >= meta.filter_m else None
+
+
+def test_may_contain_vs_oracle(ctx):
+    rng = np.random.default_rng(21)
+    images, present = [], []
+    for f in range(6):  # disjoint, sorted key ranges (level >= 1 files)
+        keys = sorted({b"user%06d" % int(x) for x in rng.integers(f * 1000, f * 1000 + 1000, 300)})
+        images.append(build(keys, m=2048, k=3))  # small filter: false positives occur
+        present += keys
+    # overlapping range, variable-length keys with shared prefixes (L0-like)
+    keys = sorted({b"user%06d" % int(x) + b"x" * int(rng.integers(0, 30)) for x in rng.integers(0, 6000, 200)})
+    images.append(build(keys, m=1_600_000, k=16))
+    present += keys
+    images.append(build([], m=1024, k=2))                              # empty table
+    images.append(build([b"a"], m=64, k=0))                            # k = 0: Test is true
+    bad = build([b"q"], m=64, k=2).copy()
+    bad[:4] = np.frombuffer(struct.pack("<I", 10 ** 6), np.uint8)
+    images.append(bad)                                                 # header fails: 0
+    probes = list(present[::3])
+    probes += [b"user%06d" % int(x) for x in rng.integers(0, 7000, 600)]
+    probes += [b"", b"user", b"user000000", b"user000000\x00", b"user005999", b"zzzz", b"a", b"q",
+               b"user%06d" % 999 + b"x" * 40]
+    # images at odd offsets in one buffer
+    offs, pos, parts = [], 0, []
+    for im in images:
+        gap = int(rng.integers(0, 23))
+        parts += [np.zeros(gap, np.uint8), im]
+        pos += gap
+        offs.append(pos)
+        pos += im.size
+    buf = np.concatenate(parts)
+    d_img = lsmgpu.to_device_bytes(buf, ctx.torch_device)
+    r = lsmgpu.decode_sst(ctx, d_img, np.array(offs, np.uint64),
+                          np.array([im.size for im in images], np.uint64))
+    kb, ko = csr(probes)
+    batch = lsmgpu.batch_to_device(ctx, kb, ko, np.zeros(1, np.uint8), np.zeros(len(probes) + 1, np.uint64))
+    hit = lsmgpu.may_contain(ctx, d_img, r, batch).cpu().numpy()
+    torch.cuda.synchronize()
+    checked = 0
+    for f, im in enumerate(images):
+        for i, key in enumerate(probes):
+            want = expected(im, key)
+            if want is None:
+                continue
+            assert hit[i, f] == want, (f, key, hit[i, f], want)
+            checked += 1
+    assert checked > 0.9 * len(images) * len(probes)
+    # no false negatives for the keys each file holds
+    for f, im in enumerate(images[:7]):
+        rc, meta, idesc, _, _ = ora.sst_decode(im)
+        held = {im[d["rec_off"] + 4:d["rec_off"] + 4 + d["key_len"]].tobytes() for d in idesc}
+        for i, key in enumerate(probes):
+            if key in held:
+                assert hit[i, f] == 1
