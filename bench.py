@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
-                    choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal"])
+                    choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal",
+                             "probe"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -383,6 +384,9 @@ def main():
     elif args.config in ("sstdec", "sstdec1"):
         from bench_sstdec import bench_sst_decode  # whole-.sst decode (§8(f) f1; config 1)
         out, data = bench_sst_decode(args, world, rank, local)
+    elif args.config == "probe":
+        from bench_sstdec import bench_may_contain  # batched MayContain (§8(f) f3)
+        out, data = bench_may_contain(args, world, rank, local)
     else:
         out, data = bench_decode(args, world, rank, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -392,6 +396,9 @@ def main():
         elif args.config in ("sstdec", "sstdec1"):
             from bench_sstdec import cpu_baseline_sst_decode
             out["cpu_baseline"] = cpu_baseline_sst_decode(args, data)
+        elif args.config == "probe":
+            from bench_sstdec import cpu_baseline_may_contain
+            out["cpu_baseline"] = cpu_baseline_may_contain(args, data)
         else:
             out["cpu_baseline"] = cpu_baseline(args, data)
     if rank == 0:

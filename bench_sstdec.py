@@ -104,3 +104,95 @@ def cpu_baseline_sst_decode(args, data):
         f = (f + 1) % len(file_off)
     return {"value": round(parsed / t / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{done} image decodes by the C restatement in {t:.1f} s (1 thread)"}
+
+
+def bench_may_contain(args, world, rank, local):
+    """batched SSTable.MayContain -- 1M probe keys (half
+    held by the files, half not) against the 208 config-3 images."""
+    from bench import barrier, max_over_ranks, sum_over_ranks
+    ctx = lsmgpu.Context(local)
+    n = (args.blocks or 100_000) * 33
+    keys, koff, vals, voff = synth.kv_stream(n, first=rank * n)
+    batch = lsmgpu.batch_to_device(ctx, keys, koff, vals, voff)
+    starts = lsmgpu.segment_files(ctx, koff, voff, lsmgpu.MAX_SSTABLE_SIZE)
+    sb = lsmgpu.build_sst(ctx, batch, starts)
+    r = lsmgpu.decode_sst(ctx, sb.out, sb.file_off, sb.file_size)
+    torch.cuda.synchronize()
+    del batch
+    nf = len(starts) - 1
+    nprobe = 1 << 20
+    rng = np.random.default_rng(synth.SEED + rank)
+    held = rng.integers(rank * n, rank * n + n, nprobe // 2)
+    absent = rng.integers(10 ** 12, 10 ** 13, nprobe - nprobe // 2)  # outside every range
+    ids = rng.permutation(np.concatenate([held, absent]))
+    pk = synth.keys_for(ids).reshape(-1)
+    pko = np.arange(nprobe + 1, dtype=np.uint64) * np.uint64(synth.KEY_LEN)
+    probes = lsmgpu.batch_to_device(ctx, pk, pko, np.zeros(1, np.uint8),
+                                    np.zeros(nprobe + 1, np.uint64))
+    hit = torch.zeros((nprobe, nf), dtype=torch.uint8, device=ctx.torch_device)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        lsmgpu.may_contain_into(ctx, sb.out, r, probes, hit, stream=stream)
+    torch.cuda.synchronize()
+    rows = hit.sum(dim=1).cpu().numpy()
+    is_held = ids < 10 ** 12
+    assert (rows[is_held] >= 1).all(), "false negative"
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        lsmgpu.may_contain_into(ctx, sb.out, r, probes, hit, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(world, time.perf_counter() - t0)
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    total = sum_over_ranks(world, float(nprobe))
+    out = {
+        "metric": "M keys/s probed by SSTable.MayContain against every file",
+        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "unit": "M keys/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: the 208 config-3 images; probes half held, half outside every range",
+        "config": {"workload": f"{nprobe} keys x {nf} .sst files per GPU (range check + bloom "
+                               f"m=1.6M k=16)", "files_per_gpu": nf, "probes_per_gpu": nprobe,
+                   "false_positive_rate_absent": float(rows[~is_held].astype(bool).mean()),
+                   "parallelism": f"dp{world} (probe batches per rank, no collective)"},
+        "roofline": {"bound": "valu (sum256 + per-file range compares)", "kernel": "may_contain_kernel",
+                     "kernel_ms": round(kern_ms, 5), "achieved": None, "peak": None,
+                     "unit": None, "frac": None, "traffic": None},
+    }
+    return out, (sb.out.cpu().numpy(), sb.file_off, r.meta_numpy(), pk, nprobe)
+
+
+def cpu_baseline_may_contain(args, data):
+    """The oracle on a sample of probes: for every file, the range check
+    (bytes order = Go string order) then ora_bloom_test on the filter words
+    decoded by ora_filter_decode; 1 thread (Python-driven C)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as ora
+    img, file_off, meta, pk, nprobe = data
+    files = []
+    for f, m in enumerate(meta):
+        o = int(file_off[f])
+        mn = img[o + m["min_key_off"]:o + m["min_key_off"] + m["min_key_len"]].tobytes()
+        mx = img[o + m["max_key_off"]:o + m["max_key_off"] + m["max_key_len"]].tobytes()
+        hdr = o + 8 + int(m["min_key_len"]) + int(m["max_key_len"])
+        bloom, _, _ = ora.Bloom.decode(img[hdr:hdr + 32 + 8 * ((int(m["filter_m"]) + 63) // 64)])
+        files.append((mn, mx, bloom))
+    t, done = 0.0, 0
+    while t < args.cpu_seconds and done < nprobe:
+        key = pk[16 * done:16 * done + 16].tobytes()
+        t0 = time.perf_counter()
+        for mn, mx, bloom in files:
+            if not (mn > key or mx < key):
+                bloom.test(key)
+        t += time.perf_counter() - t0
+        done += 1
+    return {"value": round(done / t / 1e6, 4), "unit": "M keys/s", "cores": 1, "kind": "port",
+            "sample": f"{done} probes x {len(files)} files in {t:.1f} s (1 thread, Python-driven)"}
