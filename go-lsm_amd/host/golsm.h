@@ -243,6 +243,14 @@ class Builder {  // builder.go:9-59
 // compaction.go:173-220); errs[i] uses the reference's error text.
 std::vector<std::vector<kv::Value>> DecodeDataBlocks(const std::vector<Bytes> &regions,
                                                      std::vector<Error> *errs);
+// Whole .sst images -> KV pairs in one launch (lsm_decode_sst): per image
+// SSTable.DecodeFrom + DecodeDataBlock + GetKeyValuePairs (sstable.go:87-128,
+// 214-268), the batch form of compaction's loadLevelData (compaction.go:
+// 173-220).  errs[i] carries the reference's error prefix for the failing
+// step ("decode Header failed", ..., "mismatched DataBlock and IndexBlock
+// entries").
+std::vector<std::vector<kv::KeyValuePair>> DecodeFiles(const std::vector<Bytes> &images,
+                                                       std::vector<Error> *errs);
 // Builder flush rule + SSTable.EncodeTo for a sorted batch in one launch:
 // threshold 0 = one file (memtable flush), kMaxSSTableSize = CompactAndMergeKVs.
 std::vector<Bytes> BuildImages(const std::vector<kv::KeyValuePair> &sorted, uint64_t threshold,

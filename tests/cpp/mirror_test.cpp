@@ -496,6 +496,67 @@ static void TestDecodeDataBlocksVsOracle() {  // batch decode == oracle, incl. t
     }
 }
 
+static void TestDecodeFilesVsSingleFile() {  // lsm_decode_sst batch == per-file DecodeFrom path
+    std::mt19937_64 rng(29);
+    auto recs = random_sorted(rng, 3000, 400);
+    std::vector<Bytes> images = sstable::BuildImages(recs, 64 * 1024, 8192, 4);
+    const size_t good = images.size();
+    // corrupted variants: truncations and footer fields
+    for (size_t i = 0; i < good && i < 6; i++) {
+        Bytes t = images[i];
+        t.resize(t.size() - 1 - rng() % 200);
+        images.push_back(t);
+        Bytes u = images[i];
+        const size_t at = u.size() - 32 + 8 * (rng() % 4);
+        u[at + (rng() % 3)] ^= (uint8_t)(1 + rng() % 255);
+        images.push_back(u);
+    }
+    std::vector<Error> errs;
+    auto batch = sstable::DecodeFiles(images, &errs);
+    CHECK(batch.size() == images.size());
+    for (size_t f = 0; f < images.size(); f++) {
+        sstable::SSTable t;
+        Error e = t.DecodeImage(images[f]);
+        std::vector<kv::KeyValuePair> pairs;
+        if (!e) {
+            e = t.DecodeDataBlock(images[f]);
+            if (!e) pairs = t.GetKeyValuePairs(&e);
+        }
+        CHECK((bool)e == (bool)errs[f]);
+        if (e && errs[f]) {
+            const std::string &a = e.Message(), &b = errs[f].Message();
+            CHECK(a == b);
+            if (a != b) std::fprintf(stderr, "  single: %s\n  batch:  %s\n", a.c_str(), b.c_str());
+        }
+        // both agree with the oracle's file-level decode on whether and where it fails
+        {
+            ora_sst_meta om;
+            const size_t cap = images[f].size() / 4 + 1;
+            std::vector<ora_desc> id(cap), dd(cap);
+            std::vector<int64_t> iv(cap);
+            ora_sst_decode(images[f].data(), images[f].size(), &om, id.data(), iv.data(), cap,
+                           dd.data(), cap);
+            CHECK((om.stage != 0) == (bool)errs[f]);
+            static const char *const kStep[] = {"", "decode Header", "decode FilterBlock",
+                                                "decode Footer", "decode IndexBlock",
+                                                "decode DataBlock", "mismatched"};
+            const bool seek = (om.stage == 4 && om.idx_off < 0) || (om.stage == 5 && om.data_off < 0);
+            if (om.stage > 0 && om.stage < 7 && !seek) {
+                CHECK(errs[f].Message().rfind(kStep[om.stage], 0) == 0);
+                if (errs[f].Message().rfind(kStep[om.stage], 0) != 0)
+                    std::fprintf(stderr, "  oracle stage %d, got: %s\n", om.stage,
+                                 errs[f].Message().c_str());
+            }
+            if (om.stage == 0) CHECK(om.nidx == (om.ndata ? batch[f].size() : om.nidx));
+        }
+        bool same = batch[f].size() == pairs.size();
+        for (size_t i = 0; same && i < pairs.size(); i++)
+            same = batch[f][i].key == pairs[i].key && batch[f][i].value == pairs[i].value;
+        CHECK(same);
+        if (f < good) CHECK(!errs[f] && !batch[f].empty());
+    }
+}
+
 int main(int argc, char **argv) {
     const std::pair<const char *, std::function<void()>> tests[] = {
         {"TestDataBlock_EncodeDecode", TestDataBlock_EncodeDecode},
@@ -516,6 +577,7 @@ int main(int argc, char **argv) {
         {"TestConcurrentAccess", TestConcurrentAccess},
         {"TestBuildImagesVsOracle", TestBuildImagesVsOracle},
         {"TestDecodeDataBlocksVsOracle", TestDecodeDataBlocksVsOracle},
+        {"TestDecodeFilesVsSingleFile", TestDecodeFilesVsSingleFile},
     };
     int failed_cases = 0;
     for (auto &t : tests) {
