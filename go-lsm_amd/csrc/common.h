@@ -114,7 +114,9 @@ __device__ __forceinline__ uint64_t wave_excl_scan64(uint64_t v, uint64_t *total
 
 // Copy `len` bytes from buffer offset `src` (rsrc-relative, any alignment)
 // to global `dst` (any alignment) with the whole wave: interior dwords by
-// dword stores, the <=3 edge bytes at each end by byte stores.
+// dword stores, the <=3 edge bytes at each end by byte stores.  Requires
+// src >= 3: the first dword is read from src - (dst & 3), and a wrapped
+// offset plus the folded +4 of the next dword reads as out of range (0).
 __device__ __forceinline__ void wave_copy(rsrc_t r, uint32_t src, uint8_t *dst, uint32_t len) {
     if (len == 0) return;
     uintptr_t d0 = reinterpret_cast<uintptr_t>(dst);

@@ -2231,6 +2231,18 @@ __global__ __launch_bounds__(256) void wal_compact_kernel(WalArgs a) {
 
 using namespace lsm;
 
+namespace lsm {
+// exclusive scan of u32 values into n + 1 u64 sums (for merge.hip)
+int scan_u32_to_u64(const uint32_t *d_len, uint32_t n, uint64_t *d_out, void *ws, size_t ws_bytes,
+                    hipStream_t s) {
+    return plan_scan(3, d_len, n, d_out, ws, ws_bytes, s);
+}
+size_t scan_workspace_bytes(uint32_t n) {
+    const size_t ntiles = (n + kScanTile - 1) / kScanTile;
+    return (ntiles ? ntiles : 1) * 8;
+}
+}  // namespace lsm
+
 extern "C" uint64_t lsm_max_records(int grammar, uint64_t len) {
     switch (grammar) {
     case LSM_GRAMMAR_V: return len / 4;

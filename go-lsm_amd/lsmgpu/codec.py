@@ -551,3 +551,114 @@ def bloom_probe(ctx: Context, words: torch.Tensor, m: int, k: int, batch: Record
                                        _ptr(batch.koff), batch.n, _ptr(hit),
                                        _stream_handle(stream)), "lsm_bloom_probe")
     return hit
+
+
+# ---- compaction merge ------------------------------------
+
+TOMBSTONE = "～DELETED～".encode()  # kv.DeletedValue (kv/kv.go:29)
+
+
+@dataclass
+class Merge:
+    """lsm_merge_kvs outputs: out[:nout] = input indices of the written pairs,
+    file_start[:nfiles + 1] = each file's first position in out."""
+    out: torch.Tensor         # int32[n] (u32 indices)
+    file_start: torch.Tensor  # int64[n + 1]
+    workspace: torch.Tensor
+    n: int
+    nout: int = 0
+    nfiles: int = 0
+
+
+def alloc_merge(ctx: Context, n: int) -> Merge:
+    dev = ctx.torch_device
+    ws = int(ctx.lib.lsm_merge_kvs_workspace_bytes(n))
+    return Merge(out=torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
+                 file_start=torch.zeros(n + 1, dtype=torch.int64, device=dev),
+                 workspace=torch.empty(ws, dtype=torch.uint8, device=dev), n=n)
+
+
+def merge_kvs_into(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
+                   val_desc: Optional[torch.Tensor], r: Merge, level: int = 1,
+                   threshold: int = MAX_SSTABLE_SIZE, stream=None) -> Merge:
+    """CompactAndMergeKVs (merge.go:42-94) over pairs given as descriptors
+    (key: IDX/KV descriptor, value: V descriptor or None for KV records)."""
+    counts = np.zeros(2, np.uint64)
+    _lib.check(ctx.lib.lsm_merge_kvs(
+        ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), r.n, level, threshold,
+        _ptr(r.out), _ptr(r.file_start), counts.ctypes.data, _ptr(r.workspace),
+        r.workspace.numel(), _stream_handle(stream)), "lsm_merge_kvs")
+    r.nout, r.nfiles = int(counts[0]), int(counts[1])
+    return r
+
+
+def merge_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
+              val_desc: Optional[torch.Tensor], level: int = 1,
+              threshold: int = MAX_SSTABLE_SIZE, stream=None) -> Merge:
+    r = alloc_merge(ctx, int(key_desc.shape[0]))
+    return merge_kvs_into(ctx, d_bytes, key_desc, val_desc, r, level, threshold, stream)
+
+
+def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
+               val_desc: Optional[torch.Tensor], idx: torch.Tensor, nout: int,
+               key_bytes: int, val_bytes: int, stream=None) -> RecordBatch:
+    """The selected pairs as a device CSR batch (lsm_build_sst's input);
+    key_bytes / val_bytes bound the selected bytes.  koff_host / voff_host
+    are left None (use sst_layout for the image sizes)."""
+    dev = ctx.torch_device
+    keys = torch.zeros(pad16(max(key_bytes, 1)), dtype=torch.uint8, device=dev)
+    vals = torch.zeros(pad16(max(val_bytes, 1)), dtype=torch.uint8, device=dev)
+    koff = torch.zeros(nout + 1, dtype=torch.int64, device=dev)
+    voff = torch.zeros(nout + 1, dtype=torch.int64, device=dev)
+    ws = torch.empty(int(ctx.lib.lsm_gather_kvs_workspace_bytes(nout)), dtype=torch.uint8,
+                     device=dev)
+    _lib.check(ctx.lib.lsm_gather_kvs(
+        ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), _ptr(idx), nout, _ptr(keys),
+        _ptr(koff), _ptr(vals), _ptr(voff), _ptr(ws), ws.numel(), _stream_handle(stream)),
+        "lsm_gather_kvs")
+    return RecordBatch(keys=keys, koff=koff, vals=vals, voff=voff, n=nout, koff_host=None,
+                       voff_host=None)
+
+
+def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Tensor, nfile: int,
+                       m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K,
+                       align: int = 16) -> "SstBuild":
+    """prepare_sst for a device-resident batch: image sizes by
+    lsm_sst_image_sizes, then the layout from nfile + 1 small values."""
+    dev = ctx.torch_device
+    d_size = torch.zeros(max(nfile, 1), dtype=torch.int64, device=dev)
+    _lib.check(ctx.lib.lsm_sst_image_sizes(
+        ctx.handle, _ptr(batch.koff), _ptr(batch.voff), _ptr(d_file_start), nfile, m,
+        _ptr(d_size), _stream_handle(None)), "lsm_sst_image_sizes")
+    sizes = d_size[:nfile].cpu().numpy().view(np.uint64)
+    file_start = d_file_start[:nfile + 1].cpu().numpy().view(np.uint64).copy()
+    padded = (sizes + (align - 1)) // align * align
+    file_off = np.zeros(nfile, dtype=np.uint64)
+    if nfile:
+        file_off[1:] = np.cumsum(padded)[:-1]
+    total = int(padded.sum())
+    max_recs = int(np.diff(file_start.astype(np.int64)).max()) if nfile else 0
+    ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nfile, max_recs, m, k))
+    return SstBuild(
+        out=torch.zeros(pad16(total), dtype=torch.uint8, device=dev),
+        file_start=file_start, file_off=file_off, file_size=sizes.copy(),
+        footer=torch.zeros(max(nfile, 1) * 4, dtype=torch.int64, device=dev),
+        workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
+        d_file_start=d_file_start[:nfile + 1].contiguous(),
+        d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
+        max_recs=max_recs, m=m, k=k)
+
+
+def sst_pairs(r: "SstDecode") -> tuple:
+    """Dense (key descriptors, value descriptors) of every file's pairs in
+    file order -- the positional join of GetKeyValuePairs (sstable.go:248-268),
+    i.e. loadLevelData's allPairs (compaction.go:173-193), as device index
+    gathers.  Files that failed or hold no pairs contribute nothing."""
+    meta = r.meta_numpy()
+    base = r.bases().astype(np.int64)
+    parts = [np.arange(b, b + int(mt["nidx"]), dtype=np.int64)
+             for b, mt in zip(base, meta)
+             if mt["stage"] == 0 and mt["nidx"] and mt["ndata"]]
+    sel = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+    d_sel = torch.from_numpy(sel).to(r.idx_desc.device)
+    return r.idx_desc.index_select(0, d_sel), r.data_desc.index_select(0, d_sel)

@@ -303,6 +303,52 @@ int lsm_bloom_probe(lsm_ctx *ctx, const uint64_t *d_words, uint64_t m, uint32_t 
 int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
                uint64_t *d_h, void *stream);
 
+/* ---- compaction merge ------------------------------- */
+
+/* Replaces CompactAndMergeKVs (sstable/merge.go:42-94) up to the builder:
+ * the n pairs are views into d_bytes -- key i at d_key_desc[i].rec_off + 4,
+ * d_key_desc[i].key_len bytes (an IDX or KV descriptor); value i at
+ * d_val_desc[i].rec_off + 4, d_val_desc[i].val_len bytes (a V descriptor) or,
+ * with d_val_desc == NULL, right after the key of a KV descriptor
+ * (d_key_desc[i].val_len bytes).  That is the output of lsm_decode_sst (f1)
+ * or of a KV decode / WAL replay, with no copy.
+ *
+ * Pairs leave in key order (Go string order, bytewise); equal keys leave in
+ * input order -- merge.go:41's contract, "the newest pair comes first and
+ * wins" (container/heap's own tie order is unspecified).  Per
+ * pair, as merge.go:57-85: a key equal to the last written non-empty key is
+ * skipped; a tombstone (kv.DeletedValue) is dropped when level >= 6
+ * (maxSSTableLevel); otherwise it is written; a file is flushed when the
+ * EstimateSize sum (16 + key + value bytes, kv.go:118-121) reaches
+ * threshold (maxSSTableSize, 2 MiB; must be > 0) and the last written key is
+ * forgotten at each flush.
+ *
+ * Outputs: d_out[0 .. nout) = input indices of the written pairs, in order;
+ * d_file_start[0 .. nfiles] = each file's first position in d_out (optional,
+ * n + 1 entries), d_file_start[nfiles] = nout; h_counts (host) = {nout, nfiles}.
+ * Synchronizes the stream (the radix passes are chosen from key statistics). */
+size_t lsm_merge_kvs_workspace_bytes(uint64_t n);
+int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                  const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
+                  uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts, void *d_ws,
+                  size_t ws_bytes, void *stream);
+
+/* The selected pairs d_idx[0 .. nout) as a CSR record batch -- the input of
+ * lsm_build_sst: keys packed into d_keys with d_koff[0 .. nout], values into
+ * d_vals with d_voff[0 .. nout] (the arenas must hold the selected bytes; the
+ * input's totals always suffice).  Asynchronous. */
+size_t lsm_gather_kvs_workspace_bytes(uint64_t nout);
+int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                   const lsm_rec_desc *d_val_desc, const uint32_t *d_idx, uint64_t nout,
+                   uint8_t *d_keys, uint64_t *d_koff, uint8_t *d_vals, uint64_t *d_voff,
+                   void *d_ws, size_t ws_bytes, void *stream);
+
+/* .sst image size of each file f = records [d_file_start[f], d_file_start[f+1])
+ * of a device CSR batch (as lsm_sst_image_size_host, sstable.go:131-193). */
+int lsm_sst_image_sizes(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff,
+                        const uint64_t *d_file_start, uint32_t nfile, uint64_t m,
+                        uint64_t *d_size, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

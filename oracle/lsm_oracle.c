@@ -502,3 +502,105 @@ uint64_t ora_bench_decode_golike(int grammar, const uint8_t *base, const uint64_
     free(jobs); free(tids);
     return recs;
 }
+
+/* ---- compaction merge: CompactAndMergeKVs (sstable/merge.go:42-94) ------ */
+
+typedef struct {
+    const uint8_t *bytes;
+    const uint64_t *koff;
+    const uint32_t *klen;
+} merge_keys;
+
+/* Go string comparison a < b: bytewise, a proper prefix sorts first. */
+static int key_cmp(const merge_keys *m, uint32_t a, uint32_t b) {
+    const uint32_t la = m->klen[a], lb = m->klen[b];
+    const int c = memcmp(m->bytes + m->koff[a], m->bytes + m->koff[b], la < lb ? la : lb);
+    if (c) return c;
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
+
+/* stable merge sort of indices by key (ties keep input order) */
+static void merge_sort_idx(const merge_keys *m, uint32_t *a, uint32_t *tmp, uint64_t n) {
+    if (n < 2) return;
+    const uint64_t h = n / 2;
+    merge_sort_idx(m, a, tmp, h);
+    merge_sort_idx(m, a + h, tmp, n - h);
+    uint64_t i = 0, j = h, k = 0;
+    while (i < h && j < n) tmp[k++] = key_cmp(m, a[j], a[i]) < 0 ? a[j++] : a[i++];
+    while (i < h) tmp[k++] = a[i++];
+    while (j < n) tmp[k++] = a[j++];
+    memcpy(a, tmp, n * sizeof(uint32_t));
+}
+
+/* container/heap (Go standard library, heap.go): up / down with Less = key < */
+static void goheap_up(const merge_keys *m, uint32_t *h, uint64_t j) {
+    while (j > 0) {
+        const uint64_t i = (j - 1) / 2;
+        if (!(key_cmp(m, h[j], h[i]) < 0)) break;
+        const uint32_t t = h[i]; h[i] = h[j]; h[j] = t;
+        j = i;
+    }
+}
+
+static void goheap_down(const merge_keys *m, uint32_t *h, uint64_t i, uint64_t n) {
+    for (;;) {
+        const uint64_t j1 = 2 * i + 1;
+        if (j1 >= n) break;
+        uint64_t j = j1;
+        if (j1 + 1 < n && key_cmp(m, h[j1 + 1], h[j1]) < 0) j = j1 + 1;
+        if (!(key_cmp(m, h[j], h[i]) < 0)) break;
+        const uint32_t t = h[i]; h[i] = h[j]; h[j] = t;
+        i = j;
+    }
+}
+
+static const uint8_t kTombstone[13] = {0xEF, 0xBD, 0x9E, 'D', 'E', 'L', 'E', 'T',
+                                       'E', 'D', 0xEF, 0xBD, 0x9E}; /* kv.go:29 "～DELETED～" */
+
+uint64_t ora_merge_kvs(const uint8_t *bytes, const uint64_t *koff, const uint32_t *klen,
+                       const uint64_t *voff, const uint32_t *vlen, uint64_t n, int level,
+                       uint64_t threshold, int tie, uint32_t *out, uint64_t *starts,
+                       uint64_t *nfiles) {
+    merge_keys m = {bytes, koff, klen};
+    uint32_t *order = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    uint32_t *tmp = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    if (tie == ORA_TIE_GOHEAP) {
+        /* heap.Push each pair (merge.go:47-49), then heap.Pop until empty */
+        for (uint64_t i = 0; i < n; i++) {
+            tmp[i] = (uint32_t)i;
+            goheap_up(&m, tmp, i);
+        }
+        for (uint64_t r = n; r > 0; r--) {
+            const uint32_t t = tmp[0]; tmp[0] = tmp[r - 1]; tmp[r - 1] = t;
+            goheap_down(&m, tmp, 0, r - 1);
+            order[n - r] = tmp[r - 1];
+        }
+    } else {
+        for (uint64_t i = 0; i < n; i++) order[i] = (uint32_t)i;
+        merge_sort_idx(&m, order, tmp, n);
+    }
+    /* the loop of merge.go:57-91 over the pop order */
+    uint64_t cnt = 0, nf = 0, size = 0;
+    int64_t last = -1; /* lastWrittenKey: index of its pair, -1 = "" */
+    starts[0] = 0;
+    for (uint64_t t = 0; t < n; t++) {
+        const uint32_t p = order[t];
+        if (last >= 0 && klen[last] > 0 && key_cmp(&m, p, (uint32_t)last) == 0) continue;
+        const int deleted = vlen[p] == 13 && memcmp(bytes + voff[p], kTombstone, 13) == 0;
+        if (!deleted || level < 6) {
+            out[cnt++] = p;
+            size += 4 + (uint64_t)klen[p] + 4 + (uint64_t)vlen[p] + 8; /* kv.go:118-121 */
+            last = p;
+        }
+        if (size >= threshold) { /* ShouldFlush, builder.go:40-42 */
+            starts[++nf] = cnt;
+            size = 0;
+            last = -1;
+        }
+    }
+    if (size > 0) starts[++nf] = cnt; /* merge.go:88-91 */
+    *nfiles = nf;
+    free(order);
+    free(tmp);
+    return cnt;
+}

@@ -150,6 +150,26 @@ typedef struct {
 int ora_sst_decode(const uint8_t *file, uint64_t n, ora_sst_meta *meta, ora_desc *idx_desc,
                    int64_t *idx_val, uint64_t idx_cap, ora_desc *data_desc, uint64_t data_cap);
 
+/* ---- compaction merge ----------------------------- */
+
+enum { ORA_TIE_INPUT = 0, ORA_TIE_GOHEAP = 1 };
+
+/* CompactAndMergeKVs (sstable/merge.go:42-94) over n pairs held as views into
+ * `bytes`: key i = bytes[koff[i], +klen[i]), value i = bytes[voff[i], +vlen[i]).
+ * Pairs are popped in key order (Go string order = bytewise); equal keys
+ * leave in input order (tie = ORA_TIE_INPUT, merge.go:41's stated contract)
+ * or in container/heap's own order (ORA_TIE_GOHEAP: Push = append + up,
+ * Pop = Swap(0, n-1) + down, Less = key <).  The loop is the reference's:
+ * skip a key equal to the last written one (non-empty), drop tombstones when
+ * level >= maxSSTableLevel (6), flush at size >= threshold (EstimateSize sums,
+ * builder.go:34-42), and forget the last written key at each flush.
+ * Writes the written pairs' input indices to out[] (returned count) and the
+ * files' first positions in out[] to starts[0..*nfiles]; starts[*nfiles] = count. */
+uint64_t ora_merge_kvs(const uint8_t *bytes, const uint64_t *koff, const uint32_t *klen,
+                       const uint64_t *voff, const uint32_t *vlen, uint64_t n, int level,
+                       uint64_t threshold, int tie, uint32_t *out, uint64_t *starts,
+                       uint64_t *nfiles);
+
 /* ---- CPU baseline (Go allocation pattern) ------------------------------ */
 
 /* Decode blocks the way the Go path does: a fresh heap buffer per key and

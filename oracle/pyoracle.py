@@ -61,6 +61,8 @@ def lib():
         "ora_sst_decode": (ctypes.c_int, [vp, u64, ctypes.POINTER(SstMeta), vp, vp, u64, vp,
                                           u64]),
         "ora_bench_decode_golike": (u64, [ctypes.c_int, vp, vp, vp, u64, ctypes.c_int]),
+        "ora_merge_kvs": (u64, [vp, vp, vp, vp, vp, u64, ctypes.c_int, u64, ctypes.c_int, vp, vp,
+                                vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -244,6 +246,35 @@ def sst_decode(image):
                               _p(ddesc), cap_d)
     return rc, meta, idesc[: meta.nidx].copy(), ival[: meta.nidx].copy(), \
         ddesc[: meta.ndata].copy()
+
+
+TIE_INPUT, TIE_GOHEAP = 0, 1
+
+
+def merge_kvs(buf, koff, klen, voff, vlen, level, threshold, tie=TIE_INPUT):
+    """CompactAndMergeKVs (merge.go:42-94) over views into buf ->
+    (out: written pairs' input indices, starts: file starts in out)."""
+    buf = _bytes(buf)
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    voff = np.ascontiguousarray(voff, dtype=np.uint64)
+    klen = np.ascontiguousarray(klen, dtype=np.uint32)
+    vlen = np.ascontiguousarray(vlen, dtype=np.uint32)
+    n = klen.size
+    out = np.zeros(max(n, 1), np.uint32)
+    starts = np.zeros(n + 2, np.uint64)
+    nf = u64(0)
+    cnt = lib().ora_merge_kvs(_p(buf) if buf.size else None, _p(koff), _p(klen), _p(voff), _p(vlen),
+                              n, level, threshold, tie, _p(out), _p(starts), ctypes.byref(nf))
+    return out[:cnt].copy(), starts[:nf.value + 1].copy()
+
+
+def merge_pairs(pairs, level, threshold, tie=TIE_INPUT):
+    """merge_kvs over a list of (key bytes, value bytes) -> (out, starts)."""
+    blob, koff, klen, voff, vlen, pos = [], [], [], [], [], 0
+    for k, v in pairs:
+        koff.append(pos); klen.append(len(k)); blob.append(k); pos += len(k)
+        voff.append(pos); vlen.append(len(v)); blob.append(v); pos += len(v)
+    return merge_kvs(b"".join(blob) or b"\0", koff, klen, voff, vlen, level, threshold, tie)
 
 
 def bench_decode_golike(grammar, buf, blk_off, blk_len, threads=1):

@@ -1,0 +1,169 @@
+"""GPU parity of lsm_merge_kvs / lsm_gather_kvs (the compaction merge,
+CompactAndMergeKVs merge.go:42-94) against the oracle
+(ora_merge_kvs, ORA_TIE_INPUT: equal keys in input order, merge.go:41's
+contract -- see test_merge_oracle.py for the heap's own order).
+
+Bit-exact: the written pairs' input indices, the file starts, the gathered
+CSR batch and, end to end, the .sst images built from the merge.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import lsmgpu
+import pyoracle as ora
+
+pytestmark = pytest.mark.gpu
+
+TOMB = lsmgpu.TOMBSTONE
+MiB2 = 2 * 1024 * 1024
+
+
+def lay_out(pairs, kv_layout, rng):
+    """Pairs as descriptors over one byte buffer, stored in shuffled order.
+    kv_layout: KV records [klen][key][vlen][value] (value desc = None);
+    else keys and values apart, each after 4 bytes of padding (IDX / V
+    descriptor convention: bytes at rec_off + 4)."""
+    n = len(pairs)
+    place = list(range(n))
+    rng.shuffle(place)
+    parts, pos = [], 0
+    kpos, vpos = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    kd = np.zeros(n, lsmgpu.DESC_DTYPE)
+    vd = np.zeros(n, lsmgpu.DESC_DTYPE)
+    for i in place:
+        k, v = pairs[i]
+        gap = rng.randint(0, 3)
+        parts.append(bytes(gap))
+        pos += gap
+        if kv_layout:
+            rec = len(k).to_bytes(4, "little") + k + len(v).to_bytes(4, "little") + v
+            kd[i] = (pos, len(k), len(v))
+            kpos[i], vpos[i] = pos + 4, pos + 8 + len(k)
+            parts.append(rec)
+            pos += len(rec)
+        else:
+            kd[i] = (pos, len(k), 0)
+            kpos[i] = pos + 4
+            parts.append(b"\xAA" * 4 + k)
+            pos += 4 + len(k)
+            vd[i] = (pos, 0, len(v))
+            vpos[i] = pos + 4
+            parts.append(b"\xBB" * 4 + v)
+            pos += 4 + len(v)
+    buf = np.frombuffer(b"".join(parts) + bytes(16), np.uint8)
+    return buf, kd, (None if kv_layout else vd), kpos, vpos
+
+
+def run(ctx, pairs, level, threshold, kv_layout=False, seed=0):
+    rng = random.Random(seed)
+    buf, kd, vd, kpos, vpos = lay_out(pairs, kv_layout, rng)
+    dev = ctx.torch_device
+    d_buf = lsmgpu.to_device_bytes(buf, dev)
+    d_kd = torch.from_numpy(kd.view(np.int32).reshape(-1, 4).copy()).to(dev)
+    d_vd = None if vd is None else torch.from_numpy(vd.view(np.int32).reshape(-1, 4).copy()).to(dev)
+    r = lsmgpu.merge_kvs(ctx, d_buf, d_kd, d_vd, level=level, threshold=threshold)
+    torch.cuda.synchronize()
+    got = r.out[:r.nout].cpu().numpy().view(np.uint32)
+    starts = r.file_start[:r.nfiles + 1].cpu().numpy().view(np.uint64)
+    klen = np.array([len(k) for k, _ in pairs], np.uint32)
+    vlen = np.array([len(v) for _, v in pairs], np.uint32)
+    want, wstarts = ora.merge_kvs(buf, kpos, klen, vpos, vlen, level, threshold, ora.TIE_INPUT)
+    assert np.array_equal(got, want), (level, threshold, got[:20], want[:20])
+    assert np.array_equal(starts, wstarts), (level, threshold, starts, wstarts)
+    return r, d_buf, d_kd, d_vd, got, starts
+
+
+def random_pairs(rng, n, alphabet, maxlen, tomb=0.2, maxval=40):
+    out = []
+    for _ in range(n):
+        k = bytes(rng.choice(alphabet) for _ in range(rng.randint(0, maxlen)))
+        v = TOMB if rng.random() < tomb else bytes(rng.randint(0, 255) for _ in range(rng.randint(0, maxval)))
+        out.append((k, v))
+    return out
+
+
+def test_reference_vector(ctx):
+    pairs = [(b"alpha", b"A"), (b"beta", b"B"), (b"beta", b"B2"), (b"carrot", b"C"), (b"delta", b"D")]
+    for kv in (False, True):
+        _, _, _, _, got, starts = run(ctx, pairs, 1, MiB2, kv_layout=kv)
+        assert list(got) == [0, 1, 3, 4] and list(starts) == [0, 4]
+
+
+def test_edge_sizes(ctx):
+    run(ctx, [(b"a", b"b")], 1, MiB2)
+    run(ctx, [(b"", TOMB)], 6, MiB2)                      # nothing written: no file
+    run(ctx, [(b"", b""), (b"", b"x"), (b"", TOMB)], 6, 1)
+    r = lsmgpu.merge_kvs(ctx, torch.zeros(16, dtype=torch.uint8, device=ctx.torch_device),
+                         torch.zeros((0, 4), dtype=torch.int32, device=ctx.torch_device), None)
+    assert r.nout == 0 and r.nfiles == 0
+
+
+@pytest.mark.parametrize("level", [1, 6])
+@pytest.mark.parametrize("threshold", [1, 60, 700, MiB2])
+def test_random_duplicates_tombstones_flushes(ctx, level, threshold):
+    """Short keys over a 4-letter alphabet with zero bytes (prefix, padding
+    and "a" < "a\\0" order), many duplicates, tombstones, and thresholds
+    that flush inside duplicate groups."""
+    rng = random.Random(level * 1000 + threshold % 997)
+    pairs = random_pairs(rng, 3000, b"ab\x00\xff", 11)
+    for kv in (False, True):
+        run(ctx, pairs, level, threshold, kv_layout=kv, seed=level)
+
+
+def test_long_keys_shared_prefixes(ctx):
+    """Keys of 0..300 bytes sharing long prefixes: many 8-byte chunk passes."""
+    rng = random.Random(4)
+    stems = [bytes(rng.randint(0, 255) for _ in range(rng.randint(0, 200))) for _ in range(6)]
+    pairs = []
+    for _ in range(4000):
+        k = rng.choice(stems) + bytes(rng.choice(b"\x00\x01xy") for _ in range(rng.randint(0, 100)))
+        pairs.append((k, TOMB if rng.random() < 0.1 else b"v%d" % rng.randint(0, 99)))
+    for level, threshold in ((1, MiB2), (6, 5000), (3, 1)):
+        run(ctx, pairs, level, threshold)
+
+
+def test_compaction_shaped_runs(ctx):
+    """loadLevelData's shape (compaction.go:173-193): newest files first,
+    each sorted and unique, overlapping key ranges; 2 MiB and 64 KiB files."""
+    rng = np.random.default_rng(6)
+    pairs = []
+    for r in range(6):
+        ids = np.unique(rng.integers(0, 120_000, 40_000))
+        for i in ids:
+            v = TOMB if (i * 7 + r) % 23 == 0 else b"r%d_" % r + b"x" * int(i % 90)
+            pairs.append((b"key%012d" % i, v))
+    for level, threshold in ((1, MiB2), (6, MiB2), (2, 64 * 1024)):
+        run(ctx, pairs, level, threshold, kv_layout=(level == 2))
+
+
+def test_gather_and_build_match_oracle_images(ctx):
+    """merge -> gather -> lsm_build_sst: the .sst images equal the oracle's
+    images of the oracle's merge (sstable.go:131-193 on merge.go's output)."""
+    rng = random.Random(11)
+    pairs = random_pairs(rng, 6000, b"abcdefgh", 14, tomb=0.1, maxval=300)
+    r, d_buf, d_kd, d_vd, got, starts = run(ctx, pairs, 6, 200_000)
+    kb = sum(len(k) for k, _ in pairs)
+    vb = sum(len(v) for _, v in pairs)
+    batch = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, r.out, r.nout, kb, vb)
+    torch.cuda.synchronize()
+    keys = b"".join(pairs[i][0] for i in got)
+    vals = b"".join(pairs[i][1] for i in got)
+    koff = np.concatenate([[0], np.cumsum([len(pairs[i][0]) for i in got])]).astype(np.uint64)
+    voff = np.concatenate([[0], np.cumsum([len(pairs[i][1]) for i in got])]).astype(np.uint64)
+    assert np.array_equal(batch.koff.cpu().numpy().view(np.uint64), koff)
+    assert np.array_equal(batch.voff.cpu().numpy().view(np.uint64), voff)
+    assert batch.keys[:len(keys)].cpu().numpy().tobytes() == keys
+    assert batch.vals[:len(vals)].cpu().numpy().tobytes() == vals
+    sb = lsmgpu.prepare_sst_device(ctx, batch, r.file_start, r.nfiles, m=20_000, k=5)
+    lsmgpu.build_sst_into(ctx, batch, sb)
+    torch.cuda.synchronize()
+    img = sb.out.cpu().numpy()
+    kn, vn = np.frombuffer(keys, np.uint8), np.frombuffer(vals, np.uint8)
+    for f in range(r.nfiles):
+        want, _ = ora.build_sst(kn, koff, vn, voff, int(starts[f]), int(starts[f + 1]), m=20_000, k=5)
+        o = int(sb.file_off[f])
+        assert int(sb.file_size[f]) == want.size
+        assert np.array_equal(img[o:o + want.size], want), f
