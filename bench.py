@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
                     choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal",
-                             "probe"])
+                             "probe", "compact"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -387,6 +387,9 @@ def main():
     elif args.config == "probe":
         from bench_sstdec import bench_may_contain  # batched MayContain (§8(f) f3)
         out, data = bench_may_contain(args, world, rank, local)
+    elif args.config == "compact":
+        from bench_compact import bench_compact  # L0 -> L1 compaction (§8(f) f1 + f2)
+        out, data = bench_compact(args, world, rank, local)
     else:
         out, data = bench_decode(args, world, rank, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -399,6 +402,9 @@ def main():
         elif args.config == "probe":
             from bench_sstdec import cpu_baseline_may_contain
             out["cpu_baseline"] = cpu_baseline_may_contain(args, data)
+        elif args.config == "compact":
+            from bench_compact import cpu_baseline_compact
+            out["cpu_baseline"] = cpu_baseline_compact(args, data)
         else:
             out["cpu_baseline"] = cpu_baseline(args, data)
     if rank == 0:

@@ -15,39 +15,40 @@
 // contract: equal keys leave in input order.
 //
 // GPU shape:
-//   1. key statistics (max / min key length; per 8-byte chunk the OR and AND
-//      of every key's big-endian chunk) -> the host picks the radix passes;
+//   1. key statistics in one pass (max / min key length; per 8-byte chunk the
+//      OR and AND of every key's big-endian chunk), per-block partials reduced
+//      on the host, which picks the radix passes;
 //   2. LSD radix passes (rocPRIM onesweep, stable) on the key length, then
 //      chunk D-1 .. chunk 0 (zero padded), each over only the bits that vary:
 //      the result is Go string order with input order on full ties;
 //   3. group flags (a key differing from its predecessor starts a group; an
 //      empty key is its own group because "" is never deduplicated) and the
 //      candidate of each group: its first pair that may be written;
-//   4. scans of the candidates' sizes and counts, then one wave walks the
-//      file boundaries (a flush inside a group makes the next writable pair
-//      of that group a write of its own -- the "extra" of the next file);
+//   4. one scan of the candidates' (size, count) into interleaved sums, then
+//      one wave walks the file boundaries -- one probe round per file when it
+//      starts a group; a flush inside a group makes the next writable pair of
+//      that group a write of its own (the "extra" of the next file);
 //   5. emit: each candidate's output slot from its file's start.
 // Steps 3-5 are exact for any input; only the tie order is specified above.
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
 
 namespace lsm {
-
-int scan_u32_to_u64(const uint32_t *d_len, uint32_t n, uint64_t *d_out, void *ws, size_t ws_bytes,
-                    hipStream_t s);
-size_t scan_workspace_bytes(uint32_t n);
-
 namespace {
 
 constexpr uint32_t kMergeThreads = 256;
 constexpr uint32_t kStatBlocks = 1024;
+constexpr uint32_t kFastChunks = 4;               // chunks counted in the first pass (32 B keys)
 constexpr uint32_t kMaxChunks = kKeyCap / 8 + 1;  // 1 MiB keys
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr uint64_t kFileBytes = 16;  // MergeFile
+constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanTile = kMergeThreads * kScanPer;
 
 // Go's kv.DeletedValue, "～DELETED～" (kv/kv.go:29), 13 bytes
 __constant__ uint8_t kTomb[13] = {0xEF, 0xBD, 0x9E, 'D', 'E', 'L', 'E', 'T',
@@ -81,20 +82,22 @@ __device__ __forceinline__ View view(const MergeIn &m, uint32_t i) {
     return v;
 }
 
-__device__ __forceinline__ uint32_t key_len(const MergeIn &m, uint32_t i) {
-    return reinterpret_cast<const uint32_t *>(m.kd + i)[2];
+// Four bytes at any address from the two aligned dwords that cover them
+// (inputs are readable to the next 16-byte multiple past their last byte,
+// and keys and values sit at rec_off + 4 or later).
+__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    return funnel(q[0], q[1], (uint32_t)a);
 }
 
-// Big-endian 8-byte chunk d of the key, zero past its end.
+// Big-endian 8-byte chunk d of a key of kl bytes at p, zero past its end.
 __device__ __forceinline__ uint64_t key_chunk(const uint8_t *p, uint32_t kl, uint32_t d) {
-    uint64_t c = 0;
     const uint32_t b0 = 8 * d;
-#pragma unroll
-    for (uint32_t t = 0; t < 8; t++) {
-        const uint8_t b = b0 + t < kl ? p[b0 + t] : 0;
-        c = c << 8 | b;
-    }
-    return c;
+    if (b0 >= kl) return 0;
+    const uint64_t c = (uint64_t)bswap32(ld_u32_any(p + b0)) << 32 | bswap32(ld_u32_any(p + b0 + 4));
+    const uint32_t have = kl - b0;
+    return have >= 8 ? c : c & ~(~0ull >> (8 * have));
 }
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
@@ -105,46 +108,81 @@ __device__ __forceinline__ uint64_t wave_and64(uint64_t v) {
     for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o);
     return v;
 }
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t t = __shfl_xor(v, o);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t t = __shfl_xor(v, o);
+        v = t < v ? t : v;
+    }
+    return v;
+}
 
-// stats[0] = max key length, stats[1] = min key length (as u64 words)
-__global__ __launch_bounds__(kMergeThreads) void merge_len_kernel(MergeIn m, uint64_t *stats) {
-    uint32_t mx = 0, mn = 0xFFFFFFFFu;
+// Per-block partial statistics: [0] max key length, [1] min key length,
+// [2] OR / [3] AND of the key lengths, then for chunks d < kFastChunks the OR
+// and AND of chunk d over keys longer than 8d (shorter keys hold 0 there:
+// the host folds that in with the minimum key length).
+constexpr uint32_t kStatWords = 4 + 2 * kFastChunks;
+
+__global__ __launch_bounds__(kMergeThreads) void merge_stats_kernel(MergeIn m, uint64_t *part) {
+    __shared__ uint64_t red[kMergeThreads / kWave][kStatWords];
+    uint64_t s[kStatWords];
+    s[0] = 0; s[1] = ~0ull; s[2] = 0; s[3] = ~0ull;
+    for (uint32_t d = 0; d < kFastChunks; d++) {
+        s[4 + 2 * d] = 0;
+        s[5 + 2 * d] = ~0ull;
+    }
     for (uint32_t i = blockIdx.x * kMergeThreads + threadIdx.x; i < m.n;
          i += gridDim.x * kMergeThreads) {
-        const uint32_t kl = key_len(m, i);
-        mx = kl > mx ? kl : mx;
-        mn = kl < mn ? kl : mn;
+        const View v = view(m, i);
+        s[0] = v.kl > s[0] ? v.kl : s[0];
+        s[1] = v.kl < s[1] ? v.kl : s[1];
+        s[2] |= v.kl;
+        s[3] &= v.kl;
+#pragma unroll
+        for (uint32_t d = 0; d < kFastChunks; d++) {
+            if (v.kl > 8 * d) {
+                const uint64_t c = key_chunk(m.bytes + v.ko, v.kl, d);
+                s[4 + 2 * d] |= c;
+                s[5 + 2 * d] &= c;
+            }
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t a = __shfl_xor(mx, o), b = __shfl_xor(mn, o);
-        mx = a > mx ? a : mx;
-        mn = b < mn ? b : mn;
+    s[0] = wave_max64(s[0]);
+    s[1] = wave_min64(s[1]);
+    for (uint32_t t = 2; t < kStatWords; t += 2) {
+        s[t] = wave_or64(s[t]);
+        s[t + 1] = wave_and64(s[t + 1]);
     }
-    if (lane_id() == 0) {
-        atomicMax(reinterpret_cast<unsigned long long *>(&stats[0]), (unsigned long long)mx);
-        atomicMin(reinterpret_cast<unsigned long long *>(&stats[1]), (unsigned long long)mn);
+    const uint32_t w = threadIdx.x / kWave;
+    if (lane_id() == 0)
+        for (uint32_t t = 0; t < kStatWords; t++) red[w][t] = s[t];
+    __syncthreads();
+    if (threadIdx.x < kStatWords) {
+        const uint32_t t = threadIdx.x;
+        uint64_t r = red[0][t];
+        for (uint32_t x = 1; x < kMergeThreads / kWave; x++) {
+            const uint64_t y = red[x][t];
+            if (t == 0) r = y > r ? y : r;
+            else if (t == 1) r = y < r ? y : r;
+            else if (t & 1) r &= y;
+            else r |= y;
+        }
+        part[(uint64_t)blockIdx.x * kStatWords + t] = r;
     }
 }
 
-// chunk statistics: orand[2d] = OR, orand[2d+1] = AND of chunk d over keys
-// longer than 8d (shorter keys hold 0 there: the host folds that in with the
-// minimum key length); orand[2D], [2D+1] = OR / AND of the key lengths
-__global__ __launch_bounds__(kMergeThreads) void merge_chunk_stats_kernel(MergeIn m, uint32_t D,
-                                                                          uint64_t *orand) {
+// Long keys (chunks kFastChunks .. D-1): OR / AND by atomics on orand[2d],
+// orand[2d + 1], initialized by the host.
+__global__ __launch_bounds__(kMergeThreads) void merge_long_stats_kernel(MergeIn m, uint32_t D,
+                                                                         uint64_t *orand) {
     const uint32_t i0 = blockIdx.x * kMergeThreads + threadIdx.x, step = gridDim.x * kMergeThreads;
-    uint64_t lo = 0, la = ~0ull;
-    for (uint32_t i = i0; i < m.n; i += step) {
-        const uint32_t kl = key_len(m, i);
-        lo |= kl;
-        la &= kl;
-    }
-    lo = wave_or64(lo);
-    la = wave_and64(la);
-    if (lane_id() == 0) {
-        atomicOr(reinterpret_cast<unsigned long long *>(&orand[2 * D]), (unsigned long long)lo);
-        atomicAnd(reinterpret_cast<unsigned long long *>(&orand[2 * D + 1]), (unsigned long long)la);
-    }
-    for (uint32_t d = 0; d < D; d++) {
+    for (uint32_t d = kFastChunks; d < D; d++) {
         uint64_t o = 0, a = ~0ull;
         for (uint32_t i = i0; i < m.n; i += step) {
             const View v = view(m, i);
@@ -164,18 +202,48 @@ __global__ __launch_bounds__(kMergeThreads) void merge_chunk_stats_kernel(MergeI
     }
 }
 
-// sort key of sorted position j for pass `d` (d == kNone: the key length)
+// One radix pass sorts a 64-bit key packed from several fields (the key
+// length and 8-byte chunks), each reduced to the bits that vary across all
+// keys: bits that never vary cannot decide an order, and compressing the
+// rest keeps their order (pext), so whole keys of a few varying bytes sort
+// in one pass instead of one pass per chunk.
+constexpr uint32_t kGroupFields = 8;
+struct SortGroup {
+    uint32_t nf;
+    uint32_t field[kGroupFields];  // chunk index, or kNone for the key length; most significant first
+    uint64_t mask[kGroupFields];   // its varying bits
+};
+
+// bits of v under mask, packed toward bit 0 in order (mask is wave-uniform)
+__device__ __forceinline__ uint64_t pext64(uint64_t v, uint64_t mask) {
+    uint64_t r = 0;
+    uint32_t pos = 0;
+    while (mask) {
+        const uint32_t lo = (uint32_t)__builtin_ctzll(mask);
+        const uint64_t m = mask >> lo;
+        const uint32_t len = ~m ? (uint32_t)__builtin_ctzll(~m) : 64 - lo;
+        const uint64_t bits = len >= 64 ? v >> lo : (v >> lo) & ((1ull << len) - 1);
+        r |= bits << pos;
+        pos += len;
+        mask = len + lo >= 64 ? 0 : mask & ~(((1ull << len) - 1) << lo);
+    }
+    return r;
+}
+
+// sort key of sorted position j for one pass
 __global__ __launch_bounds__(kMergeThreads) void merge_extract_kernel(MergeIn m, const uint32_t *perm,
-                                                                      uint32_t d, uint64_t *keys) {
+                                                                      SortGroup g, uint64_t *keys) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j >= m.n) return;
     const uint32_t i = perm ? perm[j] : j;
-    if (d == kNone) {
-        keys[j] = key_len(m, i);
-    } else {
-        const View v = view(m, i);
-        keys[j] = key_chunk(m.bytes + v.ko, v.kl, d);
+    const View v = view(m, i);
+    uint64_t key = 0;
+    for (uint32_t t = 0; t < g.nf; t++) {
+        const uint64_t x = g.field[t] == kNone ? v.kl : key_chunk(m.bytes + v.ko, v.kl, g.field[t]);
+        const uint32_t bits = (uint32_t)__builtin_popcountll(g.mask[t]);
+        key = (bits >= 64 ? 0 : key << bits) | pext64(x, g.mask[t]);
     }
+    keys[j] = key;
 }
 
 __global__ __launch_bounds__(kMergeThreads) void merge_iota_kernel(uint32_t *perm, uint32_t n) {
@@ -185,18 +253,17 @@ __global__ __launch_bounds__(kMergeThreads) void merge_iota_kernel(uint32_t *per
 
 __device__ __forceinline__ bool keys_equal(const uint8_t *b, const View &x, const View &y) {
     if (x.kl != y.kl) return false;
-    const uint8_t *p = b + x.ko, *q = b + y.ko;
-    for (uint32_t t = 0; t < x.kl; t++)
-        if (p[t] != q[t]) return false;
+    for (uint32_t d = 0; 8 * d < x.kl; d++)
+        if (key_chunk(b + x.ko, x.kl, d) != key_chunk(b + y.ko, y.kl, d)) return false;
     return true;
 }
 
 __device__ __forceinline__ bool is_tombstone(const uint8_t *b, const View &v) {
     if (v.vl != 13) return false;
     const uint8_t *p = b + v.vo;
-    for (int t = 0; t < 13; t++)
-        if (p[t] != kTomb[t]) return false;
-    return true;
+    // "～DELETED～" as little-endian dwords of bytes 0-3, 4-7, 8-11, then byte 12
+    return ld_u32_any(p) == 0x449EBDEFu && ld_u32_any(p + 4) == 0x54454C45u &&
+           ld_u32_any(p + 8) == 0xBDEF4445u && p[12] == kTomb[12];
 }
 
 // flags[j]: bit 0 = starts a group, bit 1 = may be written (not a tombstone
@@ -214,12 +281,12 @@ __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, c
 
 // candidate = the first pair of its group that may be written; the backward
 // scan stops at the first writable pair or the group start, so each run of
-// dropped tombstones is scanned by one pair only (O(n) in total)
+// dropped tombstones is scanned by one pair only (O(n) in total).
+// csize[j] = EstimateSize of a candidate (kv.go:118-121, >= 16), else 0.
 __global__ __launch_bounds__(kMergeThreads) void merge_candidate_kernel(MergeIn m,
                                                                         const uint32_t *perm,
                                                                         const uint8_t *flags,
-                                                                        uint32_t *csize,
-                                                                        uint32_t *cflag) {
+                                                                        uint32_t *csize) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j >= m.n) return;
     const uint8_t f = flags[j];
@@ -234,11 +301,91 @@ __global__ __launch_bounds__(kMergeThreads) void merge_candidate_kernel(MergeIn 
     uint32_t sz = 0;
     if (c) {
         const View v = view(m, perm[j]);
-        sz = 16 + v.kl + v.vl;  // EstimateSize, kv.go:118-121
+        sz = 16 + v.kl + v.vl;
     }
     csize[j] = sz;
-    cflag[j] = c ? 1u : 0u;
 }
+
+// ---- interleaved exclusive sums of candidate sizes and counts -----------
+
+struct SumPair {
+    uint64_t s, c;  // bytes and candidates before position j
+};
+
+__device__ __forceinline__ SumPair block_excl_scan2(uint64_t s, uint64_t c, SumPair *total) {
+    __shared__ uint64_t ws_[kMergeThreads / kWave], wc_[kMergeThreads / kWave];
+    uint64_t ts, tc;
+    const uint64_t xs = wave_excl_scan64(s, &ts), xc = wave_excl_scan64(c, &tc);
+    const uint32_t w = threadIdx.x / kWave;
+    if (lane_id() == 0) {
+        ws_[w] = ts;
+        wc_[w] = tc;
+    }
+    __syncthreads();
+    uint64_t ps = 0, pc = 0, as = 0, ac = 0;
+    for (uint32_t i = 0; i < kMergeThreads / kWave; i++) {
+        if (i < w) {
+            ps += ws_[i];
+            pc += wc_[i];
+        }
+        as += ws_[i];
+        ac += wc_[i];
+    }
+    __syncthreads();
+    *total = SumPair{as, ac};
+    return SumPair{xs + ps, xc + pc};
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_scan_tiles(const uint32_t *csize, uint32_t n,
+                                                                  SumPair *part) {
+    uint64_t s = 0, c = 0;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t t = 0; t < kScanPer; t++) {
+        const uint32_t v = i0 + t < n ? csize[i0 + t] : 0;
+        s += v;
+        c += v != 0;
+    }
+    SumPair tot;
+    block_excl_scan2(s, c, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_scan_partials(SumPair *part, uint32_t ntiles,
+                                                                     SumPair *sc, uint32_t n) {
+    SumPair carry{0, 0};
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += kMergeThreads) {
+        const uint32_t t = t0 + threadIdx.x;
+        const SumPair v = t < ntiles ? part[t] : SumPair{0, 0};
+        SumPair tot;
+        const SumPair x = block_excl_scan2(v.s, v.c, &tot);
+        if (t < ntiles) part[t] = SumPair{carry.s + x.s, carry.c + x.c};
+        carry.s += tot.s;
+        carry.c += tot.c;
+    }
+    if (threadIdx.x == 0) sc[n] = carry;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_scan_apply(const uint32_t *csize, uint32_t n,
+                                                                  const SumPair *part, SumPair *sc) {
+    uint32_t v[kScanPer];
+    uint64_t s = 0, c = 0;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t t = 0; t < kScanPer; t++) {
+        v[t] = i0 + t < n ? csize[i0 + t] : 0;
+        s += v[t];
+        c += v[t] != 0;
+    }
+    SumPair tot;
+    const SumPair x = block_excl_scan2(s, c, &tot);
+    uint64_t ps = x.s + part[blockIdx.x].s, pc = x.c + part[blockIdx.x].c;
+    for (uint32_t t = 0; t < kScanPer; t++) {
+        if (i0 + t < n) sc[i0 + t] = SumPair{ps, pc};
+        ps += v[t];
+        pc += v[t] != 0;
+    }
+}
+
+// ---- the file walk --------------------------------------------------------
 
 struct MergeFile {
     uint32_t p;      // first sorted position of the file
@@ -250,39 +397,24 @@ struct WalkArgs {
     MergeIn m;
     const uint32_t *perm;
     const uint8_t *flags;
-    const uint64_t *S;  // exclusive scan of candidate sizes, n + 1
-    const uint64_t *C;  // exclusive scan of candidate flags, n + 1
+    const SumPair *sc;  // n + 1
     uint64_t threshold;
     MergeFile *files;
     uint32_t *out;
     uint64_t *counts;   // [0] = written pairs, [1] = files
 };
 
-// smallest k in [lo, hi] with S[k] >= t, given S[hi] >= t; 64 probes a round
-__device__ uint32_t wave_lower_bound(const uint64_t *S, uint32_t lo, uint32_t hi, uint64_t t,
-                                     uint32_t guess) {
+// smallest k in [lo, hi] with sc[k].s >= t, given sc[hi].s >= t
+__device__ uint32_t wave_lower_bound(const SumPair *sc, uint32_t lo, uint32_t hi, uint64_t t) {
     const uint32_t lane = lane_id();
-    if (guess >= lo && guess <= hi) {  // a window of 64 around the guess first
-        uint32_t a = guess >= lo + 32 ? guess - 32 : lo;
-        if (a + 63 > hi) a = hi >= lo + 63 ? hi - 63 : lo;
-        const uint32_t k = a + lane <= hi ? a + lane : hi;
-        const uint64_t ge = __ballot(S[k] >= t);
-        if (ge & 1) {
-            hi = a;
-        } else if (ge) {
-            return uni(a + (uint32_t)__builtin_ctzll(ge));
-        } else {
-            lo = a + 63 < hi ? a + 64 : hi;
-        }
-    }
     while (hi > lo) {
-        // lane l probes lo + l*step, the last lane probes hi (S[hi] >= t), so
-        // the first lane at or above t exists and the lane before it is below
+        // lane l probes lo + l*step, the last lane probes hi (>= t), so the
+        // first lane at or above t exists and the lane before it is below
         const uint32_t span = hi - lo;
         const uint32_t step = span >= 63 ? (span + 62) / 63 : 1;
         uint32_t k = lo + lane * step;
         if (k > hi || lane == kWave - 1) k = hi;
-        const uint64_t ge = __ballot(S[k] >= t);
+        const uint64_t ge = __ballot(sc[k].s >= t);
         const uint32_t f = (uint32_t)__builtin_ctzll(ge);
         if (f == 0) return uni(lo);
         uint32_t kf = lo + f * step;
@@ -297,20 +429,62 @@ __device__ uint32_t wave_lower_bound(const uint64_t *S, uint32_t lo, uint32_t hi
 // p; if p continues a group whose pair was written just before the flush,
 // lastWrittenKey is "" again and the group's next writable pair is written
 // (the file's "extra"); then come the candidates of later groups until the
-// size reaches the threshold.
+// size reaches the threshold.  The common case -- p starts a group and the
+// file spans about as many positions as the last one -- takes one round of
+// loads: lane 0 reads flags[p] and sc[p] while lanes 1..63 probe sc around
+// the predicted end.
 __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
     const uint32_t n = a.m.n, lane = lane_id();
-    uint32_t p = 0, nf = 0, prev_span = 0;
+    const SumPair tail = a.sc[n];
+    uint32_t p = 0, nf = 0, span = 0;
     uint64_t o = 0;
+    uint32_t fast = 0, slow = 0;
     while (p < n) {
-        uint32_t g = p, w = kNone;
-        uint64_t wsize = 0;
-        if (p > 0 && !(a.flags[p] & 1)) {
+        // speculative round: lane 0 reads flags[p] and sc[p]; every lane reads
+        // sc at four positions of the window [w0, w0 + 256) around the
+        // predicted end (all five loads in one round trip)
+        const uint32_t w0 = span > 128 ? p + span - 127 : p + 1;
+        SumPair q[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t k = w0 + lane + kWave * i;
+            q[i] = a.sc[k <= n ? k : n];
+        }
+        const SumPair q0 = a.sc[p];
+        const uint8_t fl0 = lane == 0 ? a.flags[p] : 0;
+        const bool starts = p == 0 || (__builtin_amdgcn_readfirstlane(fl0) & 1);
+        const uint64_t S0 = uni64(q0.s), C0 = uni64(q0.c);
+        uint32_t g = p, w = kNone, e = kNone;
+        uint64_t wsize = 0, Cg = C0;
+        bool done = false, have_ce = false;
+        uint64_t Ce = 0;
+        if (starts) {
+            const uint64_t t = S0 + a.threshold;
+            if (tail.s < t) {
+                done = true;  // the rest fits in this file
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) {
+                    const uint64_t ge = __ballot(q[i].s >= t);
+                    if (!ge) continue;
+                    const uint32_t f = (uint32_t)__builtin_ctzll(ge);
+                    const uint32_t k = w0 + kWave * i + f;  // first probe at or above t
+                    if (k > w0 || k == p + 1) {  // the position before k is below t
+                        e = k - 1;
+                        done = true;
+                        Ce = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(q[i].c >> 32), f) << 32 |
+                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)q[i].c, f);
+                        have_ce = true;
+                    }
+                    break;
+                }
+            }
+        } else {
             // the rest of the group: its end and its first writable pair
             for (uint32_t q0 = p;; q0 += kWave) {
-                const uint32_t q = q0 + lane;
-                const uint8_t f = q < n ? a.flags[q] : 1;
-                const bool end = q >= n || (q > p && (f & 1));
+                const uint32_t qq = q0 + lane;
+                const uint8_t f = qq < n ? a.flags[qq] : 1;
+                const bool end = qq >= n || (qq > p && (f & 1));
                 const uint64_t em = __ballot(end);
                 const uint64_t wm = __ballot(!end && (f & 2)) & (em ? (em & -em) - 1 : ~0ull);
                 if (w == kNone && wm) w = uni(q0 + (uint32_t)__builtin_ctzll(wm));
@@ -323,19 +497,21 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
                 const View v = view(a.m, a.perm[w]);
                 wsize = 16 + (uint64_t)v.kl + v.vl;
             }
-        }
-        uint32_t e = kNone;  // sorted position of the pair that triggers the flush
-        if (w != kNone && wsize >= a.threshold) {
-            e = w;
-        } else {
-            const uint64_t t = a.S[g] + (a.threshold - wsize);
-            if (a.S[n] >= t) {
-                const uint32_t k = wave_lower_bound(a.S, g + 1, n, t, g + prev_span);
-                e = k - 1;
+            Cg = g < n ? uni64(a.sc[g].c) : tail.c;
+            if (w != kNone && wsize >= a.threshold) {
+                e = w;
+                done = true;
             }
         }
+        if (done) fast++; else slow++;
+        if (!done) {
+            const uint64_t Sg = g < n ? uni64(a.sc[g].s) : tail.s;
+            const uint64_t t = Sg + (a.threshold - wsize);
+            if (tail.s >= t) e = wave_lower_bound(a.sc, g + 1, n, t) - 1;
+        }
         const uint32_t end = e == kNone ? n : e + 1;
-        const uint64_t nw = (w != kNone ? 1 : 0) + (end > g ? a.C[end] - a.C[g] : 0);
+        if (!have_ce) Ce = end < n ? uni64(a.sc[end].c) : tail.c;
+        const uint64_t nw = (w != kNone ? 1 : 0) + (end > g ? Ce - Cg : 0);
         if (nw == 0) break;  // nothing left to write: no file (builder.size == 0)
         if (lane == 0) {
             a.files[nf] = MergeFile{p, w, o};
@@ -343,25 +519,27 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
         }
         o += nw;
         nf++;
-        prev_span = end - g;
+        span = end - g;
         p = end;
     }
     if (lane == 0) {
         a.files[nf] = MergeFile{n, kNone, o};
         a.counts[0] = o;
         a.counts[1] = nf;
+        a.counts[2] = fast;  // diagnostics (LSM_MERGE_DBG)
+        a.counts[3] = slow;
     }
 }
 
 // each candidate's output slot: its file's first slot, after the extra, plus
 // the candidates before it in the file
 __global__ __launch_bounds__(kMergeThreads) void merge_emit_kernel(
-    const uint32_t *perm, const uint64_t *C, const uint32_t *cflag, const MergeFile *files,
+    const uint32_t *perm, const SumPair *sc, const uint32_t *csize, const MergeFile *files,
     const uint64_t *counts, uint32_t n, uint32_t *out, uint64_t *file_start) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     const uint32_t nf = (uint32_t)counts[1];
     if (j <= nf && file_start) file_start[j] = files[j].o;
-    if (j >= n || !cflag[j]) return;
+    if (j >= n || !csize[j]) return;
     uint32_t lo = 0, hi = nf;  // last file with p <= j
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) / 2;
@@ -369,7 +547,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_emit_kernel(
     }
     if (nf == 0 || files[lo].p > j || j >= files[lo + 1].p) return;  // past the last file
     const MergeFile F = files[lo];
-    out[F.o + (F.extra != kNone ? 1 : 0) + (C[j] - C[F.p])] = perm[j];
+    out[F.o + (F.extra != kNone ? 1 : 0) + (sc[j].c - sc[F.p].c)] = perm[j];
 }
 
 // ---- gather: the written pairs -> a CSR record batch (build input) --------
@@ -384,37 +562,112 @@ __global__ __launch_bounds__(kMergeThreads) void gather_lens_kernel(MergeIn m, c
     vlen[j] = v.vl;
 }
 
-// one wave per 64 pairs: the wave copies each pair's key and value in turn
+// One wave per 64 pairs; the keys (then the values) of those pairs form one
+// contiguous output range, cut into 16-byte chunks (aligned in the output):
+//   1. each lane marks, in an LDS map, the chunks that start inside its pair;
+//   2. lanes take chunks in turn: a chunk inside one pair is five aligned
+//      source dwords funnel-shifted into one 16-byte store; any other chunk
+//      (it straddles pairs or an end of the range) is queued;
+//   3. the queue is drained four lanes per chunk, a dword (or its bytes) each.
+// Chunks are handled kMapChunks at a time (any pair size).
+constexpr uint32_t kMapChunks = 1024;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
     MergeIn m, const uint32_t *idx, uint32_t nout, const uint64_t *koff, const uint64_t *voff,
     uint8_t *keys, uint8_t *vals) {
-    const uint32_t j0 = (blockIdx.x * kMergeThreads + threadIdx.x) / kWave * kWave;
+    constexpr uint32_t W = kMergeThreads / kWave;
+    __shared__ uint64_t s_dst[W][kWave + 1];
+    __shared__ uint64_t s_src[W][kWave];
+    __shared__ uint8_t s_map[W][kMapChunks];
+    __shared__ uint16_t s_q[W][kMapChunks];
+    const uint32_t w = threadIdx.x / kWave, lane = lane_id();
+    const uint32_t j0 = (blockIdx.x * W + w) * kWave;
     if (j0 >= nout) return;
-    const uint32_t lane = lane_id(), j = j0 + lane;
-    View v{};
-    uint64_t ko = 0, vo = 0;
-    if (j < nout) {
-        v = view(m, idx[j]);
-        ko = koff[j];
-        vo = voff[j];
-    }
     const uint32_t cnt = nout - j0 < kWave ? nout - j0 : kWave;
-    for (uint32_t r = 0; r < cnt; r++) {
-        const uint64_t sk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v.ko >> 32), r) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)v.ko, r);
-        const uint64_t sv = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v.vo >> 32), r) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)v.vo, r);
-        const uint32_t kl = __builtin_amdgcn_readlane(v.kl, r);
-        const uint32_t vl = __builtin_amdgcn_readlane(v.vl, r);
-        const uint64_t dk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ko >> 32), r) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)ko, r);
-        const uint64_t dv = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vo >> 32), r) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)vo, r);
-        // resources start a dword before the bytes (keys and values sit at
-        // rec_off + 4 or later) so wave_copy's offsets never wrap below 0
-        const uint64_t ka = (sk & ~(uint64_t)3) - 4, va = (sv & ~(uint64_t)3) - 4;
-        wave_copy(make_rsrc(m.bytes + ka, kl + 12), (uint32_t)(sk - ka), keys + dk, kl);
-        wave_copy(make_rsrc(m.bytes + va, vl + 12), (uint32_t)(sv - va), vals + dv, vl);
+    View v{};
+    if (lane < cnt) v = view(m, idx[j0 + lane]);
+    for (int which = 0; which < 2; which++) {
+        const uint64_t *off = which ? voff : koff;
+        uint8_t *dst = which ? vals : keys;
+        uint64_t d0 = 0, d1 = 0;
+        if (lane < cnt) {
+            s_src[w][lane] = which ? v.vo : v.ko;
+            d0 = off[j0 + lane];
+            d1 = d0 + (which ? v.vl : v.kl);
+            s_dst[w][lane] = d0;
+        }
+        if (lane == 0) s_dst[w][cnt] = off[j0 + cnt];
+        wave_sync();
+        const uint64_t A = s_dst[w][0], B = s_dst[w][cnt];
+        for (uint64_t X0 = A & ~(uint64_t)15; X0 < B; X0 += 16 * (uint64_t)kMapChunks) {
+            const uint32_t nch = (uint32_t)((B - X0 + 15) / 16 < kMapChunks ? (B - X0 + 15) / 16
+                                                                          : kMapChunks);
+            // 1. chunks whose first byte lies in my pair
+            if (lane < cnt && d1 > d0) {
+                const uint64_t lo = d0 > X0 ? (d0 - X0 + 15) / 16 : 0;
+                const uint64_t hi = (d1 - 1 >= X0) ? (d1 - 1 - X0) / 16 : 0;  // inclusive
+                if (d1 - 1 >= X0)
+                    for (uint64_t c = lo; c <= hi && c < nch; c++) s_map[w][c] = (uint8_t)lane;
+            }
+            wave_sync();
+            // 2. chunks inside one pair; queue the rest
+            uint32_t qn = 0;
+            for (uint32_t c0 = 0; c0 < nch; c0 += kWave) {
+                const uint32_t c = c0 + lane;
+                const uint64_t x = X0 + 16 * (uint64_t)c;
+                bool regular = false;
+                if (c < nch && x >= A && x + 16 <= B) {
+                    const uint32_t r = s_map[w][c];
+                    const uint64_t e0 = s_dst[w][r], e1 = s_dst[w][r + 1];
+                    if (x + 16 <= e1) {
+                        regular = true;
+                        const uintptr_t sa =
+                            reinterpret_cast<uintptr_t>(m.bytes + s_src[w][r] + (x - e0));
+                        const uint32_t *q = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+                        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+                        const uint32_t sh = (uint32_t)sa;
+                        u32x4 o;
+                        o.x = funnel(q0, q1, sh);
+                        o.y = funnel(q1, q2, sh);
+                        o.z = funnel(q2, q3, sh);
+                        o.w = funnel(q3, q4, sh);
+                        *reinterpret_cast<u32x4 *>(dst + x) = o;
+                    }
+                }
+                const uint64_t irr = __ballot(c < nch && !regular);
+                if (c < nch && !regular) s_q[w][qn + mbcnt(irr)] = (uint16_t)c;
+                qn += (uint32_t)__builtin_popcountll(irr);
+            }
+            wave_sync();
+            // 3. queued chunks, four lanes (one dword each) per chunk
+            for (uint32_t i0 = 0; i0 < qn; i0 += kWave / 4) {
+                const uint32_t i = i0 + lane / 4;
+                if (i >= qn) continue;
+                const uint32_t c = s_q[w][i];
+                const uint64_t x = X0 + 16 * (uint64_t)c, xd = x + 4 * (lane & 3);
+                uint32_t r = x >= A ? s_map[w][c] : 0;
+                if (xd >= B) continue;
+                while (r + 1 < cnt && xd >= s_dst[w][r + 1]) r++;
+                if (xd >= A && xd + 4 <= B && xd >= s_dst[w][r] && xd + 4 <= s_dst[w][r + 1]) {
+                    *reinterpret_cast<uint32_t *>(dst + xd) =
+                        ld_u32_any(m.bytes + s_src[w][r] + (xd - s_dst[w][r]));
+                } else {
+                    for (uint32_t u = 0; u < 4; u++) {
+                        const uint64_t b = xd + u;
+                        if (b < A || b >= B) continue;
+                        while (b >= s_dst[w][r + 1]) r++;
+                        dst[b] = m.bytes[s_src[w][r] + (b - s_dst[w][r])];
+                    }
+                }
+            }
+            wave_sync();
+        }
     }
 }
 
@@ -435,16 +688,54 @@ __global__ __launch_bounds__(kMergeThreads) void sst_sizes_kernel(const uint64_t
     size[f] = hdr + filter + 4 * nr + (voff[r1] - voff[r0]) + 12 * nr + (koff[r1] - koff[r0]) + 32;
 }
 
+// ---- positional join of decoded .sst files (loadLevelData) ----------------
+
+__device__ __forceinline__ uint64_t sst_pair_count(const lsm_sst_meta &m) {
+    // GetKeyValuePairs (sstable.go:248-268): nothing from a failed decode or
+    // from a table with no data or no index entries
+    return (m.stage == LSM_SST_OK && m.nidx && m.ndata) ? m.nidx : 0;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void sst_pairs_scan_kernel(const lsm_sst_meta *meta,
+                                                                       uint32_t nfile,
+                                                                       uint64_t *prefix) {
+    uint64_t carry = 0;
+    for (uint32_t f0 = 0; f0 < nfile; f0 += kMergeThreads) {
+        const uint32_t f = f0 + threadIdx.x;
+        const uint64_t c = f < nfile ? sst_pair_count(meta[f]) : 0;
+        SumPair tot;
+        const SumPair x = block_excl_scan2(c, 0, &tot);
+        if (f < nfile) prefix[f] = carry + x.s;
+        carry += tot.s;
+    }
+    if (threadIdx.x == 0) prefix[nfile] = carry;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void sst_pairs_copy_kernel(
+    const lsm_sst_meta *meta, const uint64_t *file_off, const u32x4 *idx_desc,
+    const u32x4 *data_desc, const uint64_t *prefix, u32x4 *key_out, u32x4 *val_out) {
+    const uint32_t f = blockIdx.y;
+    const uint64_t c = sst_pair_count(meta[f]);
+    const uint64_t src = file_off[f] / 4, dst = prefix[f];  // lsm_decode_sst's offset addressing
+    for (uint64_t i = (uint64_t)blockIdx.x * kMergeThreads + threadIdx.x; i < c;
+         i += (uint64_t)gridDim.x * kMergeThreads) {
+        key_out[dst + i] = __builtin_nontemporal_load(&idx_desc[src + i]);
+        val_out[dst + i] = __builtin_nontemporal_load(&data_desc[src + i]);
+    }
+}
+
+// ---- workspace ------------------------------------------------------------
+
 struct MergeWs {
     uint32_t *perm[2];
     uint64_t *keys[2];
     uint8_t *flags;
-    uint32_t *csize, *cflag;
-    uint64_t *S, *C;
+    uint32_t *csize;
+    SumPair *sc;
+    SumPair *scan_part;
     MergeFile *files;
-    uint64_t *stats;  // [0] max len, [1] min len, [2] counts (2 words), [4..] chunk OR/AND
-    void *scan_ws;
-    size_t scan_bytes;
+    uint64_t *stats;  // [0..1] counts, then the long-key OR/AND words
+    uint64_t *part;   // kStatBlocks * kStatWords
     void *sort_tmp;
     size_t sort_bytes;
     size_t total;
@@ -453,7 +744,7 @@ struct MergeWs {
 size_t sort_tmp_bytes(uint32_t n) {
     size_t b = 0;
     (void)rocprim::radix_sort_pairs(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                              (uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 64);
+                                    (uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 64);
     return b;
 }
 
@@ -466,19 +757,18 @@ MergeWs merge_ws_layout(uint8_t *base, uint32_t n) {
         return p;
     };
     const size_t nn = n ? n : 1;
+    const size_t ntiles = (nn + kScanTile - 1) / kScanTile;
     w.perm[0] = reinterpret_cast<uint32_t *>(take(4 * nn));
     w.perm[1] = reinterpret_cast<uint32_t *>(take(4 * nn));
     w.keys[0] = reinterpret_cast<uint64_t *>(take(8 * nn));
     w.keys[1] = reinterpret_cast<uint64_t *>(take(8 * nn));
     w.flags = take(nn);
     w.csize = reinterpret_cast<uint32_t *>(take(4 * nn));
-    w.cflag = reinterpret_cast<uint32_t *>(take(4 * nn));
-    w.S = reinterpret_cast<uint64_t *>(take(8 * (nn + 1)));
-    w.C = reinterpret_cast<uint64_t *>(take(8 * (nn + 1)));
-    w.files = reinterpret_cast<MergeFile *>(take(kFileBytes * (nn + 2)));
-    w.stats = reinterpret_cast<uint64_t *>(take(8 * (4 + 2 * (size_t)kMaxChunks + 2)));
-    w.scan_bytes = scan_workspace_bytes(n);
-    w.scan_ws = take(w.scan_bytes);
+    w.sc = reinterpret_cast<SumPair *>(take(sizeof(SumPair) * (nn + 1)));
+    w.scan_part = reinterpret_cast<SumPair *>(take(sizeof(SumPair) * ntiles));
+    w.files = reinterpret_cast<MergeFile *>(take(sizeof(MergeFile) * (nn + 2)));
+    w.stats = reinterpret_cast<uint64_t *>(take(8 * (2 + 2 * (size_t)kMaxChunks)));
+    w.part = reinterpret_cast<uint64_t *>(take(8 * (size_t)kStatBlocks * kStatWords));
     w.sort_bytes = sort_tmp_bytes(n);
     w.sort_tmp = take(w.sort_bytes);
     w.total = at;
@@ -492,7 +782,8 @@ uint32_t grid_for(uint64_t n) { return (uint32_t)((n + kMergeThreads - 1) / kMer
 
 using namespace lsm;
 
-static_assert(sizeof(MergeFile) == kFileBytes, "MergeFile layout");
+static_assert(sizeof(MergeFile) == 16, "MergeFile layout");
+static_assert(sizeof(SumPair) == 16, "SumPair layout");
 
 extern "C" size_t lsm_merge_kvs_workspace_bytes(uint64_t n) {
     if (n >= 0xFFFFFFFFull) return 0;
@@ -517,34 +808,68 @@ extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec
     const MergeIn m{d_bytes, d_key_desc, d_val_desc, N};
     const uint32_t sb = grid_for(n) < kStatBlocks ? grid_for(n) : kStatBlocks;
 
-    // 1. key lengths, then per-chunk statistics
-    uint64_t init[2] = {0, ~0ull};
-    LSM_HIP_CHECK(hipMemcpyAsync(w.stats, init, 16, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(merge_len_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, w.stats);
-    uint64_t lens[2];
-    LSM_HIP_CHECK(hipMemcpyAsync(lens, w.stats, 16, hipMemcpyDeviceToHost, s));
+    // 1. key statistics: one pass, per-block partials reduced here
+    hipLaunchKernelGGL(merge_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, w.part);
+    std::vector<uint64_t> part((size_t)sb * kStatWords);
+    LSM_HIP_CHECK(hipMemcpyAsync(part.data(), w.part, part.size() * 8, hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
-    const uint32_t D = (uint32_t)((lens[0] + 7) / 8), minlen = (uint32_t)lens[1];
-    if (D > kMaxChunks) return LSM_EINVAL;
-    uint64_t *orand = w.stats + 4;
-    std::vector<uint64_t> st(2 * (size_t)D + 2);
-    for (uint32_t d = 0; d <= D; d++) {
-        st[2 * d] = 0;
-        st[2 * d + 1] = ~0ull;
+    uint64_t st[kStatWords];
+    for (uint32_t t = 0; t < kStatWords; t++) st[t] = part[t];
+    for (uint32_t b = 1; b < sb; b++) {
+        const uint64_t *q = &part[(size_t)b * kStatWords];
+        st[0] = q[0] > st[0] ? q[0] : st[0];
+        st[1] = q[1] < st[1] ? q[1] : st[1];
+        for (uint32_t t = 2; t < kStatWords; t += 2) {
+            st[t] |= q[t];
+            st[t + 1] &= q[t + 1];
+        }
     }
-    LSM_HIP_CHECK(hipMemcpyAsync(orand, st.data(), st.size() * 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(merge_chunk_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, D, orand);
-    LSM_HIP_CHECK(hipMemcpyAsync(st.data(), orand, st.size() * 8, hipMemcpyDeviceToHost, s));
-    LSM_HIP_CHECK(hipStreamSynchronize(s));
+    const uint32_t D = (uint32_t)((st[0] + 7) / 8), minlen = (uint32_t)st[1];
+    if (D > kMaxChunks) return LSM_EINVAL;
+    std::vector<uint64_t> orand(2 * (size_t)(D > kFastChunks ? D : kFastChunks));
+    for (uint32_t d = 0; d < kFastChunks; d++) {
+        orand[2 * d] = st[4 + 2 * d];
+        orand[2 * d + 1] = st[5 + 2 * d];
+    }
+    if (D > kFastChunks) {  // long keys: the remaining chunks by atomics
+        uint64_t *dev = w.stats + 2;
+        for (uint32_t d = kFastChunks; d < D; d++) {
+            orand[2 * d] = 0;
+            orand[2 * d + 1] = ~0ull;
+        }
+        LSM_HIP_CHECK(hipMemcpyAsync(dev, orand.data(), orand.size() * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(merge_long_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, D, dev);
+        LSM_HIP_CHECK(hipMemcpyAsync(orand.data() + 2 * kFastChunks, dev + 2 * kFastChunks,
+                                     (orand.size() - 2 * kFastChunks) * 8, hipMemcpyDeviceToHost, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));
+    }
 
-    // 2. stable LSD passes: key length, then chunks D-1 .. 0 (varying bits only)
+    // 2. stable LSD passes over packed groups of fields: from the least
+    //    significant field (the key length) up to chunk 0; a group holds up
+    //    to 64 varying bits
+    std::vector<std::pair<uint32_t, uint64_t>> fields;  // least significant first
+    if (st[2] & ~st[3]) fields.push_back({kNone, st[2] & ~st[3]});
+    for (uint32_t d = D; d-- > 0;) {
+        const uint64_t and_d = minlen > 8 * d ? orand[2 * d + 1] : 0;  // short keys hold 0
+        const uint64_t vary = orand[2 * d] & ~and_d;
+        if (vary) fields.push_back({d, vary});
+    }
     int cur = 0;
     bool have_perm = false;
-    auto pass = [&](uint32_t d, uint64_t vary) -> int {
-        if (!vary) return 0;
-        const int b0 = __builtin_ctzll(vary), b1 = 64 - __builtin_clzll(vary);
+    for (size_t f0 = 0; f0 < fields.size();) {
+        size_t f1 = f0;
+        uint32_t bits = 0;
+        while (f1 < fields.size() && f1 - f0 < kGroupFields &&
+               bits + __builtin_popcountll(fields[f1].second) <= 64)
+            bits += __builtin_popcountll(fields[f1++].second);
+        SortGroup g{};
+        g.nf = (uint32_t)(f1 - f0);
+        for (size_t t = 0; t < g.nf; t++) {  // most significant first
+            g.field[t] = fields[f1 - 1 - t].first;
+            g.mask[t] = fields[f1 - 1 - t].second;
+        }
         hipLaunchKernelGGL(merge_extract_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m,
-                           have_perm ? w.perm[cur] : nullptr, d, w.keys[0]);
+                           have_perm ? w.perm[cur] : nullptr, g, w.keys[0]);
         if (!have_perm) {
             hipLaunchKernelGGL(merge_iota_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s,
                                w.perm[cur], N);
@@ -552,43 +877,53 @@ extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec
         }
         size_t tb = w.sort_bytes;
         const hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, tb, w.keys[0], w.keys[1],
-                                                       w.perm[cur], w.perm[cur ^ 1], N, b0, b1, s);
+                                                       w.perm[cur], w.perm[cur ^ 1], N, 0, bits, s);
         if (e != hipSuccess) return -(1000 + (int)e);
         cur ^= 1;
-        return 0;
-    };
-    int rc = pass(kNone, st[2 * D] & ~st[2 * D + 1]);
-    for (uint32_t d = D; rc == 0 && d-- > 0;) {
-        const uint64_t and_d = minlen > 8 * d ? st[2 * d + 1] : 0;  // short keys hold 0
-        rc = pass(d, st[2 * d] & ~and_d);
+        f0 = f1;
     }
-    if (rc) return rc;
     if (!have_perm)
         hipLaunchKernelGGL(merge_iota_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s,
                            w.perm[cur], N);
     const uint32_t *perm = w.perm[cur];
 
-    // 3. groups and candidates; 4. scans and the file walk; 5. emit
+    // 3. groups and candidates; 4. sums and the file walk; 5. emit
     hipLaunchKernelGGL(merge_flags_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m, perm,
                        level, w.flags);
     hipLaunchKernelGGL(merge_candidate_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m,
-                       perm, w.flags, w.csize, w.cflag);
-    rc = scan_u32_to_u64(w.csize, N, w.S, w.scan_ws, w.scan_bytes, s);
-    if (!rc) rc = scan_u32_to_u64(w.cflag, N, w.C, w.scan_ws, w.scan_bytes, s);
-    if (rc) return rc;
-    WalkArgs wa{m, perm, w.flags, w.S, w.C, threshold, w.files, d_out, w.stats + 2};
+                       perm, w.flags, w.csize);
+    const uint32_t ntiles = (N + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(merge_scan_tiles, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
+                       w.scan_part);
+    hipLaunchKernelGGL(merge_scan_partials, dim3(1), dim3(kMergeThreads), 0, s, w.scan_part, ntiles,
+                       w.sc, N);
+    hipLaunchKernelGGL(merge_scan_apply, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
+                       w.scan_part, w.sc);
+    WalkArgs wa{m, perm, w.flags, w.sc, threshold, w.files, d_out, w.stats};
     hipLaunchKernelGGL(merge_walk_kernel, dim3(1), dim3(64), 0, s, wa);
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
-                       w.C, w.cflag, w.files, w.stats + 2, N, d_out, d_file_start);
+                       w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);
     LSM_HIP_CHECK(hipGetLastError());
-    LSM_HIP_CHECK(hipMemcpyAsync(h_counts, w.stats + 2, 16, hipMemcpyDeviceToHost, s));
+    uint64_t c4[4];
+    LSM_HIP_CHECK(hipMemcpyAsync(c4, w.stats, 32, hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
+    h_counts[0] = c4[0];
+    h_counts[1] = c4[1];
+    if (getenv("LSM_MERGE_DBG"))
+        fprintf(stderr, "lsm_merge_kvs: %llu files, walk fast %llu slow %llu\n",
+                (unsigned long long)c4[1], (unsigned long long)c4[2], (unsigned long long)c4[3]);
     return 0;
 }
 
 extern "C" size_t lsm_gather_kvs_workspace_bytes(uint64_t nout) {
     const size_t nn = nout ? nout : 1;
-    return 2 * ((4 * nn + 255) & ~(size_t)255) + scan_workspace_bytes((uint32_t)nout);
+    const size_t ntiles = (nn + kScanTile - 1) / kScanTile;
+    return 2 * ((4 * nn + 255) & ~(size_t)255) + 8 * ntiles + 256;
+}
+
+namespace lsm {
+int scan_u32_to_u64(const uint32_t *d_len, uint32_t n, uint64_t *d_out, void *ws, size_t ws_bytes,
+                    hipStream_t s);
 }
 
 extern "C" int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
@@ -605,7 +940,7 @@ extern "C" int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_re
     uint32_t *kl = static_cast<uint32_t *>(d_ws);
     uint32_t *vl = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_ws) + part);
     void *sw = static_cast<uint8_t *>(d_ws) + 2 * part;
-    const size_t sbytes = scan_workspace_bytes(N);
+    const size_t sbytes = ws_bytes - 2 * part;
     const MergeIn m{d_bytes, d_key_desc, d_val_desc, N};
     if (N)
         hipLaunchKernelGGL(gather_lens_kernel, dim3(grid_for(nout)), dim3(kMergeThreads), 0, s, m,
@@ -614,8 +949,8 @@ extern "C" int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_re
     if (!rc) rc = scan_u32_to_u64(vl, N, d_voff, sw, sbytes, s);
     if (rc) return rc;
     if (N)
-        hipLaunchKernelGGL(gather_copy_kernel, dim3(grid_for(nout)), dim3(kMergeThreads), 0, s, m,
-                           d_idx, N, d_koff, d_voff, d_keys, d_vals);
+        hipLaunchKernelGGL(gather_copy_kernel, dim3((N + kMergeThreads - 1) / kMergeThreads),
+                           dim3(kMergeThreads), 0, s, m, d_idx, N, d_koff, d_voff, d_keys, d_vals);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -628,6 +963,25 @@ extern "C" int lsm_sst_image_sizes(lsm_ctx *ctx, const uint64_t *d_koff, const u
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(sst_sizes_kernel, dim3(grid_for(nfile)), dim3(kMergeThreads), 0, s, d_koff,
                        d_voff, d_file_start, nfile, lsm_filter_block_size(m), d_size);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_sst_pairs(lsm_ctx *ctx, const lsm_sst_meta *d_meta, const uint64_t *d_file_off,
+                             uint32_t nfile, const lsm_rec_desc *d_idx_desc,
+                             const lsm_rec_desc *d_data_desc, lsm_rec_desc *d_key_out,
+                             lsm_rec_desc *d_val_out, uint64_t *d_prefix, void *stream) {
+    if (!ctx || !d_prefix) return LSM_EINVAL;
+    if (nfile && (!d_meta || !d_file_off || !d_idx_desc || !d_data_desc || !d_key_out || !d_val_out))
+        return LSM_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(sst_pairs_scan_kernel, dim3(1), dim3(kMergeThreads), 0, s, d_meta, nfile,
+                       d_prefix);
+    if (nfile)
+        hipLaunchKernelGGL(sst_pairs_copy_kernel, dim3(16, nfile), dim3(kMergeThreads), 0, s, d_meta,
+                           d_file_off, reinterpret_cast<const u32x4 *>(d_idx_desc),
+                           reinterpret_cast<const u32x4 *>(d_data_desc), d_prefix,
+                           reinterpret_cast<u32x4 *>(d_key_out), reinterpret_cast<u32x4 *>(d_val_out));
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

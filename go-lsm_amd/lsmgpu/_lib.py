@@ -98,6 +98,9 @@ SIGNATURES = {
     "lsm_sst_image_sizes": (ctypes.c_int, [ctypes.c_void_p, c_u64p, c_u64p, c_u64p,
                                            ctypes.c_uint32, ctypes.c_uint64, c_u64p,
                                            ctypes.c_void_p]),
+    "lsm_sst_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64p, ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, c_u64p, ctypes.c_void_p]),
     "lsm_dev_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_void_p)]),
     "lsm_dev_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

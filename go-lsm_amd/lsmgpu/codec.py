@@ -573,8 +573,8 @@ class Merge:
 def alloc_merge(ctx: Context, n: int) -> Merge:
     dev = ctx.torch_device
     ws = int(ctx.lib.lsm_merge_kvs_workspace_bytes(n))
-    return Merge(out=torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
-                 file_start=torch.zeros(n + 1, dtype=torch.int64, device=dev),
+    return Merge(out=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                 file_start=torch.empty(n + 1, dtype=torch.int64, device=dev),
                  workspace=torch.empty(ws, dtype=torch.uint8, device=dev), n=n)
 
 
@@ -606,10 +606,10 @@ def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
     key_bytes / val_bytes bound the selected bytes.  koff_host / voff_host
     are left None (use sst_layout for the image sizes)."""
     dev = ctx.torch_device
-    keys = torch.zeros(pad16(max(key_bytes, 1)), dtype=torch.uint8, device=dev)
-    vals = torch.zeros(pad16(max(val_bytes, 1)), dtype=torch.uint8, device=dev)
-    koff = torch.zeros(nout + 1, dtype=torch.int64, device=dev)
-    voff = torch.zeros(nout + 1, dtype=torch.int64, device=dev)
+    keys = torch.empty(pad16(max(key_bytes, 1)), dtype=torch.uint8, device=dev)
+    vals = torch.empty(pad16(max(val_bytes, 1)), dtype=torch.uint8, device=dev)
+    koff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
+    voff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
     ws = torch.empty(int(ctx.lib.lsm_gather_kvs_workspace_bytes(nout)), dtype=torch.uint8,
                      device=dev)
     _lib.check(ctx.lib.lsm_gather_kvs(
@@ -639,8 +639,8 @@ def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Ten
     total = int(padded.sum())
     max_recs = int(np.diff(file_start.astype(np.int64)).max()) if nfile else 0
     ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nfile, max_recs, m, k))
-    return SstBuild(
-        out=torch.zeros(pad16(total), dtype=torch.uint8, device=dev),
+    return SstBuild(  # every image byte is written by lsm_build_sst: no fill
+        out=torch.empty(pad16(total), dtype=torch.uint8, device=dev),
         file_start=file_start, file_off=file_off, file_size=sizes.copy(),
         footer=torch.zeros(max(nfile, 1) * 4, dtype=torch.int64, device=dev),
         workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
@@ -649,16 +649,23 @@ def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Ten
         max_recs=max_recs, m=m, k=k)
 
 
-def sst_pairs(r: "SstDecode") -> tuple:
-    """Dense (key descriptors, value descriptors) of every file's pairs in
-    file order -- the positional join of GetKeyValuePairs (sstable.go:248-268),
-    i.e. loadLevelData's allPairs (compaction.go:173-193), as device index
-    gathers.  Files that failed or hold no pairs contribute nothing."""
-    meta = r.meta_numpy()
-    base = r.bases().astype(np.int64)
-    parts = [np.arange(b, b + int(mt["nidx"]), dtype=np.int64)
-             for b, mt in zip(base, meta)
-             if mt["stage"] == 0 and mt["nidx"] and mt["ndata"]]
-    sel = np.concatenate(parts) if parts else np.zeros(0, np.int64)
-    d_sel = torch.from_numpy(sel).to(r.idx_desc.device)
-    return r.idx_desc.index_select(0, d_sel), r.data_desc.index_select(0, d_sel)
+def sst_pairs_into(ctx: Context, r: "SstDecode", key_out: torch.Tensor, val_out: torch.Tensor,
+                   prefix: torch.Tensor, stream=None) -> None:
+    """lsm_sst_pairs: the positional join of every decoded file, file after
+    file (loadLevelData's allPairs), into dense descriptor arrays."""
+    _lib.check(ctx.lib.lsm_sst_pairs(
+        ctx.handle, _ptr(r.meta), _ptr(r.d_file_off), r.nfile, _ptr(r.idx_desc), _ptr(r.data_desc),
+        _ptr(key_out), _ptr(val_out), _ptr(prefix), _stream_handle(stream)), "lsm_sst_pairs")
+
+
+def sst_pairs(ctx: Context, r: "SstDecode", stream=None) -> tuple:
+    """(key descriptors, value descriptors, prefix) of every file's pairs in
+    file order; sized from the decoded metadata."""
+    dev = r.idx_desc.device
+    cap = int(r.idx_desc.shape[0])
+    kd = torch.empty((cap, 4), dtype=torch.int32, device=dev)
+    vd = torch.empty((cap, 4), dtype=torch.int32, device=dev)
+    prefix = torch.zeros(r.nfile + 1, dtype=torch.int64, device=dev)
+    sst_pairs_into(ctx, r, kd, vd, prefix, stream=stream)
+    n = int(prefix[r.nfile].item())
+    return kd[:n], vd[:n], prefix

@@ -343,6 +343,18 @@ int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_k
                    uint8_t *d_keys, uint64_t *d_koff, uint8_t *d_vals, uint64_t *d_voff,
                    void *d_ws, size_t ws_bytes, void *stream);
 
+/* The positional join of decoded files in file order -- loadLevelData's
+ * allPairs (compaction.go:173-193) over GetKeyValuePairs (sstable.go:248-268):
+ * d_key_out / d_val_out = the files' index (key) and data (value) descriptors
+ * from lsm_decode_sst's outputs (file f's entries at slot d_file_off[f] / 4),
+ * densely, file after file; files that failed (stage != 0) or hold no data or
+ * no index entries contribute nothing.  d_prefix[0 .. nfile] = each file's
+ * first output slot, d_prefix[nfile] = the total.  Asynchronous. */
+int lsm_sst_pairs(lsm_ctx *ctx, const lsm_sst_meta *d_meta, const uint64_t *d_file_off,
+                  uint32_t nfile, const lsm_rec_desc *d_idx_desc, const lsm_rec_desc *d_data_desc,
+                  lsm_rec_desc *d_key_out, lsm_rec_desc *d_val_out, uint64_t *d_prefix,
+                  void *stream);
+
 /* .sst image size of each file f = records [d_file_start[f], d_file_start[f+1])
  * of a device CSR batch (as lsm_sst_image_size_host, sstable.go:131-193). */
 int lsm_sst_image_sizes(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff,

@@ -2,6 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 CFG=${CFG:-mixed}
+KF=${KF:-decode}
 mkdir -p gpurun_out/pmcd
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS" \
@@ -9,13 +10,13 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmcd/p$i -o run -- python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmcd/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmcd/p$i.log; exit 1; }
 done
-python - <<'PY'
-import csv, glob, collections
+KF=$KF python - <<'PY'
+import csv, glob, collections, os
 for f in sorted(glob.glob("gpurun_out/pmcd/p*/**/*counter_collection.csv", recursive=True)):
     agg = collections.defaultdict(lambda: collections.defaultdict(float)); cnt = collections.Counter()
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"][:60]
-        if "decode" not in k: continue
+        if not any(x in k for x in os.environ.get("KF", "decode").split(",")): continue
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[(k, r["Counter_Name"])] += 1
     for k, d in agg.items():

@@ -167,3 +167,44 @@ def test_gather_and_build_match_oracle_images(ctx):
         o = int(sb.file_off[f])
         assert int(sb.file_size[f]) == want.size
         assert np.array_equal(img[o:o + want.size], want), f
+
+
+def test_sst_pairs_join(ctx):
+    """lsm_sst_pairs = loadLevelData's allPairs: every decoded file's
+    (index key, data value) pairs in file order; failed files contribute
+    nothing (their GetDataBlockFromFile error aborts the Go caller instead)."""
+    rng = random.Random(13)
+    images = []
+    for f in range(5):
+        keys = sorted({b"f%d_%05d" % (f % 3, rng.randint(0, 99999)) for _ in range(rng.randint(0, 400))})
+        kb = b"".join(keys)
+        ko = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+        vals = [bytes(rng.randint(0, 255) for _ in range(rng.randint(0, 50))) for _ in keys]
+        vo = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.uint64)
+        img, _ = ora.build_sst(np.frombuffer(kb, np.uint8), ko, np.frombuffer(b"".join(vals) or b"\0", np.uint8),
+                               vo, 0, len(keys), m=4096, k=3)
+        images.append((img, keys, vals))
+    bad = images[1][0].copy()
+    bad[:4] = 255  # header length past the end: stage 1
+    images[1] = (bad, [], [])
+    offs, pos, parts = [], 0, []
+    for img, _, _ in images:
+        gap = rng.randint(0, 40)
+        parts += [np.zeros(gap, np.uint8), img]
+        pos += gap
+        offs.append(pos)
+        pos += img.size
+    buf = np.concatenate(parts)
+    d_img = lsmgpu.to_device_bytes(buf, ctx.torch_device)
+    r = lsmgpu.decode_sst(ctx, d_img, np.array(offs, np.uint64),
+                          np.array([im.size for im, _, _ in images], np.uint64))
+    kd, vd, prefix = lsmgpu.sst_pairs(ctx, r)
+    torch.cuda.synchronize()
+    kd = kd.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+    vd = vd.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+    want = [(k, v) for _, keys, vals in images for k, v in zip(keys, vals)]
+    got = [(buf[d["rec_off"] + 4:d["rec_off"] + 4 + d["key_len"]].tobytes(),
+            buf[e["rec_off"] + 4:e["rec_off"] + 4 + e["val_len"]].tobytes()) for d, e in zip(kd, vd)]
+    assert got == want
+    counts = [0 if i == 1 else len(images[i][1]) for i in range(5)]
+    assert list(prefix.cpu().numpy()) == list(np.concatenate([[0], np.cumsum(counts)]))
