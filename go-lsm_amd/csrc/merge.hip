@@ -562,15 +562,20 @@ __global__ __launch_bounds__(kMergeThreads) void gather_lens_kernel(MergeIn m, c
     vlen[j] = v.vl;
 }
 
-// One wave per 64 pairs; the keys (then the values) of those pairs form one
-// contiguous output range, cut into 16-byte chunks (aligned in the output):
-//   1. each lane marks, in an LDS map, the chunks that start inside its pair;
-//   2. lanes take chunks in turn: a chunk inside one pair is five aligned
-//      source dwords funnel-shifted into one 16-byte store; any other chunk
-//      (it straddles pairs or an end of the range) is queued;
+// One wave per 64 pairs.  Their keys form one contiguous output range and
+// their values another; both are cut into 16-byte chunks (aligned in the
+// output) numbered in one space, keys first:
+//   1. each lane marks, in an LDS map, the chunks that start inside its key
+//      or its value;
+//   2. lanes take four chunks at a time and issue every source load before
+//      any store (a round trip covers four chunks): a chunk inside one
+//      key or value is five aligned source dwords funnel-shifted into one
+//      16-byte store; any other chunk (it straddles pairs or an end of the
+//      range) is queued;
 //   3. the queue is drained four lanes per chunk, a dword (or its bytes) each.
 // Chunks are handled kMapChunks at a time (any pair size).
 constexpr uint32_t kMapChunks = 1024;
+constexpr uint32_t kUnroll = 4;
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -582,92 +587,132 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
     MergeIn m, const uint32_t *idx, uint32_t nout, const uint64_t *koff, const uint64_t *voff,
     uint8_t *keys, uint8_t *vals) {
     constexpr uint32_t W = kMergeThreads / kWave;
-    __shared__ uint64_t s_dst[W][kWave + 1];
-    __shared__ uint64_t s_src[W][kWave];
+    __shared__ uint64_t s_dst[W][2][kWave + 1];
+    __shared__ uint64_t s_src[W][2][kWave];
     __shared__ uint8_t s_map[W][kMapChunks];
     __shared__ uint16_t s_q[W][kMapChunks];
     const uint32_t w = threadIdx.x / kWave, lane = lane_id();
     const uint32_t j0 = (blockIdx.x * W + w) * kWave;
     if (j0 >= nout) return;
     const uint32_t cnt = nout - j0 < kWave ? nout - j0 : kWave;
-    View v{};
-    if (lane < cnt) v = view(m, idx[j0 + lane]);
-    for (int which = 0; which < 2; which++) {
-        const uint64_t *off = which ? voff : koff;
-        uint8_t *dst = which ? vals : keys;
-        uint64_t d0 = 0, d1 = 0;
-        if (lane < cnt) {
-            s_src[w][lane] = which ? v.vo : v.ko;
-            d0 = off[j0 + lane];
-            d1 = d0 + (which ? v.vl : v.kl);
-            s_dst[w][lane] = d0;
+    uint64_t d0[2] = {0, 0}, d1[2] = {0, 0};
+    if (lane < cnt) {
+        const View v = view(m, idx[j0 + lane]);
+        d0[0] = koff[j0 + lane];
+        d0[1] = voff[j0 + lane];
+        d1[0] = d0[0] + v.kl;
+        d1[1] = d0[1] + v.vl;
+        s_src[w][0][lane] = v.ko;
+        s_src[w][1][lane] = v.vo;
+        s_dst[w][0][lane] = d0[0];
+        s_dst[w][1][lane] = d0[1];
+    }
+    if (lane == 0) {
+        s_dst[w][0][cnt] = koff[j0 + cnt];
+        s_dst[w][1][cnt] = voff[j0 + cnt];
+    }
+    wave_sync();
+    uint64_t A[2], B[2], X[2];
+    uint32_t nc[2];
+    for (int h = 0; h < 2; h++) {
+        A[h] = s_dst[w][h][0];
+        B[h] = s_dst[w][h][cnt];
+        X[h] = A[h] & ~(uint64_t)15;
+        nc[h] = B[h] > A[h] ? (uint32_t)((B[h] - X[h] + 15) / 16) : 0;
+    }
+    uint8_t *const dsts[2] = {keys, vals};
+    const uint32_t total = nc[0] + nc[1];
+    for (uint32_t P = 0; P < total; P += kMapChunks) {
+        const uint32_t np = total - P < kMapChunks ? total - P : kMapChunks;
+        // 1. chunks whose first byte lies in my key / value
+        for (int h = 0; h < 2; h++) {
+            if (lane < cnt && d1[h] > d0[h] && d1[h] - 1 >= X[h]) {
+                const uint64_t lo = d0[h] > X[h] ? (d0[h] - X[h] + 15) / 16 : 0;
+                const uint64_t hi = (d1[h] - 1 - X[h]) / 16;
+                const uint64_t base = h ? nc[0] : 0;
+                const uint64_t c_lo = base + lo > P ? base + lo : P;
+                const uint64_t c_hi = base + hi < (uint64_t)P + np - 1 ? base + hi : (uint64_t)P + np - 1;
+                for (uint64_t c = c_lo; c <= c_hi; c++) s_map[w][c - P] = (uint8_t)lane;
+            }
         }
-        if (lane == 0) s_dst[w][cnt] = off[j0 + cnt];
         wave_sync();
-        const uint64_t A = s_dst[w][0], B = s_dst[w][cnt];
-        for (uint64_t X0 = A & ~(uint64_t)15; X0 < B; X0 += 16 * (uint64_t)kMapChunks) {
-            const uint32_t nch = (uint32_t)((B - X0 + 15) / 16 < kMapChunks ? (B - X0 + 15) / 16
-                                                                          : kMapChunks);
-            // 1. chunks whose first byte lies in my pair
-            if (lane < cnt && d1 > d0) {
-                const uint64_t lo = d0 > X0 ? (d0 - X0 + 15) / 16 : 0;
-                const uint64_t hi = (d1 - 1 >= X0) ? (d1 - 1 - X0) / 16 : 0;  // inclusive
-                if (d1 - 1 >= X0)
-                    for (uint64_t c = lo; c <= hi && c < nch; c++) s_map[w][c] = (uint8_t)lane;
-            }
-            wave_sync();
-            // 2. chunks inside one pair; queue the rest
-            uint32_t qn = 0;
-            for (uint32_t c0 = 0; c0 < nch; c0 += kWave) {
-                const uint32_t c = c0 + lane;
-                const uint64_t x = X0 + 16 * (uint64_t)c;
-                bool regular = false;
-                if (c < nch && x >= A && x + 16 <= B) {
-                    const uint32_t r = s_map[w][c];
-                    const uint64_t e0 = s_dst[w][r], e1 = s_dst[w][r + 1];
-                    if (x + 16 <= e1) {
-                        regular = true;
-                        const uintptr_t sa =
-                            reinterpret_cast<uintptr_t>(m.bytes + s_src[w][r] + (x - e0));
-                        const uint32_t *q = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
-                        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
-                        const uint32_t sh = (uint32_t)sa;
-                        u32x4 o;
-                        o.x = funnel(q0, q1, sh);
-                        o.y = funnel(q1, q2, sh);
-                        o.z = funnel(q2, q3, sh);
-                        o.w = funnel(q3, q4, sh);
-                        *reinterpret_cast<u32x4 *>(dst + x) = o;
-                    }
-                }
-                const uint64_t irr = __ballot(c < nch && !regular);
-                if (c < nch && !regular) s_q[w][qn + mbcnt(irr)] = (uint16_t)c;
-                qn += (uint32_t)__builtin_popcountll(irr);
-            }
-            wave_sync();
-            // 3. queued chunks, four lanes (one dword each) per chunk
-            for (uint32_t i0 = 0; i0 < qn; i0 += kWave / 4) {
-                const uint32_t i = i0 + lane / 4;
-                if (i >= qn) continue;
-                const uint32_t c = s_q[w][i];
-                const uint64_t x = X0 + 16 * (uint64_t)c, xd = x + 4 * (lane & 3);
-                uint32_t r = x >= A ? s_map[w][c] : 0;
-                if (xd >= B) continue;
-                while (r + 1 < cnt && xd >= s_dst[w][r + 1]) r++;
-                if (xd >= A && xd + 4 <= B && xd >= s_dst[w][r] && xd + 4 <= s_dst[w][r + 1]) {
-                    *reinterpret_cast<uint32_t *>(dst + xd) =
-                        ld_u32_any(m.bytes + s_src[w][r] + (xd - s_dst[w][r]));
-                } else {
-                    for (uint32_t u = 0; u < 4; u++) {
-                        const uint64_t b = xd + u;
-                        if (b < A || b >= B) continue;
-                        while (b >= s_dst[w][r + 1]) r++;
-                        dst[b] = m.bytes[s_src[w][r] + (b - s_dst[w][r])];
+        // 2. chunks inside one key / value, four per lane per round; queue the rest
+        uint32_t qn = 0;
+        for (uint32_t c0 = 0; c0 < np; c0 += kUnroll * kWave) {
+            uint32_t q[kUnroll][5];
+            uint32_t sh[kUnroll];
+            uint8_t *out[kUnroll];
+            bool reg[kUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kUnroll; u++) {
+                const uint32_t c = c0 + u * kWave + lane;
+                reg[u] = false;
+                out[u] = nullptr;
+                sh[u] = 0;
+                if (c < np) {
+                    const uint32_t cid = P + c;
+                    const int h = cid >= nc[0];
+                    const uint64_t x = X[h] + 16 * (uint64_t)(cid - (h ? nc[0] : 0));
+                    if (x >= A[h] && x + 16 <= B[h]) {
+                        const uint32_t r = s_map[w][c];
+                        const uint64_t e0 = s_dst[w][h][r], e1 = s_dst[w][h][r + 1];
+                        if (x + 16 <= e1) {
+                            reg[u] = true;
+                            const uintptr_t sa =
+                                reinterpret_cast<uintptr_t>(m.bytes + s_src[w][h][r] + (x - e0));
+                            const uint32_t *qa = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+                            sh[u] = (uint32_t)sa;
+                            out[u] = dsts[h] + x;
+#pragma unroll
+                            for (int t = 0; t < 5; t++) q[u][t] = qa[t];
+                        }
                     }
                 }
             }
-            wave_sync();
+#pragma unroll
+            for (uint32_t u = 0; u < kUnroll; u++) {
+                if (reg[u]) {
+                    u32x4 o;
+                    o.x = funnel(q[u][0], q[u][1], sh[u]);
+                    o.y = funnel(q[u][1], q[u][2], sh[u]);
+                    o.z = funnel(q[u][2], q[u][3], sh[u]);
+                    o.w = funnel(q[u][3], q[u][4], sh[u]);
+                    *reinterpret_cast<u32x4 *>(out[u]) = o;
+                }
+                const uint32_t c = c0 + u * kWave + lane;
+                const bool irr = c < np && !reg[u];
+                const uint64_t im = __ballot(irr);
+                if (irr) s_q[w][qn + mbcnt(im)] = (uint16_t)c;
+                qn += (uint32_t)__builtin_popcountll(im);
+            }
         }
+        wave_sync();
+        // 3. queued chunks, four lanes (one dword each) per chunk
+        for (uint32_t i0 = 0; i0 < qn; i0 += kWave / 4) {
+            const uint32_t i = i0 + lane / 4;
+            if (i >= qn) continue;
+            const uint32_t c = s_q[w][i], cid = P + c;
+            const int h = cid >= nc[0];
+            const uint64_t x = X[h] + 16 * (uint64_t)(cid - (h ? nc[0] : 0));
+            const uint64_t xd = x + 4 * (lane & 3);
+            if (xd >= B[h]) continue;
+            uint32_t r = x >= A[h] ? s_map[w][c] : 0;
+            const uint64_t *sd = s_dst[w][h];
+            const uint64_t *ss = s_src[w][h];
+            uint8_t *dst = dsts[h];
+            while (r + 1 < cnt && xd >= sd[r + 1]) r++;
+            if (xd >= A[h] && xd + 4 <= B[h] && xd >= sd[r] && xd + 4 <= sd[r + 1]) {
+                *reinterpret_cast<uint32_t *>(dst + xd) = ld_u32_any(m.bytes + ss[r] + (xd - sd[r]));
+            } else {
+                for (uint32_t u = 0; u < 4; u++) {
+                    const uint64_t b = xd + u;
+                    if (b < A[h] || b >= B[h]) continue;
+                    while (b >= sd[r + 1]) r++;
+                    dst[b] = m.bytes[ss[r] + (b - sd[r])];
+                }
+            }
+        }
+        wave_sync();
     }
 }
 
