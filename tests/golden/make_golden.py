@@ -125,6 +125,14 @@ def reference_vectors():
                        "keys": ["key1", "key2"], "values": ["value1", "value2"]}
     v["sst_iterator"] = {"src": "sstable/iterator_test.go:15-49", "m": 1024, "k": 5,
                          "keys": ["a", "b", "c", "d", "e"], "values": ["A", "B", "C", "D", "E"]}
+    # merge_test.go:12-60 TestCompactAndMergeBlocks_Basic: sorted, deduplicated,
+    # the first "beta" (B) kept, one level-1 table of 4 entries
+    v["merge_basic"] = {"src": "sstable/merge_test.go:12-60", "level": 1,
+                        "pairs": [["alpha", "A"], ["beta", "B"], ["beta", "B2"], ["carrot", "C"],
+                                  ["delta", "D"]],
+                        "expect_keys": ["alpha", "beta", "carrot", "delta"],
+                        "expect_values": ["A", "B", "C", "D"], "expect_tables": 1,
+                        "may_contain": ["alpha", "delta"], "absent": ["nonexistent", "deletedKey"]}
     v["murmur"] = {"src": "sstable/bloom/murmur_test.go:12-35", "max_len": 1000,
                    "smhasher_verification_mmh3_x64_128": "0x6384ba69"}
     return v

@@ -361,3 +361,27 @@ def test_footer_cases():
         b = struct.pack("<qqqq", *case)
         assert len(b) == REF["footer"]["footer_size"]
         assert struct.unpack("<qqqq", b) == tuple(case)
+
+
+def test_merge_basic_vector():
+    """merge_test.go:12-60 through the merge oracle (both tie orders), and the
+    one table it builds: its keys, values and filter."""
+    v = REF["merge_basic"]
+    pairs = [(k.encode(), x.encode()) for k, x in v["pairs"]]
+    for tie in (ora.TIE_INPUT, ora.TIE_GOHEAP):
+        out, starts = ora.merge_pairs(pairs, v["level"], 2 * 1024 * 1024, tie)
+        assert [pairs[i][0].decode() for i in out] == v["expect_keys"]
+        assert [pairs[i][1].decode() for i in out] == v["expect_values"]
+        assert len(starts) - 1 == v["expect_tables"]
+    keys = b"".join(pairs[i][0] for i in out)
+    vals = b"".join(pairs[i][1] for i in out)
+    koff = np.concatenate([[0], np.cumsum([len(pairs[i][0]) for i in out])]).astype(np.uint64)
+    voff = np.concatenate([[0], np.cumsum([len(pairs[i][1]) for i in out])]).astype(np.uint64)
+    img, _ = ora.build_sst(np.frombuffer(keys, np.uint8), koff, np.frombuffer(vals, np.uint8),
+                           voff, 0, len(out))
+    rc, meta, *_ = ora.sst_decode(img)
+    assert rc == 0 and meta.nidx == 4
+    hdr = 8 + meta.min_key_len + meta.max_key_len
+    f, _, _ = ora.Bloom.decode(img[hdr:])
+    assert all(f.test(k.encode()) for k in v["may_contain"])
+    assert not any(f.test(k.encode()) for k in v["absent"])
