@@ -1067,16 +1067,23 @@ __global__ __launch_bounds__(256) void bloom_probe_kernel(const uint64_t *words,
 // order, then Filter.Test (bloom.go:371-379) on the filter block as stored in
 // the image (u64 big-endian words, bitset v1.22.0 WriteTo; bit p -> word p>>6
 // bit p&63; bitset.Test is false past its length).  One thread per key
-// hashes it once (sum256) and walks the files; the files' key bounds are
-// staged in LDS as big-endian words (prefix compares in integer registers),
-// 256 files per pass.
-constexpr uint32_t kMcTile = 256;
+// hashes it once (sum256) and walks the files.  Per tile of kMcTile files the
+// block stages each file's bounds (16-byte big-endian prefixes), pointers
+// and filter parameters in LDS, packs its results four files to a dword in
+// an LDS out tile, and then writes the block's rows x tile sub-block of the
+// hit matrix coalesced (dwords when nfile is a multiple of 4).
+constexpr uint32_t kMcTile = 64;
+constexpr uint32_t kMcThreads = 256;
+constexpr uint32_t kMcRow = kMcTile / 4 + 1;  // dwords per out-tile row (+1: LDS banks)
 
 struct McFile {
     uint32_t lo[4], hi[4];  // first 16 bytes of min / max key, big-endian, zero padded
     uint32_t lo_len, hi_len;
     uint32_t ok;            // header and filter decoded (lsm_sst_meta.stage not 1 or 2)
-    uint32_t pad;
+    uint32_t k;             // filter k, capped so a probe always ends
+    uint64_t lo_at, hi_at;  // image offsets of the min / max key bytes
+    uint64_t words_at;      // image offset of the first filter word
+    uint64_t m, mr, nbits;  // filter m, its Barrett reciprocal, stored bit count
 };
 
 __device__ __forceinline__ uint32_t be_word_at(const uint8_t *p, uint64_t len, uint32_t j) {
@@ -1111,15 +1118,35 @@ __device__ __forceinline__ int bound_cmp(const uint32_t bw[4], uint64_t blen, co
     return go_cmp(bp + 16, blen - 16, kp + 16, klen - 16);
 }
 
-__global__ __launch_bounds__(256) void may_contain_kernel(const uint8_t *img,
-                                                          const uint64_t *file_off,
-                                                          const lsm_sst_meta *meta,
-                                                          uint32_t nfile, const uint8_t *keys,
-                                                          const uint64_t *koff, uint64_t nkeys,
-                                                          uint8_t *hit) {
+// Lexicographic compare of two 16-byte big-endian prefixes: -1, 0, 1 (branch-free).
+__device__ __forceinline__ int prefix_cmp(const uint32_t a[4], const uint32_t b[4]) {
+    const uint64_t a0 = (uint64_t)a[0] << 32 | a[1], a1 = (uint64_t)a[2] << 32 | a[3];
+    const uint64_t b0 = (uint64_t)b[0] << 32 | b[1], b1 = (uint64_t)b[2] << 32 | b[3];
+    const int lt = (a0 < b0) | ((a0 == b0) & (a1 < b1));
+    const int gt = (a0 > b0) | ((a0 == b0) & (a1 > b1));
+    return gt - lt;
+}
+
+// bound_cmp with the common case (prefixes differ) branch-free
+__device__ __forceinline__ int bound_cmp_fast(const uint32_t bw[4], uint64_t blen, const uint8_t *bp,
+                                              const uint32_t kw[4], uint64_t klen, const uint8_t *kp) {
+    const int c = prefix_cmp(bw, kw);
+    if (c != 0) return c;
+    return bound_cmp(bw, blen, bp, kw, klen, kp);
+}
+
+__global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *img,
+                                                                 const uint64_t *file_off,
+                                                                 const lsm_sst_meta *meta,
+                                                                 uint32_t nfile, const uint8_t *keys,
+                                                                 const uint64_t *koff, uint64_t nkeys,
+                                                                 uint8_t *hit) {
     __shared__ McFile tile[kMcTile];
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t sout[kMcThreads * kMcRow];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kMcThreads;
+    const uint64_t i = i0 + threadIdx.x;
     const bool act = i < nkeys;
+    const uint32_t rows = nkeys - i0 < kMcThreads ? (uint32_t)(nkeys - i0) : kMcThreads;
     uint64_t k0 = 0, kl = 0;
     uint64_t h[4] = {0, 0, 0, 0};
     uint32_t kw[4] = {0, 0, 0, 0};
@@ -1132,10 +1159,12 @@ __global__ __launch_bounds__(256) void may_contain_kernel(const uint8_t *img,
     }
     const uint8_t *kp = keys + k0;
     for (uint32_t f0 = 0; f0 < nfile; f0 += kMcTile) {
+        const uint32_t nt = nfile - f0 < kMcTile ? nfile - f0 : kMcTile;
         __syncthreads();
-        for (uint32_t t = threadIdx.x; t < kMcTile && f0 + t < nfile; t += blockDim.x) {
+        for (uint32_t t = threadIdx.x; t < nt; t += kMcThreads) {
             const lsm_sst_meta &M = meta[f0 + t];
-            const uint8_t *base = img + file_off[f0 + t];
+            const uint64_t fo = file_off[f0 + t];
+            const uint8_t *base = img + fo;
             McFile F;
             F.ok = M.stage != 1 && M.stage != 2;
             F.lo_len = (uint32_t)M.min_key_len;
@@ -1144,41 +1173,91 @@ __global__ __launch_bounds__(256) void may_contain_kernel(const uint8_t *img,
                 F.lo[j] = F.ok ? be_word_at(base + M.min_key_off, M.min_key_len, j) : 0;
                 F.hi[j] = F.ok ? be_word_at(base + M.max_key_off, M.max_key_len, j) : 0;
             }
-            F.pad = 0;
+            F.lo_at = fo + M.min_key_off;
+            F.hi_at = fo + M.max_key_off;
+            F.words_at = fo + M.filter_words_off;
+            // k from the file (no max(1, k) on a decoded filter); a corrupted
+            // k is capped so a probe always ends
+            F.k = M.filter_k < 4096 ? (uint32_t)M.filter_k : 4096;
+            F.m = M.filter_m;
+            F.mr = M.filter_m ? ~0ull / M.filter_m : 0;
+            F.nbits = M.filter_nbits;
             tile[t] = F;
         }
-        __syncthreads();
-        if (!act) continue;
-        const uint32_t nt = nfile - f0 < kMcTile ? nfile - f0 : kMcTile;
+        // a tile of decoded files in key order with disjoint ranges (level >= 1
+        // files) holds a key in at most one file: the last whose MinKey <= key
+        bool sorted = true;
+        if (threadIdx.x < nt) {
+            const McFile &A = tile[threadIdx.x];
+            sorted = A.ok != 0;
+            if (sorted && threadIdx.x + 1 < nt) {
+                const McFile &B = tile[threadIdx.x + 1];
+                sorted = B.ok && bound_cmp_fast(A.hi, A.hi_len, img + A.hi_at, B.lo, B.lo_len,
+                                                img + B.lo_at) < 0;
+            }
+        }
+        sorted = __syncthreads_and(sorted);
+        uint32_t cand_lo = 0, cand_hi = nt;  // files to test: [cand_lo, cand_hi)
+        if (sorted && act) {
+            uint32_t lo = 0, hi = nt;  // first t with MinKey > key
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) / 2;
+                const McFile &F = tile[mid];
+                if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0) lo = mid + 1;
+                else hi = mid;
+            }
+            cand_lo = lo ? lo - 1 : 0;
+            cand_hi = lo;
+        }
+        uint32_t pack = 0;
         for (uint32_t t = 0; t < nt; t++) {
-            const McFile &F = tile[t];
-            uint8_t r = 0;
-            if (F.ok) {
-                const lsm_sst_meta &M = meta[f0 + t];
-                const uint8_t *base = img + file_off[f0 + t];
+            uint32_t r = 0;
+            if (act && t >= cand_lo && t < cand_hi && tile[t].ok) {
+                const McFile &F = tile[t];
                 // sstable.go:301: MinKey > key || MaxKey < key -> false
-                if (bound_cmp(F.lo, F.lo_len, base + M.min_key_off, kw, kl, kp) <= 0 &&
-                    bound_cmp(F.hi, F.hi_len, base + M.max_key_off, kw, kl, kp) >= 0) {
-                    const uint64_t m = M.filter_m;
-                    // k from the file (no max(1, k) on a decoded filter); a
-                    // corrupted k is capped so a probe always ends
-                    const uint64_t k = M.filter_k < 4096 ? M.filter_k : 4096;
+                if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0 &&
+                    bound_cmp_fast(F.hi, F.hi_len, img + F.hi_at, kw, kl, kp) >= 0) {
+                    const uint64_t m = F.m;
                     r = m != 0;  // m == 0: Go's location() divides by zero
-                    const uint64_t mr = m ? ~0ull / m : 0;
-                    for (uint64_t j = 0; j < k && r; j++) {
-                        const uint64_t x = location(h[0], h[1], h[2], h[3], (uint32_t)j);
-                        const uint64_t p = m < (1ull << 63) ? mod_barrett(x, m, mr) : x % m;
-                        if (p >= M.filter_nbits) {
-                            r = 0;
-                        } else {
-                            const uint8_t byte =
-                                base[M.filter_words_off + 8 * (p >> 6) + 7 - ((p & 63) >> 3)];
-                            r = (byte >> (p & 7)) & 1;
+                    // Test's answer is the AND of all k bits (its early exit
+                    // changes nothing): eight loads in flight at a time
+                    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 8) {
+                        uint32_t bits = 1;
+#pragma unroll
+                        for (uint32_t u = 0; u < 8; u++) {
+                            const uint32_t j = j0 + u;
+                            if (j < F.k && r) {
+                                const uint64_t x = location(h[0], h[1], h[2], h[3], j);
+                                const uint64_t p = m < (1ull << 63) ? mod_barrett(x, m, F.mr) : x % m;
+                                bits &= p < F.nbits
+                                            ? (uint32_t)(img[F.words_at + 8 * (p >> 6) + 7 - ((p & 63) >> 3)] >> (p & 7)) & 1
+                                            : 0u;
+                            }
                         }
+                        r &= bits;
                     }
                 }
             }
-            hit[i * nfile + f0 + t] = r;
+            pack |= r << (8 * (t & 3));
+            if ((t & 3) == 3 || t + 1 == nt) {
+                sout[threadIdx.x * kMcRow + t / 4] = pack;
+                pack = 0;
+            }
+        }
+        __syncthreads();
+        // the rows x nt sub-block of hit, coalesced
+        if ((nfile & 3) == 0) {  // every row segment starts 4-aligned (nt is a multiple of 4)
+            const uint32_t nd = nt / 4;
+            for (uint32_t x = threadIdx.x; x < rows * nd; x += kMcThreads) {
+                const uint32_t rr = x / nd, c = x % nd;
+                *reinterpret_cast<uint32_t *>(hit + (i0 + rr) * nfile + f0 + 4 * c) =
+                    sout[rr * kMcRow + c];
+            }
+        } else {
+            for (uint32_t x = threadIdx.x; x < rows * nt; x += kMcThreads) {
+                const uint32_t rr = x / nt, c = x % nt;
+                hit[(i0 + rr) * nfile + f0 + c] = (uint8_t)(sout[rr * kMcRow + c / 4] >> (8 * (c & 3)));
+            }
         }
     }
 }
@@ -1442,9 +1521,9 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
     if (!ctx) return LSM_EINVAL;
     if (nkeys == 0 || nfile == 0) return 0;
     if (!d_img || !d_file_off || !d_meta || !d_keys || !d_koff || !d_hit) return LSM_EINVAL;
-    const uint64_t grid = (nkeys + 255) / 256;
+    const uint64_t grid = (nkeys + kMcThreads - 1) / kMcThreads;
     if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
-    hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(256), 0,
+    hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(kMcThreads), 0,
                        static_cast<hipStream_t>(stream), d_img, d_file_off, d_meta, nfile, d_keys,
                        d_koff, nkeys, d_hit);
     LSM_HIP_CHECK(hipGetLastError());

@@ -29,16 +29,30 @@ def build(keys, m, k):
     return img
 
 
+_DECODED = {}
+
+
+def _file(img):
+    """(meta, min key, max key, filter, stored bits) of an image, decoded once."""
+    kid = (id(img), img.size)
+    if kid not in _DECODED:
+        rc, meta, *_ = ora.sst_decode(img)
+        mn = img[meta.min_key_off:meta.min_key_off + meta.min_key_len].tobytes()
+        mx = img[meta.max_key_off:meta.max_key_off + meta.max_key_len].tobytes()
+        f = nbits = None
+        if meta.stage not in (1, 2):
+            hdr = 8 + meta.min_key_len + meta.max_key_len
+            f, nbits, _ = ora.Bloom.decode(img[hdr:])
+        _DECODED[kid] = (img, meta, mn, mx, f, nbits)  # img kept alive: id() stays unique
+    return _DECODED[kid][1:]
+
+
 def expected(img, key):
-    rc, meta, *_ = ora.sst_decode(img)
+    meta, mn, mx, f, nbits = _file(img)
     if meta.stage in (1, 2):
         return 0
-    mn = img[meta.min_key_off:meta.min_key_off + meta.min_key_len].tobytes()
-    mx = img[meta.max_key_off:meta.max_key_off + meta.max_key_len].tobytes()
     if mn > key or mx < key:
         return 0
-    hdr = 8 + meta.min_key_len + meta.max_key_len
-    f, nbits, _ = ora.Bloom.decode(img[hdr:])
     if meta.filter_m == 0:
         return 0
     if meta.filter_k == 0:
@@ -66,6 +80,12 @@ def test_may_contain_vs_oracle(ctx):
     probes += [b"user%06d" % int(x) for x in rng.integers(0, 7000, 600)]
     probes += [b"", b"user", b"user000000", b"user000000\x00", b"user005999", b"zzzz", b"a", b"q",
                b"user%06d" % 999 + b"x" * 40]
+    # nfile = 10 (byte write-out) and 8 (dword write-out)
+    for subset in (images, images[:8]):
+        check(ctx, rng, subset, probes)
+
+
+def check(ctx, rng, images, probes):
     # images at odd offsets in one buffer
     offs, pos, parts = [], 0, []
     for im in images:
@@ -98,3 +118,33 @@ def test_may_contain_vs_oracle(ctx):
         for i, key in enumerate(probes):
             if key in held:
                 assert hit[i, f] == 1
+
+
+def test_may_contain_many_files(ctx):
+    """More than one 128-file tile, nfile % 4 != 0 and == 0, keys shared by
+    several overlapping files."""
+    rng = np.random.default_rng(33)
+    images = []
+    for f in range(136):
+        lo = int(rng.integers(0, 5000))
+        keys = sorted({b"k%05d" % int(x) for x in rng.integers(lo, lo + 400, 40)})
+        images.append(build(keys, m=512, k=2))
+    probes = [b"k%05d" % int(x) for x in rng.integers(0, 5500, 300)] + [b"", b"z"]
+    for subset in (images, images[:135]):
+        check(ctx, rng, subset, probes)
+
+
+def test_may_contain_sorted_disjoint_files(ctx):
+    """Level >= 1 shape: files in key order with disjoint ranges (the tile
+    binary search), over two tiles; probes at the exact bounds, in the gaps
+    between files, before the first and after the last file."""
+    rng = np.random.default_rng(44)
+    images, bounds = [], []
+    for f in range(70):
+        keys = sorted({b"s%06d" % (f * 1000 + int(x)) + b"x" * int(x % 3) for x in rng.integers(0, 900, 30)})
+        images.append(build(keys, m=2048, k=4))
+        bounds += [keys[0], keys[-1]]
+    probes = bounds + [b"s%06d" % int(x) for x in rng.integers(0, 72000, 400)]
+    probes += [b"", b"r", b"s", b"t", b"s%06d" % 69950 + b"\x00"]
+    check(ctx, rng, images, probes)
+    check(ctx, rng, images[:64], probes)
