@@ -2116,6 +2116,208 @@ __global__ __launch_bounds__(64) void wal_seg_kernel(WalArgs a) {
     if (lane == 0) T = WalSeg{g, g + endp, nr, st};
 }
 
+// Lane-parallel form of wal_seg_kernel (the default).  WAL records are small
+// (~40 B for go-lsm's benchmark) and vary in shape, so one wave chasing a
+// 16 KiB segment spends its time in ~400 serial exact steps.  Here the
+// segment [g, E) (g the segment's guess as above, E its end) is split into
+// 64 shares, one per lane:
+//   1. lane 0 starts at g; lane l > 0 guesses its first record start (the
+//      first position of its share from which two plausible records follow)
+//      and chases both field phases (the guess, and the guess read as a value
+//      length), each to the first record starting past its share;
+//   2. the wave stitches the shares in order from g: the chain that starts
+//      where the previous share ended is the serial chase's; if neither
+//      does, that share is chased again from the true position;
+//   3. each lane writes the descriptors of its accepted chain.
+// The result is the serial chase of [g, E) for any input (exact check order
+// of kv.go:77-115); the segment is read from an LDS copy (plus 4 KiB past
+// its end) and past that through a range-checked buffer resource.
+constexpr uint32_t kWalStage = kWalSeg + 4096;
+
+struct WalLog {
+    rsrc_t r;       // the log's bytes, offsets relative to the aligned base
+    uint32_t h;     // log start inside the base
+    uint32_t len;
+    uint32_t s0;    // LDS copy covers resource offsets [s0, s0 + kWalStage)
+    const uint32_t *lds;
+    __device__ __forceinline__ uint32_t rd32(uint32_t x) const {  // bytes [x, x+4) of the log
+        const uint32_t o = h + x;
+        if (o >= s0 && o + 8 <= s0 + kWalStage) {
+            const uint32_t q = o - s0;
+            return funnel(lds[q >> 2], lds[(q >> 2) + 1], q);
+        }
+        const uint32_t oa = o & ~3u;
+        return funnel(ld_b32(r, oa), ld_b32(r, oa + 4), o);
+    }
+    // exact KV record at p < len (kv.go:77-115 / ora_decode_block order)
+    __device__ __forceinline__ int32_t record(uint32_t p, uint32_t &kl, uint32_t &vl) const {
+        const uint32_t rem = len - p;
+        if (rem < 4) return LSM_ST_TRUNC_LEN_PREFIX;
+        kl = rd32(p);
+        if (kl > kKeyCap) return LSM_ST_KEY_TOO_LONG;
+        if (rem - 4 < kl) return LSM_ST_TRUNC_KEY;
+        const uint32_t rem2 = rem - 4 - kl;
+        if (rem2 < 4) return LSM_ST_TRUNC_VLEN;
+        vl = rd32(p + 4 + kl);
+        if (vl > kValCap) return LSM_ST_VAL_TOO_LONG;
+        if (rem2 - 4 < vl) return LSM_ST_TRUNC_VAL;
+        return LSM_OK;
+    }
+    // chase from p while records start before `end`: count, stop position, status
+    __device__ __forceinline__ void chase(uint32_t p, uint32_t end, uint32_t &cnt, uint32_t &exitp,
+                                          int32_t &st) const {
+        cnt = 0;
+        st = LSM_OK;
+        while (p < end && p < len) {
+            uint32_t kl = 0, vl = 0;
+            st = record(p, kl, vl);
+            if (st != LSM_OK) break;
+            cnt++;
+            p += 8 + kl + vl;
+        }
+        exitp = p;
+    }
+    // plausible record start (as the segment guess: two records or the log's end)
+    __device__ __forceinline__ bool plausible(uint32_t q) const {
+        uint32_t seen = 0;
+        for (int rec = 0; rec < 2; rec++) {
+            if (q == len) return seen >= 1;
+            if ((uint64_t)q + 8 > len) return false;
+            const uint32_t k = rd32(q);
+            if (k > 1024 || (uint64_t)q + 8 + k > len) return false;
+            const uint32_t v = rd32(q + 4 + k);
+            if (v > (1u << 20) || (uint64_t)q + 8 + k + v > len) return false;
+            q += 8 + k + v;
+            seen++;
+        }
+        return true;
+    }
+};
+
+// One wave serves both phases of a segment: the shares' chains do not depend
+// on the segment's entry, only lane 0's does, so they are chased once and
+// stitched twice (from g and from g read as a value length).
+template <bool STAGE>
+__global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE ? kWalStage / 4 + 4 : 4];
+    const uint32_t s = blockIdx.x, w = blockIdx.y, lane = lane_id();
+    const uint32_t len = uni(a.wal_len[w]);
+    const uint64_t off = uni64(a.wal_off[w]);
+    const uint64_t q0 = ((uint64_t)w * a.segs + s) * 2;
+    const uint32_t start = s * kWalSeg;
+    if (start >= len || len > a.max_len) {
+        if (lane == 0) a.seg[q0] = a.seg[q0 + 1] = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+        return;
+    }
+    WalLog L;
+    const uint64_t base = off & ~(uint64_t)15;
+    L.h = (uint32_t)(off - base);
+    L.len = len;
+    L.r = make_rsrc(a.wal + base, (L.h + len + 15) & ~15u);
+    L.s0 = STAGE ? (L.h + start) & ~15u : 0xFFFFFFF0u;
+    L.lds = stage;
+    if (STAGE) {
+        for (uint32_t c = 0; c < kWalStage / 16; c += kWave) {  // the segment + 4 KiB
+            const uint32_t o = L.s0 + 16 * (c + lane);
+            if (c + lane < kWalStage / 16)
+                *reinterpret_cast<u32x4 *>(&stage[4 * (c + lane)]) = ld_b128(L.r, o);
+        }
+        __syncthreads();
+    }
+    uint32_t g = start, g1 = 0xFFFFFFFFu;  // entries of phase 0 and phase 1
+    if (s > 0) {  // the segment's guess: the first plausible start in its first 2 KiB
+        g = 0xFFFFFFFFu;
+        const uint32_t span = len - start < 2048 ? len - start : 2048;
+        for (uint32_t t0 = 0; t0 < span && g == 0xFFFFFFFFu; t0 += kWave) {
+            const uint32_t p = start + t0 + lane;
+            const uint64_t m = __ballot(t0 + lane < span && L.plausible(p));
+            if (m) g = start + t0 + (uint32_t)__builtin_ctzll(m);
+        }
+        if (g == 0xFFFFFFFFu) g = start;
+        g = uni(g);
+        const uint32_t v = (uint64_t)g + 4 <= len ? L.rd32(g) : 0xFFFFFFFFu;
+        g1 = uni((uint64_t)g + 4 + v <= len ? g + 4 + v : len);
+    }
+    const uint32_t E = start + kWalSeg < len ? start + kWalSeg : len;
+    // 1. shares of [start, E): lane 0's chains are the two entries themselves
+    const uint32_t W = (E - start + kWave - 1) / kWave;
+    const uint32_t ss = start + lane * W < E ? start + lane * W : E;
+    const uint32_t se = ss + W < E ? ss + W : E;
+    uint32_t e0 = 0xFFFFFFFFu, e1 = 0xFFFFFFFFu, c0 = 0, c1 = 0, x0 = 0, x1 = 0;
+    int32_t st0 = LSM_OK, st1 = LSM_OK;
+    if (lane > 0 && ss < se) {
+        for (uint32_t p = ss; p < se; p++)
+            if (L.plausible(p)) { e0 = p; break; }
+        if (e0 != 0xFFFFFFFFu && (uint64_t)e0 + 4 <= len) {
+            const uint32_t v = L.rd32(e0);
+            if ((uint64_t)e0 + 4 + v <= len) e1 = e0 + 4 + v;
+        }
+    }
+    if (e0 != 0xFFFFFFFFu && e0 < se) L.chase(e0, se, c0, x0, st0);
+    if (e1 != 0xFFFFFFFFu && e1 < se) L.chase(e1, se, c1, x1, st1);
+    // 2. + 3. per phase: stitch from the entry, then write the accepted chains
+    for (uint32_t ph = 0; ph < 2; ph++) {
+        const uint64_t q = q0 + ph;
+        const uint32_t gp = ph ? g1 : g;
+        if (ph == 1 && s == 0) {  // segment 0 starts at 0
+            if (lane == 0) a.seg[q] = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+            break;
+        }
+        if (gp >= E) {
+            if (lane == 0) a.seg[q] = WalSeg{gp, gp, 0, 0};
+            continue;
+        }
+        uint32_t e = gp, acc_entry = 0xFFFFFFFFu, acc_cnt = 0, total = 0;
+        int32_t status = LSM_OK;
+        bool dead = false;
+        for (uint32_t l = 0; l < kWave; l++) {
+            const uint32_t sl = uni(__builtin_amdgcn_readlane(ss, l));
+            const uint32_t el = uni(__builtin_amdgcn_readlane(se, l));
+            if (dead || sl >= el || e >= el) continue;
+            uint32_t cnt, ex;
+            int32_t st;
+            if (l > 0 && uni(__builtin_amdgcn_readlane(e0, l)) == e) {
+                cnt = uni(__builtin_amdgcn_readlane(c0, l));
+                ex = uni(__builtin_amdgcn_readlane(x0, l));
+                st = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)st0, l));
+            } else if (l > 0 && uni(__builtin_amdgcn_readlane(e1, l)) == e) {
+                cnt = uni(__builtin_amdgcn_readlane(c1, l));
+                ex = uni(__builtin_amdgcn_readlane(x1, l));
+                st = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)st1, l));
+            } else {  // the entry share, or neither guess on the chain: chase from e
+                L.chase(e, el, cnt, ex, st);
+                cnt = uni(cnt);
+                ex = uni(ex);
+                st = (int32_t)uni((uint32_t)st);
+            }
+            if (lane == l) {
+                acc_entry = e;
+                acc_cnt = cnt;
+            }
+            total += cnt;
+            e = ex;
+            if (st != LSM_OK) {
+                status = st;
+                dead = true;
+            }
+        }
+        uint32_t tot;
+        const uint32_t pre = wave_excl_scan(acc_cnt, &tot);
+        if (acc_cnt) {
+            u32x4 *dst = a.scratch + q * kWalSegSlots + pre;
+            uint32_t p = acc_entry;
+            for (uint32_t i = 0; i < acc_cnt; i++) {
+                uint32_t kl = 0, vl = 0;
+                L.record(p, kl, vl);
+                const uint64_t ro = off + p;
+                dst[i] = u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), kl, vl};
+                p += 8 + kl + vl;
+            }
+        }
+        if (lane == 0) a.seg[q] = WalSeg{gp, e, total, status};
+    }
+}
+
 __global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
     const uint32_t w = blockIdx.x, lane = lane_id();
@@ -2392,7 +2594,13 @@ extern "C" int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t
     a.seg = reinterpret_cast<WalSeg *>(ws + n * 2 * kWalSegSlots * 16);
     a.fin = reinterpret_cast<uint32_t *>(ws + n * 2 * (kWalSegSlots * 16 + sizeof(WalSeg)));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(wal_seg_kernel, dim3(2 * a.segs, nwal), dim3(kWave), 0, s, a);
+    static const char *wk = getenv("LSM_WAL_KERNEL");
+    if (wk && !strcmp(wk, "serial"))
+        hipLaunchKernelGGL(wal_seg_kernel, dim3(2 * a.segs, nwal), dim3(kWave), 0, s, a);
+    else if (wk && !strcmp(wk, "lanes"))  // shares read through the caches, no LDS copy
+        hipLaunchKernelGGL(wal_seg_lanes_kernel<false>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL(wal_seg_lanes_kernel<true>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_stitch_kernel, dim3(nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_compact_kernel, dim3(a.segs, nwal), dim3(256), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
