@@ -823,15 +823,26 @@ std::vector<std::vector<kv::KeyValuePair>> DecodeFiles(const std::vector<Bytes> 
 
 std::vector<Bytes> BuildImages(const std::vector<kv::KeyValuePair> &sorted, uint64_t threshold,
                                uint64_t m, uint64_t k) {
+    std::vector<uint64_t> koff(1, 0), voff(1, 0);
+    for (auto &p : sorted) {
+        koff.push_back(koff.back() + p.key.size());
+        voff.push_back(voff.back() + p.value.size());
+    }
+    const uint64_t n = sorted.size();
+    std::vector<uint64_t> fs(n + 2);
+    const uint64_t nf = lsm_segment_files_host(koff.data(), voff.data(), n, threshold, fs.data());
+    fs.resize(nf + 1);
+    return BuildImagesAt(sorted, fs, m, k);
+}
+
+std::vector<Bytes> BuildImagesAt(const std::vector<kv::KeyValuePair> &sorted,
+                                 const std::vector<uint64_t> &fs, uint64_t m, uint64_t k) {
     Device &d = Device::ThisThread();
     Bytes keys, vals;
     std::vector<uint64_t> koff, voff;
     csr(sorted, [](const kv::KeyValuePair &p) -> const std::string & { return p.key; }, &keys, &koff);
     csr(sorted, [](const kv::KeyValuePair &p) -> const kv::Value & { return p.value; }, &vals, &voff);
-    const uint64_t n = sorted.size();
-    std::vector<uint64_t> fs(n + 2);
-    const uint64_t nf = lsm_segment_files_host(koff.data(), voff.data(), n, threshold, fs.data());
-    fs.resize(nf + 1);
+    const uint64_t nf = fs.empty() ? 0 : fs.size() - 1;
     std::vector<uint64_t> fo(nf), sz(nf);
     uint64_t total = 0, maxr = 0;
     for (uint64_t f = 0; f < nf; f++) {
@@ -868,6 +879,65 @@ std::vector<Bytes> BuildImages(const std::vector<kv::KeyValuePair> &sorted, uint
     }
     d.Sync();
     return out;
+}
+
+std::vector<SSTable> CompactAndMergeKVs(const std::vector<kv::KeyValuePair> &kvs, int level) {
+    std::vector<SSTable> results;
+    const size_t n = kvs.size();
+    if (n == 0) return results;  // no builder.size: no table (merge.go:88-91)
+    Device &d = Device::ThisThread();
+    // the pairs as views: [4 bytes][key] [4 bytes][value], the IDX / V
+    // descriptor convention (bytes at rec_off + 4)
+    size_t total = 0;
+    for (auto &p : kvs) total += 8 + p.key.size() + p.value.size();
+    uint8_t *h = (uint8_t *)d.Host(0, pad16(total));
+    std::vector<lsm_rec_desc> kd(n), vd(n);
+    size_t at = 0;
+    for (size_t i = 0; i < n; i++) {
+        const kv::KeyValuePair &p = kvs[i];
+        kd[i] = lsm_rec_desc{at, (uint32_t)p.key.size(), 0};
+        std::memset(h + at, 0, 4);
+        std::memcpy(h + at + 4, p.key.data(), p.key.size());
+        at += 4 + p.key.size();
+        vd[i] = lsm_rec_desc{at, 0, (uint32_t)p.value.size()};
+        std::memset(h + at, 0, 4);
+        if (!p.value.empty()) std::memcpy(h + at + 4, p.value.data(), p.value.size());
+        at += 4 + p.value.size();
+    }
+    std::memset(h + at, 0, pad16(total) - at);
+    void *d_buf = d.Dev(0, pad16(total));
+    void *d_kd = d.Dev(1, n * sizeof(lsm_rec_desc));
+    void *d_vd = d.Dev(2, n * sizeof(lsm_rec_desc));
+    void *d_out = d.Dev(3, n * 4);
+    void *d_fs = d.Dev(4, (n + 1) * 8);
+    const size_t ws = lsm_merge_kvs_workspace_bytes(n);
+    void *d_ws = d.Dev(5, ws);
+    d.H2D(d_buf, h, pad16(total));
+    d.H2D(d_kd, kd.data(), n * sizeof(lsm_rec_desc));
+    d.H2D(d_vd, vd.data(), n * sizeof(lsm_rec_desc));
+    uint64_t counts[2] = {0, 0};
+    check(lsm_merge_kvs(d.ctx(), (const uint8_t *)d_buf, (const lsm_rec_desc *)d_kd,
+                        (const lsm_rec_desc *)d_vd, n, level, kMaxSSTableSize, (uint32_t *)d_out,
+                        (uint64_t *)d_fs, counts, d_ws, ws, d.stream()),
+          "lsm_merge_kvs");
+    std::vector<uint32_t> out(counts[0]);
+    std::vector<uint64_t> fs(counts[1] + 1);
+    if (counts[0]) d.D2H(out.data(), d_out, counts[0] * 4);
+    d.D2H(fs.data(), d_fs, fs.size() * 8);
+    d.Sync();
+    std::vector<kv::KeyValuePair> written;
+    written.reserve(out.size());
+    for (uint32_t i : out) written.push_back(kvs[i]);
+    const std::vector<Bytes> images = BuildImagesAt(written, fs);
+    for (const Bytes &img : images) {
+        SSTable t;
+        Error e = t.DecodeImage(img);
+        if (!e) e = t.DecodeDataBlock(img);
+        if (e) throw std::runtime_error("CompactAndMergeKVs: built image does not decode: " + e.Message());
+        t.level = level;
+        results.push_back(std::move(t));
+    }
+    return results;
 }
 
 }  // namespace sstable

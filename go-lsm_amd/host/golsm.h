@@ -217,6 +217,7 @@ class SSTable {
     kv::Value GetValueByOffset(int64_t offset, Error *err);           // sstable.go:271-296
     bool MayContain(const kv::Key &key);                                // sstable.go:300-305
     const std::string &FilePath() const { return path_; }
+    int level = 0;  // sstable.go:46 (set by NewSSTableWithLevel / CompactAndMergeKVs)
 
   private:
     std::string path_;
@@ -255,6 +256,17 @@ std::vector<std::vector<kv::KeyValuePair>> DecodeFiles(const std::vector<Bytes> 
 // threshold 0 = one file (memtable flush), kMaxSSTableSize = CompactAndMergeKVs.
 std::vector<Bytes> BuildImages(const std::vector<kv::KeyValuePair> &sorted, uint64_t threshold,
                                uint64_t m = bloom::kDefaultM, uint64_t k = bloom::kDefaultK);
+// The same for given file boundaries: file f = sorted[starts[f], starts[f+1]).
+std::vector<Bytes> BuildImagesAt(const std::vector<kv::KeyValuePair> &sorted,
+                                 const std::vector<uint64_t> &starts,
+                                 uint64_t m = bloom::kDefaultM, uint64_t k = bloom::kDefaultK);
+// CompactAndMergeKVs (merge.go:42-94) over lsm_merge_kvs: pairs in key order,
+// a key equal to the last written one skipped, tombstones dropped at level 6,
+// a new table at every 2 MiB of EstimateSize, the last written key forgotten
+// at each flush.  Pairs with equal keys leave in input order (merge.go:41's
+// contract; container/heap's own order is unspecified).  The
+// tables are returned as decoded from their built images, level set.
+std::vector<SSTable> CompactAndMergeKVs(const std::vector<kv::KeyValuePair> &kvs, int level);
 
 }  // namespace sstable
 }  // namespace golsm

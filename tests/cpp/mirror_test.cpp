@@ -557,6 +557,72 @@ static void TestDecodeFilesVsSingleFile() {  // lsm_decode_sst batch == per-file
     }
 }
 
+static void TestCompactAndMergeKVs() {  // merge_test.go:12-60 + the oracle (ORA_TIE_INPUT)
+    {
+        std::vector<kv::KeyValuePair> in = {{"alpha", kv::Value{'A'}},
+                                            {"beta", kv::Value{'B'}},
+                                            {"beta", kv::Value{'B', '2'}},
+                                            {"carrot", kv::Value{'C'}},
+                                            {"delta", kv::Value{'D'}}};
+        auto sst = sstable::CompactAndMergeKVs(in, 1);
+        CHECK(sst.size() == 1);
+        if (sst.size() == 1) {
+            CHECK(sst[0].level == 1);
+            CHECK(sst[0].DataBlock.Entries.size() == 4);
+            std::vector<std::string> keys;
+            for (auto &e : sst[0].IndexBlock.Indexes) keys.push_back(e.Key);
+            CHECK((keys == std::vector<std::string>{"alpha", "beta", "carrot", "delta"}));
+            CHECK(sst[0].DataBlock.Entries.size() > 1 && sst[0].DataBlock.Entries[1] == kv::Value{'B'});
+            CHECK(sst[0].MayContain("alpha") && sst[0].MayContain("delta"));
+            CHECK(!sst[0].MayContain("nonexistent") && !sst[0].MayContain("deletedKey"));
+        }
+        CHECK(sstable::CompactAndMergeKVs({}, 1).empty());
+    }
+    // many pairs, duplicates, tombstones at the last level, several tables
+    std::mt19937_64 rng(41);
+    const std::string tomb = "\xEF\xBD\x9E" "DELETED" "\xEF\xBD\x9E";
+    std::vector<kv::KeyValuePair> in;
+    for (int i = 0; i < 40000; i++) {  // ~22k distinct keys, ~3 MB: two or more tables
+        std::string k = "key" + std::to_string(rng() % 30000);
+        kv::Value v;
+        if (rng() % 10 == 0) v.assign(tomb.begin(), tomb.end());
+        else v.assign(60 + rng() % 120, (uint8_t)('a' + rng() % 26));
+        in.push_back({k, v});
+    }
+    for (int level : {1, 6}) {
+        auto sst = sstable::CompactAndMergeKVs(in, level);
+        // the oracle over the same pairs
+        std::string blob;
+        std::vector<uint64_t> koff, voff;
+        std::vector<uint32_t> klen, vlen;
+        for (auto &p : in) {
+            koff.push_back(blob.size()); klen.push_back((uint32_t)p.key.size()); blob += p.key;
+            voff.push_back(blob.size()); vlen.push_back((uint32_t)p.value.size());
+            blob.append(p.value.begin(), p.value.end());
+        }
+        std::vector<uint32_t> out(in.size());
+        std::vector<uint64_t> starts(in.size() + 2);
+        uint64_t nf = 0;
+        const uint64_t cnt = ora_merge_kvs((const uint8_t *)blob.data(), koff.data(), klen.data(),
+                                           voff.data(), vlen.data(), in.size(), level,
+                                           sstable::kMaxSSTableSize, ORA_TIE_INPUT, out.data(),
+                                           starts.data(), &nf);
+        CHECK(sst.size() == nf);
+        bool same = sst.size() == nf;
+        for (uint64_t f = 0; same && f < nf; f++) {
+            const auto &E = sst[f].DataBlock.Entries;
+            const auto &I = sst[f].IndexBlock.Indexes;
+            same = E.size() == starts[f + 1] - starts[f] && I.size() == E.size() && sst[f].level == level;
+            for (uint64_t r = 0; same && r < E.size(); r++) {
+                const auto &want = in[out[starts[f] + r]];
+                same = I[r].Key == want.key && E[r] == want.value;
+            }
+        }
+        CHECK(same);
+        CHECK(cnt > 0 && nf >= 2);
+    }
+}
+
 int main(int argc, char **argv) {
     const std::pair<const char *, std::function<void()>> tests[] = {
         {"TestDataBlock_EncodeDecode", TestDataBlock_EncodeDecode},
@@ -578,6 +644,7 @@ int main(int argc, char **argv) {
         {"TestBuildImagesVsOracle", TestBuildImagesVsOracle},
         {"TestDecodeDataBlocksVsOracle", TestDecodeDataBlocksVsOracle},
         {"TestDecodeFilesVsSingleFile", TestDecodeFilesVsSingleFile},
+        {"TestCompactAndMergeKVs", TestCompactAndMergeKVs},
     };
     int failed_cases = 0;
     for (auto &t : tests) {
