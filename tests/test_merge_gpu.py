@@ -208,3 +208,30 @@ def test_sst_pairs_join(ctx):
     assert got == want
     counts = [0 if i == 1 else len(images[i][1]) for i in range(5)]
     assert list(prefix.cpu().numpy()) == list(np.concatenate([[0], np.cumsum(counts)]))
+
+
+def test_full_size_compaction_merge(ctx):
+    """The compact bench's workload at full size (216 images: 8 level-0 update
+    flushes + 208 level-1 files, 3.43M pairs) through lsm_decode_sst ->
+    lsm_sst_pairs -> lsm_merge_kvs, against ora_merge_kvs on the same views."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench_compact import build_images, level0_runs
+    from lsmgpu import synth
+    n1 = 100_000 * 33
+    img, file_off, file_size = build_images(ctx, level0_runs(n1, 0, 0) + [synth.kv_stream(n1)])
+    r = lsmgpu.alloc_sst_decode(ctx, file_off, file_size, int(img.numel()))
+    lsmgpu.decode_sst_into(ctx, img, r)
+    kd, vd, prefix = lsmgpu.sst_pairs(ctx, r)
+    for level in (1, 6):
+        m = lsmgpu.merge_kvs(ctx, img, kd, vd, level=level)
+        torch.cuda.synchronize()
+        got = m.out[:m.nout].cpu().numpy().view(np.uint32)
+        starts = m.file_start[:m.nfiles + 1].cpu().numpy().view(np.uint64)
+        k = kd.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+        v = vd.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+        want, wstarts = ora.merge_kvs(img.cpu().numpy(), k["rec_off"] + 4, k["key_len"],
+                                      v["rec_off"] + 4, v["val_len"], level, MiB2, ora.TIE_INPUT)
+        assert np.array_equal(got, want) and np.array_equal(starts, wstarts), level
+        assert m.nfiles >= 200

@@ -117,3 +117,22 @@ def test_segments_inside_large_values_and_bad_guesses(ctx):
         st, od, _ = ora.decode_block(lsmgpu.GRAMMAR_KV, allb, offs[w], len(both[w]))
         assert int(r.status[w]) == st and int(r.nrec[w]) == len(od)
         assert np.array_equal(desc[bases[w]:bases[w] + len(od)], od)
+
+
+def test_bench_sized_replay(ctx):
+    """The wal bench's workload at full size: 64 memtable-sized logs, every
+    descriptor equal to the oracle's serial chase of each log."""
+    buf, off, ln, nrec = synth.wal_logs(64)
+    dev = ctx.torch_device
+    d = lsmgpu.to_device_bytes(buf, dev)
+    o = torch.tensor(np.asarray(off, np.uint64).view(np.int64), device=dev)
+    l2 = torch.tensor(np.asarray(ln, np.uint32).view(np.int32), device=dev)
+    r = lsmgpu.wal_replay(ctx, d, o, l2)
+    torch.cuda.synchronize()
+    assert (r.status.cpu().numpy() == 0).all()
+    assert np.array_equal(r.nrec.cpu().numpy(), nrec)
+    desc = r.desc_numpy()
+    bases = r.bases(np.asarray(off, np.uint64)).astype(np.int64)
+    for w in range(64):
+        st, od, _ = ora.decode_block(lsmgpu.GRAMMAR_KV, buf, int(off[w]), int(ln[w]))
+        assert st == 0 and np.array_equal(desc[bases[w]:bases[w] + nrec[w]], od), w
