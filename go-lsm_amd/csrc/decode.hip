@@ -2239,8 +2239,12 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         g1 = uni((uint64_t)g + 4 + v <= len ? g + 4 + v : len);
     }
     const uint32_t E = start + kWalSeg < len ? start + kWalSeg : len;
-    // 1. shares of [start, E): lane 0's chains are the two entries themselves
-    const uint32_t W = (E - start + kWave - 1) / kWave;
+    // 1. shares of [start, E): lane 0's chains are the two entries themselves.
+    //    A share width of a multiple of 128 B would start every lane on the
+    //    same LDS bank; widths of 4 mod 8 dwords spread them.
+    uint32_t W = (E - start + kWave - 1) / kWave;
+    W = (W + 3) & ~3u;
+    if ((W / 4) % 8 != 4) W += 4 * ((12 - (W / 4) % 8) % 8);
     const uint32_t ss = start + lane * W < E ? start + lane * W : E;
     const uint32_t se = ss + W < E ? ss + W : E;
     uint32_t e0 = 0xFFFFFFFFu, e1 = 0xFFFFFFFFu, c0 = 0, c1 = 0, x0 = 0, x1 = 0;
@@ -2638,9 +2642,11 @@ extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t
     a.fail = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) +
                                           (size_t)nfile * sizeof(SstWork));
     LSM_HIP_CHECK(hipMemsetAsync(a.fail, 0xFF, (size_t)nfile * 8, s));
-    // parallel passes: ~2048 workgroups over the batch, at most 64 per file
-    uint32_t g = (2048 + nfile - 1) / nfile;
+    // parallel passes: ~kSstWgs workgroups over the batch, at most 64 per file
+    static const uint32_t kSstWgs = getenv("LSM_SST_WGS") ? (uint32_t)atoi(getenv("LSM_SST_WGS")) : 2048;
+    uint32_t g = (kSstWgs + nfile - 1) / nfile;
     if (g > 64) g = 64;
+    if (g == 0) g = 1;
     hipLaunchKernelGGL(sst_index_kernel, dim3(g, nfile), dim3(256), 0, s, a);
     hipLaunchKernelGGL(sst_index_fixup_kernel, dim3(nfile), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(sst_data_verify_kernel, dim3(g, nfile), dim3(256), 0, s, a);
