@@ -55,7 +55,14 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and os.environ.get("LSM_BENCH_REHEARSE"):
+        # rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0,
+        # gloo for the barrier and the two scalar reductions (never a result)
+        import torch.distributed as dist
+        local = 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
