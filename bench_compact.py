@@ -95,11 +95,12 @@ def bench_compact(args, world, rank, local):
         mark(2)
         lsmgpu.merge_kvs_into(ctx, img, kd, vd, mg, level=1, stream=stream)
         mark(3)
-        batch = lsmgpu.gather_kvs(ctx, img, kd, vd, mg.out, mg.nout, key_bytes, val_bytes,
+        # keys packed; values read in place by the build (no second copy)
+        batch = lsmgpu.gather_kvs(ctx, img, kd, vd, mg.out, mg.nout, key_bytes, None,
                                   stream=stream)
         mark(4)
         sb = lsmgpu.prepare_sst_device(ctx, batch, mg.file_start, mg.nfiles)
-        lsmgpu.build_sst_into(ctx, batch, sb, stream=stream)
+        lsmgpu.build_sst_views_into(ctx, batch, sb, img, kd, vd, mg.out, stream=stream)
         mark(5)
         return sb, batch
 
@@ -120,10 +121,10 @@ def bench_compact(args, world, rank, local):
                 for i, nm in enumerate(ev_names)}
     in_bytes = float(file_size.astype(np.float64).sum())
     total = sum_over_ranks(world, in_bytes)
-    # the dominant stage, lsm_gather_kvs: per written pair the index (4 B) and
-    # two descriptors (32 B) read, koff / voff written (16 B), and the key and
-    # value bytes read once and written once
-    kv_bytes = float(batch.koff[mg.nout].item() + batch.voff[mg.nout].item())
+    # lsm_gather_kvs (keys only): per written pair the index (4 B) and two
+    # descriptors (32 B) read, koff / voff written (16 B), the key bytes read
+    # once and written once
+    kv_bytes = float(batch.koff[mg.nout].item())
     gather_alg = 52.0 * mg.nout + 2.0 * kv_bytes
     from bench import HBM_PEAK_GBS
     g_ach = gather_alg / (stage_ms["gather"] * 1e-3) / 1e9

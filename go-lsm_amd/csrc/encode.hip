@@ -935,7 +935,8 @@ struct SstArgs {
     int64_t *footer;
     uint64_t m, nwords;
     uint32_t k;
-    uint32_t dbg;  // diagnostics only: bit 0 skips the V region, bit 1 the IDX region
+    uint32_t dbg;     // diagnostics only: bit 0 skips the V region, bit 1 the IDX region
+    uint32_t skip_v;  // the V region is written from value views (lsm_build_sst_views)
 };
 
 struct SstLayout {
@@ -986,12 +987,148 @@ __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
     S.idx_base = (int64_t)L.data_off;
     S.rs = L.s;
     S.vrs = Vs;
-    if (!(a.dbg & 1))
+    if (!(a.dbg & 1) && !a.skip_v)
         encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
                                         lds[wave].gather, nullptr, &lds[wave].ct);
     if (!(a.dbg & 2))
         encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
                                           lds[wave].gather, nullptr, &lds[wave].ct);
+}
+
+// Data region (V grammar, sstable.go:159-175) of file blockIdx.x straight
+// from value views: record j of the batch is [u32 vlen][value], its value at
+// bytes + view(idx[j]) (a V descriptor, or the value of a KV descriptor).
+// One wave per 64 records: their records form one contiguous output range,
+// cut into 16-byte chunks (aligned in the output); an LDS map gives each
+// chunk its record; a chunk inside one value is five aligned source dwords
+// funnel-shifted into one 16-byte store, any other chunk (a length prefix,
+// a record boundary, an end of the range) is queued and written a dword or
+// a byte at a time.  Chunks are handled kVvMap at a time (any value size).
+struct VViewArgs {
+    const uint8_t *bytes;
+    const u32x4 *kd, *vd;  // vd == null: KV descriptors (value after the key)
+    const uint32_t *idx;
+};
+constexpr uint32_t kVvMap = 1024;
+
+__device__ __forceinline__ uint32_t ld_any32(const uint8_t *p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    return funnel(q[0], q[1], (uint32_t)a);
+}
+
+__device__ __forceinline__ void vv_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VViewArgs v) {
+    constexpr uint32_t W = kSstWaves;
+    __shared__ uint64_t s_dst[W][kWave + 1];  // output offset of record r's length prefix
+    __shared__ uint64_t s_src[W][kWave];      // source offset of its value bytes
+    __shared__ uint32_t s_vl[W][kWave];
+    __shared__ uint8_t s_map[W][kVvMap];
+    __shared__ uint16_t s_q[W][kVvMap];
+    const uint32_t f = blockIdx.x, w = threadIdx.x / kWave, lane = lane_id();
+    const SstLayout L = sst_layout(a, f);
+    const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kSstChunkRecs + (uint64_t)w * kWave;
+    if (c0 >= L.e) return;
+    const uint32_t cnt = (uint32_t)((L.e - c0) < (uint64_t)kWave ? (L.e - c0) : kWave);
+    const uint64_t Vs = uni64(a.voff[L.s]);
+    // record j's prefix at out + rbase + 4 j + voff[j]
+    const uint64_t rbase = uni64(a.file_off[f]) + L.data_off - 4 * L.s - Vs;
+    uint64_t d0 = 0, d1 = 0;
+    if (lane < cnt) {
+        const uint64_t j = c0 + lane;
+        const uint32_t i = v.idx[j];
+        const u32x4 k = v.kd[i];
+        uint64_t src;
+        uint32_t vl;
+        if (v.vd) {
+            const u32x4 d = v.vd[i];
+            src = ((uint64_t)d.y << 32 | d.x) + 4;
+            vl = d.w;
+        } else {
+            src = ((uint64_t)k.y << 32 | k.x) + 8 + k.z;
+            vl = k.w;
+        }
+        d0 = rbase + 4 * j + a.voff[j];
+        d1 = d0 + 4 + vl;
+        s_dst[w][lane] = d0;
+        s_src[w][lane] = src;
+        s_vl[w][lane] = vl;
+    }
+    if (lane == 0) s_dst[w][cnt] = rbase + 4 * (c0 + cnt) + a.voff[c0 + cnt];
+    vv_sync();
+    const uint64_t A = s_dst[w][0], B = s_dst[w][cnt], X = A & ~(uint64_t)15;
+    const uint64_t nch = (B - X + 15) / 16;
+    uint8_t *out = a.out;
+    for (uint64_t P = 0; P < nch; P += kVvMap) {
+        const uint32_t np = (uint32_t)(nch - P < kVvMap ? nch - P : kVvMap);
+        // 1. chunks whose first byte lies in my record
+        if (lane < cnt) {
+            const uint64_t lo = d0 > X ? (d0 - X + 15) / 16 : 0;
+            const uint64_t hi = (d1 - 1 - X) / 16;
+            const uint64_t c_lo = lo > P ? lo : P;
+            const uint64_t c_hi = hi < P + np - 1 ? hi : P + np - 1;
+            for (uint64_t c = c_lo; c <= c_hi; c++) s_map[w][c - P] = (uint8_t)lane;
+        }
+        vv_sync();
+        // 2. chunks inside one value; queue the rest
+        uint32_t qn = 0;
+        for (uint32_t cc0 = 0; cc0 < np; cc0 += kWave) {
+            const uint32_t c = cc0 + lane;
+            const uint64_t x = X + 16 * (P + c);
+            bool regular = false;
+            if (c < np && x >= A && x + 16 <= B) {
+                const uint32_t r = s_map[w][c];
+                const uint64_t e0 = s_dst[w][r] + 4, e1 = s_dst[w][r + 1];
+                if (x >= e0 && x + 16 <= e1) {
+                    regular = true;
+                    const uintptr_t sa = reinterpret_cast<uintptr_t>(v.bytes + s_src[w][r] + (x - e0));
+                    const uint32_t *q = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+                    const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+                    const uint32_t sh = (uint32_t)sa;
+                    u32x4 o;
+                    o.x = funnel(q0, q1, sh);
+                    o.y = funnel(q1, q2, sh);
+                    o.z = funnel(q2, q3, sh);
+                    o.w = funnel(q3, q4, sh);
+                    *reinterpret_cast<u32x4 *>(out + x) = o;
+                }
+            }
+            const bool irr = c < np && !regular;
+            const uint64_t im = __ballot(irr);
+            if (irr) s_q[w][qn + mbcnt(im)] = (uint16_t)c;
+            qn += (uint32_t)__builtin_popcountll(im);
+        }
+        vv_sync();
+        // 3. queued chunks: four lanes per chunk, a dword (or its bytes) each
+        for (uint32_t i0 = 0; i0 < qn; i0 += kWave / 4) {
+            const uint32_t i = i0 + lane / 4;
+            if (i >= qn) continue;
+            const uint32_t c = s_q[w][i];
+            const uint64_t x = X + 16 * (P + c), xd = x + 4 * (lane & 3);
+            if (xd >= B) continue;
+            uint32_t r = x >= A ? s_map[w][c] : 0;
+            while (r + 1 < cnt && xd >= s_dst[w][r + 1]) r++;
+            const uint64_t e0 = s_dst[w][r] + 4;
+            if (xd >= A && xd + 4 <= B && xd >= e0 && xd + 4 <= s_dst[w][r + 1]) {
+                *reinterpret_cast<uint32_t *>(out + xd) = ld_any32(v.bytes + s_src[w][r] + (xd - e0));
+            } else {
+                for (uint32_t u = 0; u < 4; u++) {
+                    const uint64_t b = xd + u;
+                    if (b < A || b >= B) continue;
+                    while (b >= s_dst[w][r + 1]) r++;
+                    const uint64_t t = b - s_dst[w][r];  // byte t of record r
+                    out[b] = t < 4 ? (uint8_t)(s_vl[w][r] >> (8 * t))
+                                   : v.bytes[s_src[w][r] + (t - 4)];
+                }
+            }
+        }
+        vv_sync();
+    }
 }
 
 // Header, filter-block prefix and footer of file blockIdx.x (one wave; byte
@@ -1389,15 +1526,16 @@ static uint32_t sst_dbg() {
     return v;
 }
 
-extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
-                             const uint8_t *d_vals, const uint64_t *d_voff,
-                             const uint64_t *d_file_start, uint32_t nfile,
-                             uint32_t max_file_records, uint64_t m, uint32_t k, uint8_t *d_out,
-                             const uint64_t *d_file_off, int64_t *d_footer, void *d_workspace,
-                             size_t ws_bytes, void *stream) {
+static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                          const uint8_t *d_vals, const uint64_t *d_voff,
+                          const uint64_t *d_file_start, uint32_t nfile,
+                          uint32_t max_file_records, uint64_t m, uint32_t k, uint8_t *d_out,
+                          const uint64_t *d_file_off, int64_t *d_footer, void *d_workspace,
+                          size_t ws_bytes, void *stream, const VViewArgs *views) {
     if (!ctx || m == 0 || m >= (1ull << 63)) return LSM_EINVAL;
     if (nfile == 0) return 0;
-    if (!d_keys || !d_koff || !d_vals || !d_voff || !d_file_start || !d_out || !d_file_off)
+    if (!d_keys || !d_koff || (!d_vals && !views) || !d_voff || !d_file_start || !d_out ||
+        !d_file_off)
         return LSM_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint64_t nwords = (m + 63) / 64;
@@ -1491,13 +1629,50 @@ extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t
     a.nwords = nwords;
     a.k = kk;
     a.dbg = sst_dbg();
+    a.skip_v = views != nullptr;
     if (chunks) {
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, chunks), dim3(256), 0, s, a);
         LSM_HIP_CHECK(hipGetLastError());
+        if (views) {
+            hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, s, a,
+                               *views);
+            LSM_HIP_CHECK(hipGetLastError());
+        }
     }
     hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                             const uint8_t *d_vals, const uint64_t *d_voff,
+                             const uint64_t *d_file_start, uint32_t nfile,
+                             uint32_t max_file_records, uint64_t m, uint32_t k, uint8_t *d_out,
+                             const uint64_t *d_file_off, int64_t *d_footer, void *d_workspace,
+                             size_t ws_bytes, void *stream) {
+    if (!d_vals && nfile) return LSM_EINVAL;
+    return build_sst_impl(ctx, d_keys, d_koff, d_vals, d_voff, d_file_start, nfile,
+                          max_file_records, m, k, d_out, d_file_off, d_footer, d_workspace,
+                          ws_bytes, stream, nullptr);
+}
+
+extern "C" int lsm_build_sst_views(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                                   const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                                   const lsm_rec_desc *d_val_desc, const uint32_t *d_idx,
+                                   const uint64_t *d_voff, const uint64_t *d_file_start,
+                                   uint32_t nfile, uint32_t max_file_records, uint64_t m,
+                                   uint32_t k, uint8_t *d_out, const uint64_t *d_file_off,
+                                   int64_t *d_footer, void *d_workspace, size_t ws_bytes,
+                                   void *stream) {
+    if (nfile && (!d_bytes || !d_key_desc || !d_idx)) return LSM_EINVAL;
+    VViewArgs v;
+    v.bytes = d_bytes;
+    v.kd = reinterpret_cast<const u32x4 *>(d_key_desc);
+    v.vd = reinterpret_cast<const u32x4 *>(d_val_desc);
+    v.idx = d_idx;
+    return build_sst_impl(ctx, d_keys, d_koff, nullptr, d_voff, d_file_start, nfile,
+                          max_file_records, m, k, d_out, d_file_off, d_footer, d_workspace,
+                          ws_bytes, stream, &v);
 }
 
 extern "C" int lsm_bloom_probe(lsm_ctx *ctx, const uint64_t *d_words, uint64_t m, uint32_t k,

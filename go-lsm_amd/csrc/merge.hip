@@ -620,6 +620,7 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
         X[h] = A[h] & ~(uint64_t)15;
         nc[h] = B[h] > A[h] ? (uint32_t)((B[h] - X[h] + 15) / 16) : 0;
     }
+    if (!vals) nc[1] = 0;  // keys only (lsm_build_sst_views reads the values in place)
     uint8_t *const dsts[2] = {keys, vals};
     const uint32_t total = nc[0] + nc[1];
     for (uint32_t P = 0; P < total; P += kMapChunks) {
@@ -976,8 +977,7 @@ extern "C" int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_re
                               uint8_t *d_keys, uint64_t *d_koff, uint8_t *d_vals, uint64_t *d_voff,
                               void *d_ws, size_t ws_bytes, void *stream) {
     if (!ctx || !d_koff || !d_voff || nout >= 0xFFFFFFFFull) return LSM_EINVAL;
-    if (nout && (!d_bytes || !d_key_desc || !d_idx || !d_keys || !d_vals || !d_ws))
-        return LSM_EINVAL;
+    if (nout && (!d_bytes || !d_key_desc || !d_idx || !d_keys || !d_ws)) return LSM_EINVAL;
     if (ws_bytes < lsm_gather_kvs_workspace_bytes(nout)) return LSM_ESPACE;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint32_t N = (uint32_t)nout;

@@ -12,5 +12,5 @@ from .codec import (  # noqa: F401
     sum256, to_device_bytes, SST_META_DTYPE, SST_STAGE_NAMES, SstDecode, alloc_sst_decode,
     decode_sst, decode_sst_into, wal_replay, wal_replay_into, wal_workspace,
     may_contain, may_contain_into, Merge, alloc_merge, merge_kvs, merge_kvs_into, gather_kvs,
-    prepare_sst_device, sst_pairs, sst_pairs_into, TOMBSTONE)
+    prepare_sst_device, sst_pairs, sst_pairs_into, TOMBSTONE, build_sst_views_into)
 from . import synth  # noqa: F401

@@ -67,6 +67,11 @@ SIGNATURES = {
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                      ctypes.c_uint32, c_u8p, c_u64p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_build_sst_views": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u8p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, c_u64p, c_u64p,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                           ctypes.c_uint32, c_u8p, c_u64p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "lsm_bloom_probe": (ctypes.c_int, [ctypes.c_void_p, c_u64p, ctypes.c_uint64, ctypes.c_uint32,
                                        c_u8p, c_u64p, ctypes.c_uint64, c_u8p, ctypes.c_void_p]),
     "lsm_sum256": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_uint64, c_u64p,

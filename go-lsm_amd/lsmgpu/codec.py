@@ -607,7 +607,8 @@ def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
     are left None (use sst_layout for the image sizes)."""
     dev = ctx.torch_device
     keys = torch.empty(pad16(max(key_bytes, 1)), dtype=torch.uint8, device=dev)
-    vals = torch.empty(pad16(max(val_bytes, 1)), dtype=torch.uint8, device=dev)
+    vals = (torch.empty(pad16(max(val_bytes, 1)), dtype=torch.uint8, device=dev)
+            if val_bytes is not None else None)  # None: keys only (build_sst_views_into)
     koff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
     voff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
     ws = torch.empty(int(ctx.lib.lsm_gather_kvs_workspace_bytes(nout)), dtype=torch.uint8,
@@ -669,3 +670,16 @@ def sst_pairs(ctx: Context, r: "SstDecode", stream=None) -> tuple:
     sst_pairs_into(ctx, r, kd, vd, prefix, stream=stream)
     n = int(prefix[r.nfile].item())
     return kd[:n], vd[:n], prefix
+
+
+def build_sst_views_into(ctx: Context, batch: RecordBatch, sb: "SstBuild", d_bytes: torch.Tensor,
+                         key_desc: torch.Tensor, val_desc: Optional[torch.Tensor],
+                         idx: torch.Tensor, stream=None) -> None:
+    """lsm_build_sst_views: the images of a keys-only gathered batch, values
+    read in place from their views (value i = view of pair idx[i])."""
+    nf = len(sb.file_start) - 1
+    _lib.check(ctx.lib.lsm_build_sst_views(
+        ctx.handle, _ptr(batch.keys), _ptr(batch.koff), _ptr(d_bytes), _ptr(key_desc),
+        _ptr(val_desc), _ptr(idx), _ptr(batch.voff), _ptr(sb.d_file_start), nf, sb.max_recs, sb.m,
+        sb.k, _ptr(sb.out), _ptr(sb.d_file_off), _ptr(sb.footer), _ptr(sb.workspace),
+        sb.workspace.numel(), _stream_handle(stream)), "lsm_build_sst_views")

@@ -287,6 +287,21 @@ int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
                   uint8_t *d_out, const uint64_t *d_file_off, int64_t *d_footer,
                   void *d_workspace, size_t ws_bytes, void *stream);
 
+/* lsm_build_sst with the values read in place: value i of the batch is the
+ * value of pair d_idx[i], a view into d_bytes (d_val_desc[d_idx[i]], a V
+ * descriptor; or, d_val_desc == NULL, the value of KV descriptor
+ * d_key_desc[d_idx[i]]); d_voff is the exclusive scan of those value lengths.
+ * The keys come packed (d_keys / d_koff).  That is the output of
+ * lsm_merge_kvs + lsm_gather_kvs(..., d_vals = NULL, ...): the values are not
+ * copied twice.  Same images as lsm_build_sst. */
+int lsm_build_sst_views(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                        const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                        const lsm_rec_desc *d_val_desc, const uint32_t *d_idx,
+                        const uint64_t *d_voff, const uint64_t *d_file_start, uint32_t nfile,
+                        uint32_t max_file_records, uint64_t m, uint32_t k, uint8_t *d_out,
+                        const uint64_t *d_file_off, int64_t *d_footer, void *d_workspace,
+                        size_t ws_bytes, void *stream);
+
 /* ---- bloom probe (verification side, Filter.Test bloom.go:371-379) ------- */
 
 /* Standalone bloom build: Filter.Add of every key (bloom.go:175-181) into
@@ -336,7 +351,8 @@ int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_ke
 /* The selected pairs d_idx[0 .. nout) as a CSR record batch -- the input of
  * lsm_build_sst: keys packed into d_keys with d_koff[0 .. nout], values into
  * d_vals with d_voff[0 .. nout] (the arenas must hold the selected bytes; the
- * input's totals always suffice).  Asynchronous. */
+ * input's totals always suffice).  d_vals == NULL packs the keys only (d_voff
+ * is still written) for lsm_build_sst_views.  Asynchronous. */
 size_t lsm_gather_kvs_workspace_bytes(uint64_t nout);
 int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
                    const lsm_rec_desc *d_val_desc, const uint32_t *d_idx, uint64_t nout,

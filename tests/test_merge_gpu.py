@@ -167,6 +167,18 @@ def test_gather_and_build_match_oracle_images(ctx):
         o = int(sb.file_off[f])
         assert int(sb.file_size[f]) == want.size
         assert np.array_equal(img[o:o + want.size], want), f
+    # values read in place: keys-only gather + lsm_build_sst_views, same images
+    for kv_layout in (False, True):
+        r2, d_buf2, d_kd2, d_vd2, got2, _ = run(ctx, pairs, 6, 200_000, kv_layout=kv_layout)
+        kb2 = lsmgpu.gather_kvs(ctx, d_buf2, d_kd2, d_vd2, r2.out, r2.nout, kb, None)
+        sb2 = lsmgpu.prepare_sst_device(ctx, kb2, r2.file_start, r2.nfiles, m=20_000, k=5)
+        lsmgpu.build_sst_views_into(ctx, kb2, sb2, d_buf2, d_kd2, d_vd2, r2.out)
+        torch.cuda.synchronize()
+        img2 = sb2.out.cpu().numpy()
+        for f in range(r2.nfiles):
+            want, _ = ora.build_sst(kn, koff, vn, voff, int(starts[f]), int(starts[f + 1]), m=20_000, k=5)
+            o = int(sb2.file_off[f])
+            assert np.array_equal(img2[o:o + want.size], want), (kv_layout, f)
 
 
 def test_sst_pairs_join(ctx):
