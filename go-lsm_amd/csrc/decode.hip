@@ -2274,7 +2274,80 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         uint32_t e = gp, acc_entry = 0xFFFFFFFFu, acc_cnt = 0, total = 0;
         int32_t status = LSM_OK;
         bool dead = false;
-        for (uint32_t l = 0; l < kWave; l++) {
+        // fast stitch: the share k holding the entry is chased exactly; after
+        // it, lane l's choice of chain (0: from e0, 1: from e1) is a function
+        // of lane l-1's choice (its chain's exit matched against lane l's
+        // entries); a 6-step scan composes these maps across the lanes.  Any
+        // miss (a wrong guess, or a record longer than a share) falls back to
+        // the serial stitch below.
+        bool fast = false;
+        {
+            const uint32_t k = (gp - start) / W;
+            const uint32_t last = (E - 1 - start) / W < kWave - 1 ? (E - 1 - start) / W : kWave - 1;
+            const uint32_t sek = uni(__builtin_amdgcn_readlane(se, k));
+            uint32_t ck, xk;
+            int32_t stk;
+            L.chase(gp, sek, ck, xk, stk);
+            ck = uni(ck);
+            xk = uni(xk);
+            stk = (int32_t)uni((uint32_t)stk);
+            auto match = [&](uint32_t x) -> uint32_t {
+                return (e0 != 0xFFFFFFFFu && x == e0) ? 0u : (e1 != 0xFFFFFFFFu && x == e1) ? 1u : 2u;
+            };
+            // map from lane l-1's choice to lane l's, as h0 | h1 << 4 (2 = miss)
+            const uint32_t xp0 = __shfl_up(x0, 1), xp1 = __shfl_up(x1, 1);
+            const uint32_t ep0 = __shfl_up(e0, 1), ep1 = __shfl_up(e1, 1);
+            uint32_t h;
+            if (lane <= k) {
+                h = 0u | 1u << 4;  // identity (never used: lane k+1's map is constant)
+            } else if (lane == k + 1) {
+                const uint32_t c = match(xk);
+                h = c | c << 4;
+            } else {
+                const uint32_t m0 = ep0 != 0xFFFFFFFFu ? match(xp0) : 2u;
+                const uint32_t m1 = ep1 != 0xFFFFFFFFu ? match(xp1) : 2u;
+                h = m0 | m1 << 4;
+            }
+#pragma unroll
+            for (uint32_t d = 1; d < kWave; d <<= 1) {
+                const uint32_t pv = __shfl_up(h, d);
+                if (lane >= d) {  // h := h o pv
+                    const uint32_t p0 = pv & 15, p1 = pv >> 4;
+                    const uint32_t n0 = p0 == 2 ? 2u : p0 == 0 ? (h & 15) : (h >> 4);
+                    const uint32_t n1 = p1 == 2 ? 2u : p1 == 0 ? (h & 15) : (h >> 4);
+                    h = n0 | n1 << 4;
+                }
+            }
+            const uint32_t ch = h & 15;  // lanes k+1 .. last: the chosen chain
+            const bool live = lane > k && lane <= last;
+            const int32_t cst = ch == 0 ? st0 : st1;
+            const uint64_t errm = __ballot(live && ch < 2 && cst != LSM_OK);
+            const uint32_t lim = stk != LSM_OK ? k : errm ? (uint32_t)__builtin_ctzll(errm) : last;
+            const uint64_t below = lim >= kWave - 1 ? ~0ull : (2ull << lim) - 1;  // lanes <= lim
+            const uint64_t missm = __ballot(live && ch == 2) & below;
+            if (!missm) {
+                fast = true;
+                if (lane == k) {
+                    acc_entry = gp;
+                    acc_cnt = ck;
+                } else if (live && lane <= lim) {
+                    acc_entry = ch == 0 ? e0 : e1;
+                    acc_cnt = ch == 0 ? c0 : c1;
+                }
+                const uint32_t xe = ch == 0 ? x0 : x1;
+                if (lim == k) {
+                    e = xk;
+                    status = stk;
+                } else {
+                    e = uni(__builtin_amdgcn_readlane(xe, lim));
+                    status = errm ? (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)cst, lim)) : LSM_OK;
+                }
+                uint32_t t;
+                wave_excl_scan(acc_cnt, &t);
+                total = t;
+            }
+        }
+        for (uint32_t l = 0; !fast && l < kWave; l++) {
             const uint32_t sl = uni(__builtin_amdgcn_readlane(ss, l));
             const uint32_t el = uni(__builtin_amdgcn_readlane(se, l));
             if (dead || sl >= el || e >= el) continue;
