@@ -1277,8 +1277,10 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
                                                                  const lsm_sst_meta *meta,
                                                                  uint32_t nfile, const uint8_t *keys,
                                                                  const uint64_t *koff, uint64_t nkeys,
-                                                                 uint8_t *hit) {
+                                                                 uint8_t *hit, uint32_t nobloom,
+                                                                 const uint32_t *grouped) {
     __shared__ McFile tile[kMcTile];
+    if (*grouped) return;  // the files are sorted and disjoint: mc_* kernels answer
     __shared__ uint32_t sout[kMcThreads * kMcRow];
     const uint64_t i0 = (uint64_t)blockIdx.x * kMcThreads;
     const uint64_t i = i0 + threadIdx.x;
@@ -1357,11 +1359,11 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
                     const uint64_t m = F.m;
                     r = m != 0;  // m == 0: Go's location() divides by zero
                     // Test's answer is the AND of all k bits (its early exit
-                    // changes nothing): eight loads in flight at a time
-                    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 8) {
+                    // changes nothing): sixteen loads in flight at a time
+                    for (uint32_t j0 = 0; j0 < F.k && r && !nobloom; j0 += 16) {
                         uint32_t bits = 1;
 #pragma unroll
-                        for (uint32_t u = 0; u < 8; u++) {
+                        for (uint32_t u = 0; u < 16; u++) {
                             const uint32_t j = j0 + u;
                             if (j < F.k && r) {
                                 const uint64_t x = location(h[0], h[1], h[2], h[3], j);
@@ -1397,6 +1399,305 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
             }
         }
     }
+}
+
+// Grouped path for the level >= 1 shape (every file decoded, files in key
+// order with disjoint ranges, at most kMcMaxFiles files): each probe has at
+// most one candidate file.  The candidates are hashed once, grouped by file
+// (a counting sort), and each file's workgroup stages the filter in LDS and
+// tests its probes' bits there: the filter bits are read once from HBM
+// instead of once per probe bit.
+constexpr uint32_t kMcLdsBytes = 150 * 1024;  // filter words staged in LDS per file
+constexpr uint32_t kMcTestThreads = 1024;
+constexpr uint32_t kMcNone = 0xFFFFFFFFu;
+constexpr uint32_t kMcGroupThreads = 1024;
+constexpr uint32_t kMcGroupPer = 4;  // probes per thread
+constexpr uint32_t kMcGroupProbes = kMcGroupThreads * kMcGroupPer;
+constexpr uint32_t kMcMaxFiles = 2048;  // LDS bounds + counters; more files: per-probe path
+
+struct McWs {
+    uint32_t *flag;     // [0] = 1: grouped path
+    McFile *files;
+    uint32_t *hist;     // nfile + 1: counts, then exclusive offsets
+    uint32_t *cursor;   // nfile
+    uint32_t *cand;     // nkeys
+    uint64_t *hash;     // 4 * nkeys
+    uint32_t *list;     // nkeys
+};
+
+__device__ __forceinline__ McFile mc_file(const uint8_t *img, const uint64_t *file_off,
+                                          const lsm_sst_meta &M, uint32_t f) {
+    const uint64_t fo = file_off[f];
+    const uint8_t *base = img + fo;
+    McFile F;
+    F.ok = M.stage != 1 && M.stage != 2;
+    F.lo_len = (uint32_t)M.min_key_len;
+    F.hi_len = (uint32_t)M.max_key_len;
+    for (uint32_t j = 0; j < 4; j++) {
+        F.lo[j] = F.ok ? be_word_at(base + M.min_key_off, M.min_key_len, j) : 0;
+        F.hi[j] = F.ok ? be_word_at(base + M.max_key_off, M.max_key_len, j) : 0;
+    }
+    F.lo_at = fo + M.min_key_off;
+    F.hi_at = fo + M.max_key_off;
+    F.words_at = fo + M.filter_words_off;
+    F.k = M.filter_k < 4096 ? (uint32_t)M.filter_k : 4096;
+    F.m = M.filter_m;
+    F.mr = M.filter_m ? ~0ull / M.filter_m : 0;
+    F.nbits = M.filter_nbits;
+    return F;
+}
+
+__global__ __launch_bounds__(256) void mc_prep_kernel(const uint8_t *img, const uint64_t *file_off,
+                                                      const lsm_sst_meta *meta, uint32_t nfile,
+                                                      McWs w) {
+    bool ok = true;
+    for (uint32_t f = threadIdx.x; f < nfile; f += blockDim.x) {
+        const McFile F = mc_file(img, file_off, meta[f], f);
+        w.files[f] = F;
+        w.hist[f] = 0;
+        w.cursor[f] = 0;
+        // m < 2^63 for the Barrett reduction
+        ok = ok && F.ok && F.m < (1ull << 63);
+    }
+    if (nfile > kMcMaxFiles) ok = false;
+    __syncthreads();
+    for (uint32_t f = threadIdx.x; f + 1 < nfile; f += blockDim.x) {
+        const McFile &A = w.files[f], &B = w.files[f + 1];
+        ok = ok && bound_cmp_fast(A.hi, A.hi_len, img + A.hi_at, B.lo, B.lo_len, img + B.lo_at) < 0;
+    }
+    ok = __syncthreads_and(ok);
+    if (threadIdx.x == 0) {
+        w.flag[0] = ok ? 1u : 0u;
+        w.hist[nfile] = 0;
+    }
+}
+
+// Probes are grouped block-locally first (LDS counters), so each workgroup
+// adds to a file's global counter once: 1M probes over 208 files serialised
+// on 208 global atomics took 350 us, the block-local counts take a few.
+// The files' bound prefixes sit in LDS for the candidate search.
+__global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint8_t *img, uint32_t nfile,
+                                                                      const uint8_t *keys,
+                                                                      const uint64_t *koff,
+                                                                      uint64_t nkeys, McWs w) {
+    __shared__ uint4 slo[kMcMaxFiles], shi[kMcMaxFiles];
+    __shared__ uint32_t lh[kMcMaxFiles];
+    if (!w.flag[0]) return;
+    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads) {
+        const McFile &F = w.files[f];
+        slo[f] = make_uint4(F.lo[0], F.lo[1], F.lo[2], F.lo[3]);
+        shi[f] = make_uint4(F.hi[0], F.hi[1], F.hi[2], F.hi[3]);
+        lh[f] = 0;
+    }
+    // every probe's key bytes and hash, all loads in flight before the search
+    uint64_t k0[kMcGroupPer], kl[kMcGroupPer];
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        k0[p] = i < nkeys ? koff[i] : 0;
+        kl[p] = i < nkeys ? koff[i + 1] - k0[p] : 0;
+    }
+    uint32_t kw[kMcGroupPer][4];
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++)
+        for (uint32_t j = 0; j < 4; j++) kw[p][j] = be_word_at(keys + k0[p], kl[p], j);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        if (i >= nkeys) break;
+        const uint8_t *kp = keys + k0[p];
+        uint32_t lo = 0, hi = nfile;  // first file with MinKey > key
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            const uint4 v = slo[mid];
+            const uint32_t bw[4] = {v.x, v.y, v.z, v.w};
+            int c = prefix_cmp(bw, kw[p]);
+            if (c == 0) {
+                const McFile &F = w.files[mid];
+                c = bound_cmp(bw, F.lo_len, img + F.lo_at, kw[p], kl[p], kp);
+            }
+            if (c <= 0) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t c = kMcNone;
+        if (lo > 0) {
+            const uint4 v = shi[lo - 1];
+            const uint32_t bw[4] = {v.x, v.y, v.z, v.w};
+            int r = prefix_cmp(bw, kw[p]);
+            if (r == 0) {
+                const McFile &F = w.files[lo - 1];
+                r = bound_cmp(bw, F.hi_len, img + F.hi_at, kw[p], kl[p], kp);
+            }
+            if (r >= 0) {
+                c = lo - 1;
+                atomicAdd(&lh[c], 1u);
+                uint64_t h[4];  // only candidates are ever tested
+                sum256(kp, kl[p], h);
+                for (int j = 0; j < 4; j++) w.hash[4 * i + j] = h[j];
+            }
+        }
+        w.cand[i] = c;
+    }
+    __syncthreads();
+    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads)
+        if (lh[f]) atomicAdd(&w.hist[f], lh[f]);
+}
+
+__global__ __launch_bounds__(256) void mc_offsets_kernel(uint32_t nfile, McWs w) {
+    if (!w.flag[0]) return;
+    __shared__ uint32_t part[256];
+    uint32_t carry = 0;
+    for (uint32_t f0 = 0; f0 < nfile; f0 += 256) {
+        const uint32_t f = f0 + threadIdx.x;
+        const uint32_t v = f < nfile ? w.hist[f] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive scan in LDS
+            const uint32_t t = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+            __syncthreads();
+            part[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (f < nfile) w.hist[f] = carry + part[threadIdx.x] - v;
+        carry += part[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) w.hist[nfile] = carry;
+}
+
+// Same probe->workgroup mapping as mc_classify_kernel: ranks inside the
+// workgroup from LDS counters, one global reservation per (workgroup, file).
+// Each candidate's hit byte starts at 1; a filter part that finds a clear bit
+// stores 0 (every writer stores the same value, so no atomics).
+__global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nfile, uint64_t nkeys, McWs w,
+                                                                     uint8_t *hit) {
+    __shared__ uint32_t lh[kMcMaxFiles];
+    if (!w.flag[0]) return;
+    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads) lh[f] = 0;
+    __syncthreads();
+    uint32_t c[kMcGroupPer], rk[kMcGroupPer];
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        c[p] = i < nkeys ? w.cand[i] : kMcNone;
+        rk[p] = c[p] != kMcNone ? atomicAdd(&lh[c[p]], 1u) : 0;
+    }
+    __syncthreads();
+    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads)
+        if (lh[f]) lh[f] = w.hist[f] + atomicAdd(&w.cursor[f], lh[f]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        if (c[p] != kMcNone) {
+            w.list[lh[c[p]] + rk[p]] = (uint32_t)i;
+            hit[i * nfile + c[p]] = 1;
+        }
+    }
+}
+
+// One workgroup per file: the first kMcLdsBytes of the stored filter words
+// go to LDS (all loads in flight), the rest (a 1.6M-bit filter is 200 KB) is
+// read from L2, where the workgroup's repeated touches keep it.  Each probe's
+// k locations are computed once; a probe whose bit is clear stores 0 over the
+// 1 the scatter wrote.  The hashes of the first probes are loaded before the
+// LDS fill.
+__global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *img, uint32_t nfile, McWs w,
+                                                                 uint8_t *hit) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
+    if (!w.flag[0]) return;
+    const uint32_t f = blockIdx.x;
+    const uint32_t b0 = w.hist[f], b1 = w.hist[f + 1];
+    if (b0 == b1) return;
+    const McFile F = w.files[f];
+    uint32_t t = b0 + threadIdx.x, i = 0;
+    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    if (t < b1) {
+        i = w.list[t];
+        h0 = w.hash[4 * (uint64_t)i]; h1 = w.hash[4 * (uint64_t)i + 1];
+        h2 = w.hash[4 * (uint64_t)i + 2]; h3 = w.hash[4 * (uint64_t)i + 3];
+    }
+    // LDS holds the words from the 16-byte boundary below them: aligned
+    // 16-byte loads, each chunk holding at least one filter byte (no fault)
+    const uint8_t *src = img + F.words_at;
+    const uint64_t nb = 8 * ((F.nbits + 63) / 64);
+    const uint32_t delta = (uint32_t)((uintptr_t)src & 15);
+    const uint64_t in_lds = nb < kMcLdsBytes - 16 ? nb : kMcLdsBytes - 16;  // bytes [0, in_lds)
+    const uint4 *src16 = reinterpret_cast<const uint4 *>(src - delta);
+    uint4 *dst16 = reinterpret_cast<uint4 *>(fbytes);
+    const uint32_t n16 = (uint32_t)((delta + in_lds + 15) / 16);
+    constexpr uint32_t kU = (kMcLdsBytes / 16 + kMcTestThreads - 1) / kMcTestThreads;
+    if (n16) {
+        uint4 v[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {  // clamped: every load is issued, no branches
+            const uint32_t x = u * kMcTestThreads + threadIdx.x;
+            v[u] = src16[x < n16 ? x : n16 - 1];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t x = u * kMcTestThreads + threadIdx.x;
+            if (x < n16) dst16[x] = v[u];
+        }
+    }
+    __syncthreads();
+    const uint8_t *lb = fbytes + delta;
+    const bool small = F.m <= (1ull << 30);
+    const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
+    while (t < b1) {
+        const uint32_t tn = t + kMcTestThreads;
+        uint32_t in = 0;
+        uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+        if (tn < b1) {  // next probe's hash in flight during this one's tests
+            in = w.list[tn];
+            n0 = w.hash[4 * (uint64_t)in]; n1 = w.hash[4 * (uint64_t)in + 1];
+            n2 = w.hash[4 * (uint64_t)in + 2]; n3 = w.hash[4 * (uint64_t)in + 3];
+        }
+        uint32_t r = F.m != 0;  // m == 0: Go's location() divides by zero
+        // Test is the AND of all k bits (its early exit changes nothing):
+        // sixteen bit reads in flight at a time
+        for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
+            uint32_t bits = 1;
+#pragma unroll
+            for (uint32_t u = 0; u < 16; u++) {
+                const uint32_t j = j0 + u;
+                if (j < F.k) {
+                    const uint64_t x = location(h0, h1, h2, h3, j);
+                    const uint64_t p = small ? mod_small(x, m32, rl, rh) : mod_barrett(x, F.m, F.mr);
+                    if (p >= F.nbits) {
+                        bits = 0;  // bitset.Test is false past its length
+                    } else {
+                        const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+                        const uint32_t byte = q < in_lds ? lb[q] : src[q];
+                        bits &= byte >> (p & 7);
+                    }
+                }
+            }
+            r = bits & 1;
+        }
+        if (!r) hit[(uint64_t)i * nfile + f] = 0;
+        t = tn; i = in; h0 = n0; h1 = n1; h2 = n2; h3 = n3;
+    }
+}
+
+McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
+    McWs w{};
+    size_t at = 0;
+    auto take = [&](size_t bytes) -> uint8_t * {
+        uint8_t *p = base ? base + at : nullptr;
+        at += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    w.flag = reinterpret_cast<uint32_t *>(take(16));
+    w.files = reinterpret_cast<McFile *>(take(sizeof(McFile) * (size_t)(nfile ? nfile : 1)));
+    w.hist = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
+    w.cursor = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
+    w.cand = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
+    w.hash = reinterpret_cast<uint64_t *>(take(32 * (nkeys ? nkeys : 1)));
+    w.list = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
+    if (total) *total = at;
+    return w;
 }
 
 template <int G>
@@ -1689,18 +1990,46 @@ extern "C" int lsm_bloom_probe(lsm_ctx *ctx, const uint64_t *d_words, uint64_t m
     return 0;
 }
 
+extern "C" size_t lsm_may_contain_workspace_bytes(uint32_t nfile, uint64_t nkeys) {
+    size_t t = 0;
+    mc_ws_layout(nullptr, nfile, nkeys, &t);
+    return t;
+}
+
 extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
                                const lsm_sst_meta *d_meta, uint32_t nfile, const uint8_t *d_keys,
                                const uint64_t *d_koff, uint64_t nkeys, uint8_t *d_hit,
-                               void *stream) {
+                               void *d_workspace, size_t ws_bytes, void *stream) {
     if (!ctx) return LSM_EINVAL;
     if (nkeys == 0 || nfile == 0) return 0;
-    if (!d_img || !d_file_off || !d_meta || !d_keys || !d_koff || !d_hit) return LSM_EINVAL;
+    if (!d_img || !d_file_off || !d_meta || !d_keys || !d_koff || !d_hit || !d_workspace)
+        return LSM_EINVAL;
+    size_t need = 0;
+    const McWs w = mc_ws_layout(static_cast<uint8_t *>(d_workspace), nfile, nkeys, &need);
+    if (ws_bytes < need) return LSM_ESPACE;
     const uint64_t grid = (nkeys + kMcThreads - 1) / kMcThreads;
     if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
-    hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(kMcThreads), 0,
-                       static_cast<hipStream_t>(stream), d_img, d_file_off, d_meta, nfile, d_keys,
-                       d_koff, nkeys, d_hit);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    static const uint32_t nobloom = getenv("LSM_MC_NOBLOOM") ? 1u : 0u;  // diagnostics only
+    static const bool linear = getenv("LSM_MC_LINEAR") != nullptr;       // A/B: per-probe path only
+    if (linear || nkeys > 0xFFFFFFFFull) {  // list entries are 32-bit
+        LSM_HIP_CHECK(hipMemsetAsync(w.flag, 0, 4, s));
+    } else {
+        hipLaunchKernelGGL(mc_prep_kernel, dim3(1), dim3(256), 0, s, d_img, d_file_off, d_meta, nfile, w);
+        // the grouped path writes only the candidate byte of each row
+        LSM_HIP_CHECK(hipMemsetAsync(d_hit, 0, (size_t)nkeys * nfile, s));
+        const uint32_t ggrid = (uint32_t)((nkeys + kMcGroupProbes - 1) / kMcGroupProbes);
+        hipLaunchKernelGGL(mc_classify_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, d_img,
+                           nfile, d_keys, d_koff, nkeys, w);
+        hipLaunchKernelGGL(mc_offsets_kernel, dim3(1), dim3(256), 0, s, nfile, w);
+        hipLaunchKernelGGL(mc_scatter_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, nfile, nkeys, w,
+                           d_hit);
+        hipLaunchKernelGGL(mc_test_kernel, dim3(nfile), dim3(kMcTestThreads), kMcLdsBytes, s,
+                           d_img, nfile, w, d_hit);
+    }
+    hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(kMcThreads), 0, s, d_img,
+                       d_file_off, d_meta, nfile, d_keys, d_koff, nkeys, d_hit, nobloom,
+                       (const uint32_t *)w.flag);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -11,6 +11,6 @@ from .codec import (  # noqa: F401
     decode_blocks, decode_into, encode_blocks, pad16, plan, prepare_sst, replan, segment_files,
     sum256, to_device_bytes, SST_META_DTYPE, SST_STAGE_NAMES, SstDecode, alloc_sst_decode,
     decode_sst, decode_sst_into, wal_replay, wal_replay_into, wal_workspace,
-    may_contain, may_contain_into, Merge, alloc_merge, merge_kvs, merge_kvs_into, gather_kvs,
+    may_contain, may_contain_into, may_contain_workspace, Merge, alloc_merge, merge_kvs, merge_kvs_into, gather_kvs,
     prepare_sst_device, sst_pairs, sst_pairs_into, TOMBSTONE, build_sst_views_into)
 from . import synth  # noqa: F401

@@ -381,13 +381,21 @@ def decode_sst(ctx: Context, d_img: torch.Tensor, file_off: np.ndarray, file_len
     return r
 
 
+def may_contain_workspace(ctx: Context, nfile: int, nkeys: int) -> torch.Tensor:
+    n = int(ctx.lib.lsm_may_contain_workspace_bytes(nfile, nkeys))
+    return torch.empty(max(n, 16), dtype=torch.uint8, device=ctx.torch_device)
+
+
 def may_contain_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
-                     hit: torch.Tensor, stream=None) -> None:
+                     hit: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None) -> None:
     """lsm_may_contain: SSTable.MayContain of every key of `batch` against
     every file decoded into r; hit viewed as uint8[nkeys, nfile]."""
+    if ws is None:
+        ws = may_contain_workspace(ctx, r.nfile, batch.n)
     _lib.check(ctx.lib.lsm_may_contain(ctx.handle, _ptr(d_img), _ptr(r.d_file_off), _ptr(r.meta),
                                        r.nfile, _ptr(batch.keys), _ptr(batch.koff), batch.n,
-                                       _ptr(hit), _stream_handle(stream)), "lsm_may_contain")
+                                       _ptr(hit), _ptr(ws), ws.numel(), _stream_handle(stream)),
+               "lsm_may_contain")
 
 
 def may_contain(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",

@@ -148,3 +148,16 @@ def test_may_contain_sorted_disjoint_files(ctx):
     probes += [b"", b"r", b"s", b"t", b"s%06d" % 69950 + b"\x00"]
     check(ctx, rng, images, probes)
     check(ctx, rng, images[:64], probes)
+
+
+def test_may_contain_sorted_large_filters(ctx):
+    """Grouped path with the production filter (m = 1.6M bits, k = 16: all
+    four LDS parts hold stored words), files at odd offsets, probes held,
+    in the gaps and outside the level."""
+    rng = np.random.default_rng(55)
+    images = []
+    for f in range(5):
+        keys = sorted({b"L%07d" % (f * 10000 + int(x)) for x in rng.integers(0, 9000, 400)})
+        images.append(build(keys, m=1_600_000, k=16))
+    probes = [b"L%07d" % int(x) for x in rng.integers(0, 52000, 3000)] + [b"", b"L", b"M"]
+    check(ctx, rng, images, probes)
