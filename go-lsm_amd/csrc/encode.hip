@@ -1407,11 +1407,11 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
 // (a counting sort), and each file's workgroup stages the filter in LDS and
 // tests its probes' bits there: the filter bits are read once from HBM
 // instead of once per probe bit.
-constexpr uint32_t kMcLdsBytes = 150 * 1024;  // filter words staged in LDS per file
+constexpr uint32_t kMcLdsBytes = 144 * 1024;  // filter words staged in LDS per file
 constexpr uint32_t kMcTestThreads = 1024;
 constexpr uint32_t kMcNone = 0xFFFFFFFFu;
 constexpr uint32_t kMcGroupThreads = 1024;
-constexpr uint32_t kMcGroupPer = 4;  // probes per thread
+constexpr uint32_t kMcGroupPer = 2;  // probes per thread
 constexpr uint32_t kMcGroupProbes = kMcGroupThreads * kMcGroupPer;
 constexpr uint32_t kMcMaxFiles = 2048;  // LDS bounds + counters; more files: per-probe path
 
@@ -1479,7 +1479,8 @@ __global__ __launch_bounds__(256) void mc_prep_kernel(const uint8_t *img, const 
 __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint8_t *img, uint32_t nfile,
                                                                       const uint8_t *keys,
                                                                       const uint64_t *koff,
-                                                                      uint64_t nkeys, McWs w) {
+                                                                      uint64_t nkeys, McWs w,
+                                                                      uint8_t *hit) {
     __shared__ uint4 slo[kMcMaxFiles], shi[kMcMaxFiles];
     __shared__ uint32_t lh[kMcMaxFiles];
     if (!w.flag[0]) return;
@@ -1489,18 +1490,46 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
         shi[f] = make_uint4(F.hi[0], F.hi[1], F.hi[2], F.hi[3]);
         lh[f] = 0;
     }
-    // every probe's key bytes and hash, all loads in flight before the search
-    uint64_t k0[kMcGroupPer], kl[kMcGroupPer];
+    // every probe's first 16 key bytes (dword loads; batches are 16-byte
+    // padded), all loads in flight before the search
+    uint64_t k0[kMcGroupPer], kl[kMcGroupPer], f0[kMcGroupPer], f1[kMcGroupPer];
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
         const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
         k0[p] = i < nkeys ? koff[i] : 0;
         kl[p] = i < nkeys ? koff[i + 1] - k0[p] : 0;
     }
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++) {
+        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        f0[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p]) : 0;
+        f1[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p] + 8) : 0;
+    }
+    {   // the workgroup's rows of the hit matrix start at 0 (16-byte stores
+        // while the key loads are in flight)
+        const uint64_t r0 = (uint64_t)blockIdx.x * kMcGroupProbes;
+        const uint64_t r1 = r0 + kMcGroupProbes < nkeys ? r0 + kMcGroupProbes : nkeys;
+        uint8_t *z = hit + r0 * nfile;
+        const uint64_t nz = (r1 - r0) * nfile;
+        const uint64_t head = ((16 - ((uintptr_t)z & 15)) & 15) < nz ? ((16 - ((uintptr_t)z & 15)) & 15) : nz;
+        const uint64_t n16 = (nz - head) / 16, tail = head + 16 * n16;
+        if (threadIdx.x < head) z[threadIdx.x] = 0;
+        uint4 *z16 = reinterpret_cast<uint4 *>(z + head);
+        for (uint64_t x = threadIdx.x; x < n16; x += kMcGroupThreads) z16[x] = make_uint4(0, 0, 0, 0);
+        if (tail + threadIdx.x < nz) z[tail + threadIdx.x] = 0;
+    }
     uint32_t kw[kMcGroupPer][4];
 #pragma unroll
-    for (uint32_t p = 0; p < kMcGroupPer; p++)
-        for (uint32_t j = 0; j < 4; j++) kw[p][j] = be_word_at(keys + k0[p], kl[p], j);
+    for (uint32_t p = 0; p < kMcGroupPer; p++) {
+        // zero the bytes past the key, then the big-endian prefix words
+        const uint64_t l = kl[p];
+        if (l < 8) { f0[p] &= l ? (~0ull >> (64 - 8 * l)) : 0; f1[p] = 0; }
+        else if (l < 16) f1[p] &= l > 8 ? (~0ull >> (128 - 8 * l)) : 0;
+        kw[p][0] = __builtin_bswap32((uint32_t)f0[p]);
+        kw[p][1] = __builtin_bswap32((uint32_t)(f0[p] >> 32));
+        kw[p][2] = __builtin_bswap32((uint32_t)f1[p]);
+        kw[p][3] = __builtin_bswap32((uint32_t)(f1[p] >> 32));
+    }
     __syncthreads();
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
@@ -1533,7 +1562,7 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
                 c = lo - 1;
                 atomicAdd(&lh[c], 1u);
                 uint64_t h[4];  // only candidates are ever tested
-                sum256(kp, kl[p], h);
+                sum256_pre(kp, kl[p], f0[p], f1[p], h);
                 for (int j = 0; j < 4; j++) w.hash[4 * i + j] = h[j];
             }
         }
@@ -1604,7 +1633,7 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nf
 // 1 the scatter wrote.  The hashes of the first probes are loaded before the
 // LDS fill.
 __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *img, uint32_t nfile, McWs w,
-                                                                 uint8_t *hit) {
+                                                                 uint8_t *hit, uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
     if (!w.flag[0]) return;
     const uint32_t f = blockIdx.x;
@@ -1619,32 +1648,38 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
         h2 = w.hash[4 * (uint64_t)i + 2]; h3 = w.hash[4 * (uint64_t)i + 3];
     }
     // LDS holds the words from the 16-byte boundary below them: aligned
-    // 16-byte loads, each chunk holding at least one filter byte (no fault)
+    // 16-byte global->LDS loads (no VGPR staging, all in flight), each chunk
+    // holding at least one filter byte (no fault).  Lanes past the end load
+    // the last chunk again into LDS the filter does not use.
     const uint8_t *src = img + F.words_at;
     const uint64_t nb = 8 * ((F.nbits + 63) / 64);
     const uint32_t delta = (uint32_t)((uintptr_t)src & 15);
     const uint64_t in_lds = nb < kMcLdsBytes - 16 ? nb : kMcLdsBytes - 16;  // bytes [0, in_lds)
     const uint4 *src16 = reinterpret_cast<const uint4 *>(src - delta);
-    uint4 *dst16 = reinterpret_cast<uint4 *>(fbytes);
     const uint32_t n16 = (uint32_t)((delta + in_lds + 15) / 16);
-    constexpr uint32_t kU = (kMcLdsBytes / 16 + kMcTestThreads - 1) / kMcTestThreads;
-    if (n16) {
-        uint4 v[kU];
+    constexpr uint32_t kU = kMcLdsBytes / 16 / kMcTestThreads;
+    static_assert(kMcLdsBytes % (16 * kMcTestThreads) == 0, "whole rounds of 16-byte loads");
+    // 1 KiB wave chunks, the order rotated per file: the filters sit at the
+    // same offset of ~2 MB files, so unrotated fills hit the same channels
+    const uint32_t nwc = (n16 + kWave - 1) / kWave, wave = threadIdx.x / kWave;
+    const uint32_t rot = nwc ? (f * 37u) % nwc : 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {  // clamped: every load is issued, no branches
-            const uint32_t x = u * kMcTestThreads + threadIdx.x;
-            v[u] = src16[x < n16 ? x : n16 - 1];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t x = u * kMcTestThreads + threadIdx.x;
-            if (x < n16) dst16[x] = v[u];
+    for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t cl = u * (kMcTestThreads / kWave) + wave;
+        if (cl < nwc) {
+            const uint32_t c = cl + rot < nwc ? cl + rot : cl + rot - nwc;
+            const uint32_t xw = c * kWave, x = xw + (threadIdx.x & (kWave - 1));
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(src16 + (x < n16 ? x : n16 - 1)),
+                (__attribute__((address_space(3))) void *)(fbytes + 16 * xw), 16, 0, 0);
         }
     }
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint8_t *lb = fbytes + delta;
     const bool small = F.m <= (1ull << 30);
     const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
+    if (dbg & 1) return;  // diagnostics: the LDS fill only
     while (t < b1) {
         const uint32_t tn = t + kMcTestThreads;
         uint32_t in = 0;
@@ -1669,7 +1704,9 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
                         bits = 0;  // bitset.Test is false past its length
                     } else {
                         const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
-                        const uint32_t byte = q < in_lds ? lb[q] : src[q];
+                        uint32_t byte;
+                        if (q < in_lds) byte = lb[q];
+                        else byte = (dbg & 2) ? 0xFFu : src[q];  // the tail past the LDS copy, from L2
                         bits &= byte >> (p & 7);
                     }
                 }
@@ -2012,20 +2049,19 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
     hipStream_t s = static_cast<hipStream_t>(stream);
     static const uint32_t nobloom = getenv("LSM_MC_NOBLOOM") ? 1u : 0u;  // diagnostics only
     static const bool linear = getenv("LSM_MC_LINEAR") != nullptr;       // A/B: per-probe path only
+    static const uint32_t mcdbg = getenv("LSM_MC_DBG") ? (uint32_t)atoi(getenv("LSM_MC_DBG")) : 0u;
     if (linear || nkeys > 0xFFFFFFFFull) {  // list entries are 32-bit
         LSM_HIP_CHECK(hipMemsetAsync(w.flag, 0, 4, s));
     } else {
         hipLaunchKernelGGL(mc_prep_kernel, dim3(1), dim3(256), 0, s, d_img, d_file_off, d_meta, nfile, w);
-        // the grouped path writes only the candidate byte of each row
-        LSM_HIP_CHECK(hipMemsetAsync(d_hit, 0, (size_t)nkeys * nfile, s));
         const uint32_t ggrid = (uint32_t)((nkeys + kMcGroupProbes - 1) / kMcGroupProbes);
         hipLaunchKernelGGL(mc_classify_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, d_img,
-                           nfile, d_keys, d_koff, nkeys, w);
+                           nfile, d_keys, d_koff, nkeys, w, d_hit);
         hipLaunchKernelGGL(mc_offsets_kernel, dim3(1), dim3(256), 0, s, nfile, w);
         hipLaunchKernelGGL(mc_scatter_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, nfile, nkeys, w,
                            d_hit);
         hipLaunchKernelGGL(mc_test_kernel, dim3(nfile), dim3(kMcTestThreads), kMcLdsBytes, s,
-                           d_img, nfile, w, d_hit);
+                           d_img, nfile, w, d_hit, mcdbg);
     }
     hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(kMcThreads), 0, s, d_img,
                        d_file_off, d_meta, nfile, d_keys, d_koff, nkeys, d_hit, nobloom,

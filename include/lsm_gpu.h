@@ -229,10 +229,10 @@ int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_of
  * did not decode (stage 1 or 2) reports 0.  d_hit[i * nfile + f] = 1 when
  * key i may be in file f.  Deviations on corrupted filters only: m == 0
  * reports 0 (Go divides by zero) and k is capped at 4096 probes.
- * When every file decoded and the files are in key order with disjoint
- * ranges (a level >= 1 set), the probes are grouped by their one candidate
- * file and each filter is tested from LDS; otherwise every key is checked
- * against every file.  The workspace holds the grouping (see
+ * When every file decoded, the files are in key order with disjoint ranges
+ * (a level >= 1 set), nfile <= 2048 and nkeys < 2^32, the probes are grouped
+ * by their one candidate file and each filter is tested from LDS; otherwise
+ * every key is checked against every file.  The workspace holds the grouping (see
  * lsm_may_contain_workspace_bytes); d_hit is written whole either way. */
 size_t lsm_may_contain_workspace_bytes(uint32_t nfile, uint64_t nkeys);
 int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
