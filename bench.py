@@ -233,7 +233,8 @@ def bench_decode(args, world, rank, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "decode_v2_kernel<KV,8>",
+            "kernel": ("lsm_wal_replay (seg + stitch + compact launches)" if args.config == "wal"
+                       else "decode_v2_kernel<KV,8>"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

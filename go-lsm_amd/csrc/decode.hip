@@ -2132,17 +2132,23 @@ __global__ __launch_bounds__(64) void wal_seg_kernel(WalArgs a) {
 // The result is the serial chase of [g, E) for any input (exact check order
 // of kv.go:77-115); the segment is read from an LDS copy (plus 4 KiB past
 // its end) and past that through a range-checked buffer resource.
-constexpr uint32_t kWalStage = kWalSeg + 4096;
+// LDS copy of a segment plus a tail for the chains that cross its end.  The
+// copy sets the occupancy (160 KiB LDS per CU): + 1 KiB admits 9 waves per CU
+// and measured 603 GiB/s on the wal bench; + 3.5 KiB (8 waves) 552 and + 4 KiB
+// (20,496 B: 7 waves) 542.  Reads past the tail go through the buffer resource.
+constexpr uint32_t kWalStage = kWalSeg + 1024;
+constexpr uint32_t kWalStage4k = kWalSeg + 4096;  // LSM_WAL_KERNEL=stage4k (A/B)
 
 struct WalLog {
     rsrc_t r;       // the log's bytes, offsets relative to the aligned base
     uint32_t h;     // log start inside the base
     uint32_t len;
-    uint32_t s0;    // LDS copy covers resource offsets [s0, s0 + kWalStage)
+    uint32_t s0;    // LDS copy covers resource offsets [s0, s0 + sz)
+    uint32_t sz;
     const uint32_t *lds;
     __device__ __forceinline__ uint32_t rd32(uint32_t x) const {  // bytes [x, x+4) of the log
         const uint32_t o = h + x;
-        if (o >= s0 && o + 8 <= s0 + kWalStage) {
+        if (o >= s0 && o + 8 <= s0 + sz) {
             const uint32_t q = o - s0;
             return funnel(lds[q >> 2], lds[(q >> 2) + 1], q);
         }
@@ -2197,9 +2203,9 @@ struct WalLog {
 // One wave serves both phases of a segment: the shares' chains do not depend
 // on the segment's entry, only lane 0's does, so they are chased once and
 // stitched twice (from g and from g read as a value length).
-template <bool STAGE>
+template <uint32_t STAGE>  // bytes copied to LDS (0: read through the caches)
 __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE ? kWalStage / 4 + 4 : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE ? STAGE / 4 + 4 : 4];
     const uint32_t s = blockIdx.x, w = blockIdx.y, lane = lane_id();
     const uint32_t len = uni(a.wal_len[w]);
     const uint64_t off = uni64(a.wal_off[w]);
@@ -2215,11 +2221,12 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     L.len = len;
     L.r = make_rsrc(a.wal + base, (L.h + len + 15) & ~15u);
     L.s0 = STAGE ? (L.h + start) & ~15u : 0xFFFFFFF0u;
+    L.sz = STAGE;
     L.lds = stage;
     if (STAGE) {
-        for (uint32_t c = 0; c < kWalStage / 16; c += kWave) {  // the segment + 4 KiB
+        for (uint32_t c = 0; c < STAGE / 16; c += kWave) {  // the segment + a tail
             const uint32_t o = L.s0 + 16 * (c + lane);
-            if (c + lane < kWalStage / 16)
+            if (c + lane < STAGE / 16)
                 *reinterpret_cast<u32x4 *>(&stage[4 * (c + lane)]) = ld_b128(L.r, o);
         }
         __syncthreads();
@@ -2431,7 +2438,59 @@ __global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
         const WalSeg T0 = sl < nseg ? a.seg[q0] : WalSeg{0, 0, 0, 0};
         const WalSeg T1 = sl < nseg ? a.seg[q0 + 1] : WalSeg{0, 0, 0, 0};
         uint32_t f_pre = 0, f_cnt = 0;
-        for (uint32_t j = 0; j < kWave && s0 + j < nseg; j++) {
+        // fast form: segment j's choice of chain (0, 1; 2 = neither, or the
+        // previous chain runs past segment j's end) is a function of segment
+        // j-1's choice; a 6-step scan composes these maps across the 64
+        // segments of the group, as wal_seg_lanes_kernel does across shares.
+        // Any miss before the first error falls back to the serial walk.
+        bool fast = false;
+        if (!dead && s0 < nseg) {
+            const uint32_t gl = nseg - s0 < kWave ? nseg - s0 : kWave;  // live segments
+            const bool live = lane < gl;
+            const uint32_t send = (sl + 1) * kWalSeg;
+            auto match = [&](uint32_t x) -> uint32_t {
+                return x >= send ? 2u : x == T0.entry ? 0u : x == T1.entry ? 1u : 2u;
+            };
+            const uint32_t xp0 = __shfl_up(T0.exit, 1), xp1 = __shfl_up(T1.exit, 1);
+            uint32_t h;
+            if (lane == 0) {
+                const uint32_t c = match(e);
+                h = c | c << 4;
+            } else {
+                h = match(xp0) | match(xp1) << 4;
+            }
+#pragma unroll
+            for (uint32_t d = 1; d < kWave; d <<= 1) {
+                const uint32_t pv = __shfl_up(h, d);
+                if (lane >= d) {  // h := h o pv
+                    const uint32_t p0 = pv & 15, p1 = pv >> 4;
+                    const uint32_t n0 = p0 == 2 ? 2u : p0 == 0 ? (h & 15) : (h >> 4);
+                    const uint32_t n1 = p1 == 2 ? 2u : p1 == 0 ? (h & 15) : (h >> 4);
+                    h = n0 | n1 << 4;
+                }
+            }
+            const uint32_t ch = h & 15;
+            const int32_t cst = ch == 0 ? T0.status : T1.status;
+            const uint64_t errm = __ballot(live && ch < 2 && cst != LSM_OK);
+            const uint32_t lim = errm ? (uint32_t)__builtin_ctzll(errm) : gl - 1;
+            const uint64_t below = lim >= kWave - 1 ? ~0ull : (2ull << lim) - 1;  // lanes <= lim
+            if (!(__ballot(live && ch == 2) & below)) {
+                fast = true;
+                const bool take = live && lane <= lim;
+                const uint32_t nr = take ? (ch == 0 ? T0.nrec : T1.nrec) : 0u;
+                const uint32_t xe = ch == 0 ? T0.exit : T1.exit;
+                uint32_t sum;
+                f_pre = total + wave_excl_scan(nr, &sum);
+                f_cnt = nr | (take && ch == 1 ? 0x80000000u : 0u);
+                total += uni(sum);
+                e = uni(__builtin_amdgcn_readlane(xe, lim));
+                if (errm) {
+                    status = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)cst, lim));
+                    dead = true;
+                }
+            }
+        }
+        for (uint32_t j = 0; !fast && j < kWave && s0 + j < nseg; j++) {
             const uint32_t s = s0 + j;
             uint32_t pre = total, cnt = 0;
             if (!dead && e < len && e < (s + 1) * kWalSeg) {
@@ -2675,9 +2734,11 @@ extern "C" int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t
     if (wk && !strcmp(wk, "serial"))
         hipLaunchKernelGGL(wal_seg_kernel, dim3(2 * a.segs, nwal), dim3(kWave), 0, s, a);
     else if (wk && !strcmp(wk, "lanes"))  // shares read through the caches, no LDS copy
-        hipLaunchKernelGGL(wal_seg_lanes_kernel<false>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL(wal_seg_lanes_kernel<0>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
+    else if (wk && !strcmp(wk, "stage4k"))
+        hipLaunchKernelGGL(wal_seg_lanes_kernel<kWalStage4k>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
     else
-        hipLaunchKernelGGL(wal_seg_lanes_kernel<true>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL(wal_seg_lanes_kernel<kWalStage>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_stitch_kernel, dim3(nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_compact_kernel, dim3(a.segs, nwal), dim3(256), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
