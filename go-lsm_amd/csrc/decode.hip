@@ -2224,7 +2224,9 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     L.sz = STAGE;
     L.lds = stage;
     if (STAGE) {
-        for (uint32_t c = 0; c < STAGE / 16; c += kWave) {  // the segment + a tail
+        // the segment + a tail (the loads are already all in flight: staging
+        // by buffer_load ... lds measured no faster)
+        for (uint32_t c = 0; c < STAGE / 16; c += kWave) {
             const uint32_t o = L.s0 + 16 * (c + lane);
             if (c + lane < STAGE / 16)
                 *reinterpret_cast<u32x4 *>(&stage[4 * (c + lane)]) = ld_b128(L.r, o);
