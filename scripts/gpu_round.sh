@@ -8,7 +8,7 @@ OUT=gpurun_out
 TAG=${TAG:-r01}
 mkdir -p $OUT
 export TMPDIR=/tmp
-step() { local name=$1 lim=$2; shift 2; echo "== $name"; timeout -k 10 $lim "$@"; }
+step() { local name=$1 lim=$2; shift 2; echo "== $name" >&2; timeout -k 10 $lim "$@"; }
 
 step pytest 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1 \
   || { tail -60 $OUT/pytest_gpu_$TAG.log; exit 1; }
