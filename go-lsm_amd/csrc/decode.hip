@@ -2137,6 +2137,9 @@ __global__ __launch_bounds__(64) void wal_seg_kernel(WalArgs a) {
 // and measured 603 GiB/s on the wal bench; + 3.5 KiB (8 waves) 552 and + 4 KiB
 // (20,496 B: 7 waves) 542.  Reads past the tail go through the buffer resource.
 constexpr uint32_t kWalStage = kWalSeg + 1024;
+#ifndef LSM_WAL_DBG
+#define LSM_WAL_DBG 0  // timing diagnostics only: 1 skips the write-out, 2 phase 1
+#endif
 constexpr uint32_t kWalStage4k = kWalSeg + 4096;  // LSM_WAL_KERNEL=stage4k (A/B)
 
 struct WalLog {
@@ -2269,7 +2272,7 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     if (e0 != 0xFFFFFFFFu && e0 < se) L.chase(e0, se, c0, x0, st0);
     if (e1 != 0xFFFFFFFFu && e1 < se) L.chase(e1, se, c1, x1, st1);
     // 2. + 3. per phase: stitch from the entry, then write the accepted chains
-    for (uint32_t ph = 0; ph < 2; ph++) {
+    for (uint32_t ph = 0; ph < ((LSM_WAL_DBG & 2) ? 1 : 2); ph++) {
         const uint64_t q = q0 + ph;
         const uint32_t gp = ph ? g1 : g;
         if (ph == 1 && s == 0) {  // segment 0 starts at 0
@@ -2389,7 +2392,7 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         }
         uint32_t tot;
         const uint32_t pre = wave_excl_scan(acc_cnt, &tot);
-        if (acc_cnt) {
+        if (acc_cnt && !(LSM_WAL_DBG & 1)) {
             u32x4 *dst = a.scratch + q * kWalSegSlots + pre;
             uint32_t p = acc_entry;
             for (uint32_t i = 0; i < acc_cnt; i++) {

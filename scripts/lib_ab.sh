@@ -7,6 +7,7 @@ mkdir -p gpurun_out
 orig=$(mktemp); cp go-lsm_amd/liblsm_gpu.so $orig
 trap 'cp $orig go-lsm_amd/liblsm_gpu.so' EXIT
 for v in $VARIANTS; do
+  [ -z "$K" ] && break  # K empty: timing-only variants, no parity
   cp build_var/liblsm_gpu_$v.so go-lsm_amd/liblsm_gpu.so
   timeout -k 10 300 python -u -m pytest tests -m gpu -q -k "$K" --timeout 120 --timeout-method thread \
       -p no:cacheprovider > gpurun_out/libab_test_$v.log 2>&1 || { tail -30 gpurun_out/libab_test_$v.log; exit 1; }
