@@ -1640,6 +1640,8 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             if (!strcmp(e, "large8")) return 40;
             if (!strcmp(e, "v2split")) return 41;
             if (!strcmp(e, "v2r4")) return 42;
+            if (!strcmp(e, "v2r6")) return 43;
+            if (!strcmp(e, "v2r5")) return 44;
             if (!strcmp(e, "spec_w1")) return 31;
             if (!strcmp(e, "spec_w2")) return 32;
             if (!strcmp(e, "pipe")) return 33;
@@ -1664,6 +1666,8 @@ int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
             return rc ? rc : launch_large<G, kLargeNCH>(ctx, b, s);
         }
         case 42: return launch_v2<G, kNChunk>(a, s);
+        case 43: return launch_v2<G, 6>(a, s);
+        case 44: return launch_v2<G, 5>(a, s);
         case 40: {
             DecodeArgs b = a;
             b.split = 1;
