@@ -2010,7 +2010,10 @@ __global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
 //   wal_compact_kernel: each segment's records move to their final slots.
 // The result equals one serial chase for any input; guesses only decide how
 // much is chased twice.
-constexpr uint32_t kWalSeg = 16 * 1024;
+#ifndef LSM_WAL_SEG_KIB
+#define LSM_WAL_SEG_KIB 16  // other sizes: diagnostic builds only (an open parity item)
+#endif
+constexpr uint32_t kWalSeg = LSM_WAL_SEG_KIB * 1024;
 constexpr uint32_t kWalSegSlots = kWalSeg / 8 + 1;  // records starting in a segment
 
 struct WalSeg {
@@ -2273,8 +2276,12 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
             if ((uint64_t)e0 + 4 + v <= len) e1 = e0 + 4 + v;
         }
     }
-    if (e0 != 0xFFFFFFFFu && e0 < se) L.chase(e0, se, c0, x0, st0);
-    if (e1 != 0xFFFFFFFFu && e1 < se) L.chase(e1, se, c1, x1, st1);
+    // A guess at or past the share's end is a chain with no records that
+    // passes its position through (exit = the guess); chase() returns exactly
+    // that.  Leaving its exit unset once made a share holding only a value
+    // field report exit 0 when the previous chain ended on that guess.
+    if (e0 != 0xFFFFFFFFu) L.chase(e0, se, c0, x0, st0);
+    if (e1 != 0xFFFFFFFFu) L.chase(e1, se, c1, x1, st1);
     // 2. + 3. per phase: stitch from the entry, then write the accepted chains
     for (uint32_t ph = 0; ph < ((LSM_WAL_DBG & 2) ? 1 : 2); ph++) {
         const uint64_t q = q0 + ph;

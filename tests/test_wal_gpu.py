@@ -136,3 +136,33 @@ def test_bench_sized_replay(ctx):
     for w in range(64):
         st, od, _ = ora.decode_block(lsmgpu.GRAMMAR_KV, buf, int(off[w]), int(ln[w]))
         assert st == 0 and np.array_equal(desc[bases[w]:bases[w] + nrec[w]], od), w
+
+
+def test_record_spanning_last_share_of_a_segment(ctx):
+    """A segment's last lane share (the 64 bytes before a 16 KiB boundary)
+    holding a record's value-length field but no record start: the guess
+    from that field (phase 1 of the share) leads exactly to the next record
+    start, past the share.  That chain has no records and must pass the
+    position through (it once reported exit 0 and the log was over-counted).
+    Records of 8 B keys and 90-140 B ASCII values make the case common."""
+    rng = np.random.Generator(np.random.PCG64(77))
+    logs, hits = [], 0
+    for _ in range(3):
+        parts, pos, vfields, starts = [], 0, [], []
+        while pos < 256 * 1024:
+            i = len(starts)
+            k = b"key%05d" % (i % 100000)
+            v = bytes(rng.integers(97, 123, int(rng.integers(90, 141))).astype(np.uint8))
+            starts.append(pos)
+            vfields.append(pos + 4 + len(k))
+            parts.append(struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v)
+            pos += 8 + len(k) + len(v)
+        lg = b"".join(parts)
+        st, vf = np.array(starts), np.array(vfields)
+        for b in range(16384, len(lg) - 16384, 16384):
+            if not ((st >= b - 64) & (st < b)).any() and ((vf >= b - 64) & (vf < b)).any():
+                hits += 1
+        logs.append(lg)
+    assert hits >= 3, hits  # the case is exercised
+    status, got = replay_and_check(ctx, logs)
+    assert (status == 0).all()
