@@ -166,3 +166,40 @@ def test_record_spanning_last_share_of_a_segment(ctx):
     assert hits >= 3, hits  # the case is exercised
     status, got = replay_and_check(ctx, logs)
     assert (status == 0).all()
+
+
+def _fuzz_log(rng, nbytes, kmax, vmax, ascii_bytes, vbig):
+    parts, pos = [], 0
+    while pos < nbytes:
+        k = int(rng.integers(0, kmax + 1))
+        v = int(rng.integers(0, vmax + 1))
+        if vbig and rng.random() < 0.02:
+            v = int(rng.integers(4096, 40000))  # values spanning whole shares/segments
+        lo, hi = (97, 123) if ascii_bytes else (0, 256)
+        kb = rng.integers(lo, hi, k).astype(np.uint8).tobytes()
+        vb = rng.integers(lo, hi, v).astype(np.uint8).tobytes()
+        parts.append(struct.pack("<I", k) + kb + struct.pack("<I", v) + vb)
+        pos += 8 + k + v
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("profile", [
+    (16, 100, True, False),    # config-2 record shape
+    (24, 300, True, False),    # records near a share's width
+    (8, 70, False, False),     # binary lengths-look-alike bytes
+    (40, 1200, True, True),    # large values, multi-segment records
+    (4, 12, False, False),     # tiny records (dense guesses)
+])
+def test_fuzz_record_shapes(ctx, profile):
+    """Randomized record shapes against the oracle, intact and cut at a
+    random point (a crash mid-append), so the share guesses, both stitch
+    levels and their fallbacks meet many layouts."""
+    kmax, vmax, ascii_bytes, vbig = profile
+    rng = np.random.Generator(np.random.PCG64(1000 + kmax * 7 + vmax))
+    logs = []
+    for i in range(6):
+        lg = _fuzz_log(rng, int(rng.integers(20_000, 180_000)), kmax, vmax, ascii_bytes, vbig)
+        if i % 2:
+            lg = lg[:int(rng.integers(1, len(lg)))]
+        logs.append(lg)
+    replay_and_check(ctx, logs)
