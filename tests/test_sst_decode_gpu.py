@@ -232,3 +232,32 @@ def test_config3_images(ctx):
         rc, om, *_ = ora.sst_decode(out[o:o + n])
         for name, _ in ora.SstMeta._fields_:
             assert int(meta[f][name]) == int(getattr(om, name)), (f, name)
+
+
+@pytest.mark.parametrize("shape", ["rare_key_break", "wide_values", "tiny_records", "mid_corrupt"])
+def test_fuzz_large_tables(ctx, shape):
+    """Tables large enough to be split over many workgroups, with the
+    stride / offset hypotheses broken rarely (so a break can land on a
+    workgroup boundary) or a byte corrupted somewhere in the middle."""
+    rng = np.random.default_rng(sum(map(ord, shape)))
+    images = []
+    for _ in range(4):
+        n = int(rng.integers(5_000, 16_000))
+        if shape == "rare_key_break":
+            keys = [b"k%015d" % i if rng.random() > 0.001 else b"k%016d" % i for i in range(n)]
+            vals = [rng.integers(0, 256, 100, dtype=np.uint8).tobytes() for _ in range(n)]
+        elif shape == "wide_values":
+            keys, vals = kv_set(rng, n, vmax=600)
+        elif shape == "tiny_records":
+            keys = [rng.integers(97, 123, int(rng.integers(0, 4)), dtype=np.uint8).tobytes() for _ in range(n)]
+            vals = [rng.integers(0, 256, int(rng.integers(0, 5)), dtype=np.uint8).tobytes() for _ in range(n)]
+        else:
+            keys, vals = kv_set(rng, n, vmax=150)
+        im = build(keys, vals)
+        if shape == "mid_corrupt":
+            d_off, d_size, i_off, i_size = footer(im)
+            im = im.copy()
+            at = int(rng.integers(d_off, i_off + i_size))
+            im[at] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        images.append(im)
+    check(ctx, images, seed=11)
