@@ -161,3 +161,22 @@ def test_may_contain_sorted_large_filters(ctx):
         images.append(build(keys, m=1_600_000, k=16))
     probes = [b"L%07d" % int(x) for x in rng.integers(0, 52000, 3000)] + [b"", b"L", b"M"]
     check(ctx, rng, images, probes)
+
+
+def test_may_contain_sorted_shared_long_prefixes(ctx):
+    """Grouped path where every bound shares its first 16+ bytes (the LDS
+    bound prefixes tie and the byte comparison decides): keys "tenant-...-/"
+    + a counter, files disjoint and in order; probes at the bounds, between
+    files, equal to the shared prefix, one byte longer or shorter."""
+    rng = np.random.default_rng(66)
+    pre = b"tenant-00000000000/"  # 19 bytes
+    images, bounds = [], []
+    for f in range(40):
+        keys = sorted({pre + b"%06d" % (f * 1000 + int(x)) for x in rng.integers(0, 900, 25)})
+        images.append(build(keys, m=4096, k=3))
+        bounds += [keys[0], keys[-1]]
+    probes = bounds + [pre + b"%06d" % int(x) for x in rng.integers(0, 41000, 500)]
+    probes += [pre, pre[:16], pre[:15], pre + b"\x00", pre[:16] + b"\xff", pre + b"999999", b""]
+    probes += [pre[:16] + b"%09d" % int(x) for x in rng.integers(0, 10**9, 50)]  # ties, then bytes
+    assert all(bounds[i] < bounds[i + 1] for i in range(len(bounds) - 1))  # sorted, disjoint
+    check(ctx, rng, images, probes)
