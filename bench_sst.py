@@ -52,6 +52,8 @@ def bench_sst(args, world, rank, local):
     # algorithmic bytes: keys + values + CSR offsets read once, images written
     alg = float(keys.size + vals.size + 16 * (n + 1)) + img
     achieved = alg / (kern_ms * 1e-3) / 1e9
+    from bench import traffic_from_profile
+    traffic, tsrc = traffic_from_profile(f"sst:{nf}")
     out = {
         "metric": "GiB/s of .sst image bytes encoded (builder rule + fused bloom)",
         "value": round(img_all * args.steps / elapsed / GIB, 2),
@@ -71,7 +73,8 @@ def bench_sst(args, world, rank, local):
                    "parallelism": f"dp{world} (record ranges per rank, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "lsm_build_sst (bloom + regions + meta)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": tsrc,
                      "alg_bytes_per_launch": int(alg), "kernel_ms": round(kern_ms, 5)},
     }
     return out, (keys, koff, vals, voff, starts)

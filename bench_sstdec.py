@@ -60,6 +60,8 @@ def bench_sst_decode(args, world, rank, local):
     # i64 offset (8 B) and a value view (16 B) written; 112 B meta per file
     alg = parsed + 40.0 * n + 112.0 * nf
     achieved = alg / (kern_ms * 1e-3) / 1e9
+    from bench import traffic_from_profile
+    traffic, tsrc = traffic_from_profile(f"{args.config}:{nf}")
     out = {
         "metric": "GiB/s of .sst data+index region bytes decoded to KV records",
         "value": round(parsed_all * args.steps / elapsed / GIB, 2),
@@ -80,7 +82,8 @@ def bench_sst_decode(args, world, rank, local):
                    "parallelism": f"dp{world} (files per rank, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "lsm_decode_sst (4 launches)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": tsrc,
                      "alg_bytes_per_launch": int(alg), "kernel_ms": round(kern_ms, 5)},
     }
     return out, (sb.out.cpu().numpy(), sb.file_off, sb.file_size, meta)
@@ -156,6 +159,8 @@ def bench_may_contain(args, world, rank, local):
     total = sum_over_ranks(world, float(nprobe))
     fbits = r.meta_numpy()["filter_nbits"].astype(np.float64)
     alg = float(nprobe) * nf + pk.size + 8.0 * (nprobe + 1) + float((8 * np.ceil(fbits / 64)).sum())
+    from bench import traffic_from_profile
+    traffic, tsrc = traffic_from_profile(f"probe:{nf}:{nprobe}")
     out = {
         "metric": "M keys/s probed by SSTable.MayContain against every file",
         "value": round(total * args.steps / elapsed / 1e6, 2),
@@ -173,7 +178,7 @@ def bench_may_contain(args, world, rank, local):
         "roofline": {"bound": "hbm", "kernel": "lsm_may_contain (all launches)",
                      "kernel_ms": round(kern_ms, 5), "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1),
                      "peak": 8000.0, "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / 8000.0, 4),
-                     "traffic": None, "alg_bytes_per_launch": int(alg)},
+                     "traffic": traffic, "traffic_source": tsrc, "alg_bytes_per_launch": int(alg)},
     }
     return out, (sb.out.cpu().numpy(), sb.file_off, r.meta_numpy(), pk, nprobe)
 
