@@ -6,9 +6,13 @@ Default workload (N=1): BASELINE config 2 -- batch-decode 100,000 synthetic
 per 4,096-byte slot), device resident, descriptor output.  One step = one
 lsm_decode_blocks launch over the whole batch.
 
-N>1 (torchrun, one process per GPU): the global batch is N x 100,000 blocks
-dealt round-robin (block i -> rank i mod N); no data-path collective, the
-ranks only meet at the barriers around the timed region (weak scaling).
+N>1 (one process per GPU): BASELINE config 4 -- a fixed global batch of
+1,000,000 blocks dealt round-robin (block i -> rank i mod N; strong scaling,
+`--global-blocks` sets the batch, `--blocks` switches to a per-GPU batch and
+weak scaling).  No data-path collective: the ranks only meet at the barriers
+around the timed region and in two scalar reductions.  Launched by the driver
+under torch.distributed.run; a plain `python bench.py --gpus N` starts that
+launcher itself as a child process before anything touches the GPU.
 
 value = sum of parsed block bytes over all ranks / max-over-ranks wall time.
 """
@@ -24,15 +28,19 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "go-lsm_amd"))
 
-import lsmgpu  # noqa: E402
-from lsmgpu import synth  # noqa: E402
+# lsmgpu (the HIP library) is imported by main() only after the launcher
+# decision: a parent that spawns the rank processes never loads it.
+lsmgpu = None
+synth = None
+
+CONFIG4_GLOBAL_BLOCKS = 1_000_000  # BASELINE.json configs[3]
 
 METRIC = "GiB/s of device-resident .sst data-block bytes decoded to KV records"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
 GIB = float(1 << 30)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -40,7 +48,13 @@ def parse():
     ap.add_argument("--config", default="decode4k",
                     choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal",
                              "probe", "compact"])
-    ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
+    ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU (weak scaling)")
+    ap.add_argument("--global-blocks", type=int, default=None,
+                    help="fixed global batch dealt round-robin over the ranks (strong "
+                         "scaling); default %d for decode4k at N>1 (config 4)"
+                         % CONFIG4_GLOBAL_BLOCKS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher and deal only (gloo, no device work): prints the deal")
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -48,13 +62,42 @@ def parse():
                     help="host-resident blocks: pinned H2D -> decode -> compact -> D2H "
                          "(the PCIe-inclusive rate recorded in DESIGN.md; not the headline)")
     ap.add_argument("--chunk", type=int, default=8192, help="blocks per e2e pipeline chunk")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`python bench.py --gpus N` without a launcher around it: start N rank
+    processes under torch.distributed.run as a CHILD (this process has not
+    touched the GPU and never does), pass rank 0's JSON line through, and
+    return the child's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: "
+                         "launch one process per GPU (torch.distributed.run) or omit WORLD_SIZE")
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        return world, rank, local
     if world > 1 and os.environ.get("LSM_BENCH_REHEARSE"):
         # rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0,
         # gloo for the barrier and the two scalar reductions (never a result)
@@ -98,8 +141,26 @@ def sum_over_ranks(world, x):
 
 
 def shard_block_ids(rank, world, per):
-    """Round-robin deal of the global batch: block i -> rank i mod N."""
+    """Round-robin deal of a global batch of N x per blocks: block i -> rank i mod N."""
     return rank + world * np.arange(per, dtype=np.int64)
+
+
+def deal_global(rank, world, total):
+    """Round-robin deal of a fixed global batch of `total` blocks (config 4):
+    rank r gets blocks r, r+N, r+2N, ... < total."""
+    return np.arange(rank, total, world, dtype=np.int64)
+
+
+def block_ids_for(args, world, rank):
+    """This rank's global block ids and the scaling mode of the line."""
+    per_default = 100_000 if args.config == "decode4k" else 6_400
+    total = args.global_blocks
+    if total is None and args.blocks is None and world > 1 and args.config == "decode4k":
+        total = CONFIG4_GLOBAL_BLOCKS
+    if total is not None:
+        return deal_global(rank, world, total), "strong", total
+    per = args.blocks or per_default
+    return shard_block_ids(rank, world, per), "weak", per * world
 
 
 def traffic_from_profile(workload_key):
@@ -120,17 +181,22 @@ def traffic_from_profile(workload_key):
     return best if best else (None, None)
 
 
+UNIFORM = {"decode4k": dict(recs=33, slot=4096), "decode64k": dict(recs=528, slot=65536)}
+
+
 def make_workload(args, world, rank):
     if args.config in ("decode4k", "decode64k"):
-        per = args.blocks or (100_000 if args.config == "decode4k" else 6_400)
-        ids = shard_block_ids(rank, world, per)
-        if args.config == "decode4k":
-            buf, off, ln = synth.uniform_kv_blocks(ids)
-            desc = "decode %d x 4 KiB KV blocks per GPU (33 x 16 B key / 100 B value)" % per
+        ids, scaling, total = block_ids_for(args, world, rank)
+        shape = UNIFORM[args.config]
+        # 4 KiB: 33 x 124 B = 4,092 parsed bytes; 64 KiB: 528 x 124 B = 65,472
+        buf, off, ln = synth.uniform_kv_blocks(ids, **shape)
+        kib = shape["slot"] // 1024
+        if scaling == "strong":
+            desc = (f"decode {total} x {kib} KiB KV blocks ({shape['recs']} x 16 B key / 100 B "
+                    f"value) dealt round-robin over {world} GPU(s)")
         else:
-            # 64 KiB slots: 528 records x 124 B = 65,472 parsed bytes
-            buf, off, ln = synth.uniform_kv_blocks(ids, recs=528, slot=65536)
-            desc = "decode %d x 64 KiB KV blocks per GPU (528 x 16 B key / 100 B value)" % per
+            desc = (f"decode {ids.size} x {kib} KiB KV blocks per GPU ({shape['recs']} x 16 B "
+                    "key / 100 B value)")
         return buf, off, ln, desc
     if args.config == "mixed":
         total = (args.blocks or 1 << 30)
@@ -192,11 +258,16 @@ def bench_decode(args, world, rank, local):
     barrier(world)
     t1 = time.perf_counter()
     elapsed = max_over_ranks(world, t1 - t0)
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    times = np.array([s.elapsed_time(e) for s, e in zip(starts, ends)])
+    # the timed output is checked after the timed region: the line fails on a
+    # single wrong descriptor (kv/kv.go:77-115 record chain, closed form)
+    verify_decode(args, r, d_off, d_len, nblk)
 
     parsed = float(blk_len.astype(np.float64).sum())
     parsed_all = sum_over_ranks(world, parsed)
     value = parsed_all * args.steps / elapsed / GIB
+    scaling = block_ids_for(args, world, rank)[1] if args.config in UNIFORM else "weak"
 
     # algorithmic bytes of one launch: block bytes +
     # per-block metadata (blk_off 8 + blk_len 4) read; 16 B per record
@@ -205,6 +276,7 @@ def bench_decode(args, world, rank, local):
     alg = parsed + 12.0 * nblk + 16.0 * nrec_total + 8.0 * nblk
     if args.arena:
         alg += float(nrec_total) * (16 + 100) if args.config != "mixed" else parsed
+    kern_ms = float(times.mean())
     achieved = alg / (kern_ms * 1e-3) / 1e9
     wkey = f"{args.config}:{nblk}:{'arena' if args.arena else 'desc'}"
     traffic, tsrc = traffic_from_profile(wkey)
@@ -217,10 +289,11 @@ def bench_decode(args, world, rank, local):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seed 0x5EED, keys k%015d, splitmix64 values)",
+        "verified": "every record descriptor, nrec and status of the timed output (closed form)",
         "config": {
             "workload": wdesc,
             "grammar": "KV (kv/kv.go:46-115)",
@@ -243,9 +316,58 @@ def bench_decode(args, world, rank, local):
             "traffic_source": tsrc,
             "alg_bytes_per_launch": int(alg),
             "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_median": round(float(np.median(times)), 5),
+            "kernel_ms_min": round(float(times.min()), 5),
         },
     }
     return out, (buf, blk_off, blk_len)
+
+
+def verify_decode(args, r, d_off, d_len, nblk):
+    """Check the decode output the timed region produced, on the device.
+
+    For every block: status 0, records chained back to back from blk_off
+    (record j+1 starts where record j ends: 8 + klen + vlen bytes later,
+    kv/kv.go:77-115), the chain ending exactly at blk_off + blk_len.  For the
+    uniform configs also the closed form: nrec, klen = 16, vlen = 100, record j
+    at blk_off + 124 j.  WAL replay output is dense per log (checked the same
+    way through its own nrec)."""
+    if args.config == "wal":
+        return
+    dev = r.nrec.device
+    nrec = r.nrec[:nblk].to(torch.int64)
+    assert int((r.status[:nblk] != 0).sum()) == 0, "decode reported errors"
+    off = d_off.to(torch.int64)
+    ln = d_len.to(torch.int64) & 0xFFFFFFFF
+    base = off // lsmgpu.codec.MIN_RECORD[lsmgpu.GRAMMAR_KV]
+    chunk = 1 << 16
+    for b0 in range(0, nblk, chunk):
+        b1 = min(nblk, b0 + chunk)
+        n = nrec[b0:b1]
+        tot = int(n.sum())
+        blk = torch.repeat_interleave(torch.arange(b0, b1, device=dev), n)
+        first = torch.cumsum(n, 0) - n
+        j = torch.arange(tot, device=dev) - torch.repeat_interleave(first, n)
+        slot = base[blk] + j
+        d = r.desc[slot].to(torch.int64)
+        rec_off = (d[:, 0] & 0xFFFFFFFF) | (d[:, 1] << 32)
+        klen, vlen = d[:, 2] & 0xFFFFFFFF, d[:, 3] & 0xFFFFFFFF
+        end = rec_off + 8 + klen + vlen
+        # chain: first record at blk_off, each next one at the previous end
+        starts_ok = torch.where(j == 0, rec_off == off[blk],
+                                rec_off == torch.roll(end, 1))
+        assert bool(starts_ok.all()), "decode: record chain broken"
+        last = torch.cumsum(n, 0) - 1
+        nz = n > 0
+        assert bool((end[last[nz]] == (off[b0:b1] + ln[b0:b1])[nz]).all()), \
+            "decode: chain does not end at blk_off + blk_len"
+        assert bool((ln[b0:b1][~nz] == 0).all()), "decode: empty output for a non-empty block"
+        if args.config in UNIFORM:
+            recs = UNIFORM[args.config]["recs"]
+            assert bool((n == recs).all()), "decode: nrec"
+            assert bool(((klen == 16) & (vlen == 100)).all()), "decode: record lengths"
+            assert bool((rec_off == off[blk] + 124 * j).all()), "decode: record offsets"
+
 
 
 def bench_e2e(args, world, rank, local):
@@ -340,6 +462,44 @@ def bench_e2e(args, world, rank, local):
     }
 
 
+def host_cpu():
+    """The host cores a CPU baseline may use, and what they are.
+
+    On the GPU box `nproc` / os.cpu_count() report the whole machine while the
+    job's CPU share is OMP_NUM_THREADS (16 per GPU); the baselines use that
+    share (capped by the affinity mask) and record all three numbers."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or affinity
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": max(1, min(share, affinity)), "nproc": os.cpu_count(),
+            "affinity": affinity, "model": model}
+
+
+def timed_threads(fn, items, threads, budget):
+    """Run fn(item) over items on `threads` host threads (ctypes releases the
+    GIL, so the C restatement runs in parallel), repeating whole passes until
+    `budget` seconds have passed.  -> (passes, seconds)."""
+    from concurrent.futures import ThreadPoolExecutor
+    passes, t = 0, 0.0
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        while t < budget or passes == 0:
+            t0 = time.perf_counter()
+            list(ex.map(fn, items))
+            t += time.perf_counter() - t0
+            passes += 1
+    return passes, t
+
+
 def cpu_baseline(args, data):
     """The oracle's Go-pattern decode (fresh heap buffer per key and value,
     append-grown slices; oracle/lsm_oracle.c) timed on this host's cores."""
@@ -347,7 +507,8 @@ def cpu_baseline(args, data):
     import pyoracle as ora
 
     buf, blk_off, blk_len = data
-    threads = min(16, os.cpu_count() or 1)
+    cpu = host_cpu()
+    threads = cpu["threads"]
     parsed = float(blk_len.astype(np.float64).sum())
 
     def timed(th, nb, budget):
@@ -372,12 +533,50 @@ def cpu_baseline(args, data):
         "sample": f"full workload ({blk_off.size} blocks, {recs} records) x {reps} passes "
                   f"in {t:.1f} s on {threads} threads; 1-thread: {nb1} blocks x {reps1} passes",
         "value_1t": round(p1 * reps1 / t1 / GIB, 3),
+        "host": cpu,
     }
 
 
-def main():
-    args = parse()
+def dry_run(args, world, rank):
+    """--dry-run: the launcher and the deal without device work (CPU, gloo).
+    Rank 0 prints the deal: blocks per rank and checksums of the dealt ids."""
+    if args.config in UNIFORM:
+        ids, scaling, total = block_ids_for(args, world, rank)
+    else:
+        ids, scaling, total = np.arange(rank, rank + 1, dtype=np.int64), "weak", world
+    assert bool((ids % world == rank).all())
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([ids.size, int(ids.sum()), int((ids.astype(np.float64) ** 2).sum())],
+                         dtype=torch.float64)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        rows = [p.tolist() for p in parts]
+    else:
+        rows = [[ids.size, int(ids.sum()), float((ids.astype(np.float64) ** 2).sum())]]
+    return {"dry_run": True, "n_gpus": world, "config": args.config, "scaling": scaling,
+            "global_blocks": total, "blocks_per_rank": [int(r[0]) for r in rows],
+            "id_sum": int(sum(r[1] for r in rows)), "id_sumsq": float(sum(r[2] for r in rows)),
+            "pid": os.getpid()}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
     world, rank, local = dist_setup(args)
+    if args.dry_run:
+        out = dry_run(args, world, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    global lsmgpu, synth
+    import lsmgpu as _lsmgpu
+    lsmgpu, synth = _lsmgpu, _lsmgpu.synth
     if args.e2e:
         out = bench_e2e(args, world, rank, local)
         if rank == 0:

@@ -47,7 +47,7 @@ extern "C" int lsm_dev_alloc(lsm_ctx *ctx, size_t bytes, void **out) {
     *out = nullptr;
     int rc = bind(ctx);
     if (rc) return rc;
-    size_t n = ((bytes + 15) & ~(size_t)15) + 16;
+    size_t n = ((bytes + 15) & ~(size_t)15) + LSM_INPUT_SLACK;  // include/lsm_gpu.h
     LSM_HIP_CHECK(hipMalloc(out, n));
     return 0;
 }

@@ -1213,6 +1213,11 @@ constexpr uint32_t kMcTile = 64;
 constexpr uint32_t kMcThreads = 256;
 constexpr uint32_t kMcRow = kMcTile / 4 + 1;  // dwords per out-tile row (+1: LDS banks)
 
+// Filter.Test tests hashNum locations and stops at the first clear bit; a
+// stored k beyond this (only a corrupted file) is capped so a probe of a
+// saturated filter ends (deviations).
+constexpr uint32_t kMcMaxK = 1u << 24;
+
 struct McFile {
     uint32_t lo[4], hi[4];  // first 16 bytes of min / max key, big-endian, zero padded
     uint32_t lo_len, hi_len;
@@ -1315,9 +1320,10 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
             F.lo_at = fo + M.min_key_off;
             F.hi_at = fo + M.max_key_off;
             F.words_at = fo + M.filter_words_off;
-            // k from the file (no max(1, k) on a decoded filter); a corrupted
-            // k is capped so a probe always ends
-            F.k = M.filter_k < 4096 ? (uint32_t)M.filter_k : 4096;
+            // k from the file (no max(1, k) on a decoded filter); Test's
+            // early exit ends a probe at its first clear bit, a corrupted k
+            // beyond kMcMaxK is capped (deviations)
+            F.k = M.filter_k < kMcMaxK ? (uint32_t)M.filter_k : kMcMaxK;
             F.m = M.filter_m;
             F.mr = M.filter_m ? ~0ull / M.filter_m : 0;
             F.nbits = M.filter_nbits;
@@ -1328,7 +1334,10 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
         bool sorted = true;
         if (threadIdx.x < nt) {
             const McFile &A = tile[threadIdx.x];
-            sorted = A.ok != 0;
+            // MinKey <= MaxKey too: a corrupted header with min > max breaks
+            // the order the binary search relies on
+            sorted = A.ok != 0 &&
+                     bound_cmp_fast(A.lo, A.lo_len, img + A.lo_at, A.hi, A.hi_len, img + A.hi_at) <= 0;
             if (sorted && threadIdx.x + 1 < nt) {
                 const McFile &B = tile[threadIdx.x + 1];
                 sorted = B.ok && bound_cmp_fast(A.hi, A.hi_len, img + A.hi_at, B.lo, B.lo_len,
@@ -1357,7 +1366,10 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
                 if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0 &&
                     bound_cmp_fast(F.hi, F.hi_len, img + F.hi_at, kw, kl, kp) >= 0) {
                     const uint64_t m = F.m;
-                    r = m != 0;  // m == 0: Go's location() divides by zero
+                    // hashNum 0: Test is true (bloom.go:373 loop never runs);
+                    // m == 0 with k > 0: Go's location() divides by zero and
+                    // panics, answered false here
+                    r = F.k == 0 || m != 0;
                     // Test's answer is the AND of all k bits (its early exit
                     // changes nothing): sixteen loads in flight at a time
                     for (uint32_t j0 = 0; j0 < F.k && r && !nobloom; j0 += 16) {
@@ -1440,7 +1452,7 @@ __device__ __forceinline__ McFile mc_file(const uint8_t *img, const uint64_t *fi
     F.lo_at = fo + M.min_key_off;
     F.hi_at = fo + M.max_key_off;
     F.words_at = fo + M.filter_words_off;
-    F.k = M.filter_k < 4096 ? (uint32_t)M.filter_k : 4096;
+    F.k = M.filter_k < kMcMaxK ? (uint32_t)M.filter_k : kMcMaxK;
     F.m = M.filter_m;
     F.mr = M.filter_m ? ~0ull / M.filter_m : 0;
     F.nbits = M.filter_nbits;
@@ -1456,8 +1468,10 @@ __global__ __launch_bounds__(256) void mc_prep_kernel(const uint8_t *img, const 
         w.files[f] = F;
         w.hist[f] = 0;
         w.cursor[f] = 0;
-        // m < 2^63 for the Barrett reduction
-        ok = ok && F.ok && F.m < (1ull << 63);
+        // m < 2^63 for the Barrett reduction; MinKey <= MaxKey (a corrupted
+        // header with min > max would break the order of the bound search)
+        ok = ok && F.ok && F.m < (1ull << 63) &&
+             bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, F.hi, F.hi_len, img + F.hi_at) <= 0;
     }
     if (nfile > kMcMaxFiles) ok = false;
     __syncthreads();
@@ -1689,7 +1703,8 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
             n0 = w.hash[4 * (uint64_t)in]; n1 = w.hash[4 * (uint64_t)in + 1];
             n2 = w.hash[4 * (uint64_t)in + 2]; n3 = w.hash[4 * (uint64_t)in + 3];
         }
-        uint32_t r = F.m != 0;  // m == 0: Go's location() divides by zero
+        // k == 0: true; m == 0 < k: Go panics, answered false
+        uint32_t r = F.k == 0 || F.m != 0;
         // Test is the AND of all k bits (its early exit changes nothing):
         // sixteen bit reads in flight at a time
         for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {

@@ -46,7 +46,7 @@ void check(int rc, const char *what) {
 
 const char *eof_or_unexpected(size_t got) { return got == 0 ? "EOF" : "unexpected EOF"; }
 
-size_t pad16(size_t n) { return ((n + 15) & ~(size_t)15) + 16; }
+size_t pad16(size_t n) { return ((n + 15) & ~(size_t)15) + LSM_INPUT_SLACK; }
 
 // One-launch batch decode of host blocks; descriptors come back per block.
 struct Decoded {

@@ -45,9 +45,12 @@ def _stream_handle(stream: Optional[torch.cuda.Stream]):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+INPUT_SLACK = 32  # LSM_INPUT_SLACK, include/lsm_gpu.h
+
+
 def pad16(n: int) -> int:
-    """Device inputs must be readable to the next 16-byte multiple (+16 slack)."""
-    return ((n + 15) // 16) * 16 + 16
+    """Device inputs must be readable to roundup16(n) + LSM_INPUT_SLACK."""
+    return ((n + 15) // 16) * 16 + INPUT_SLACK
 
 
 def to_device_bytes(buf: np.ndarray, device) -> torch.Tensor:

@@ -8,9 +8,12 @@
  * allocation and no host synchronisation (hipGraph-capturable); the caller
  * owns every buffer and the library keeps no pointer after the call returns.
  *
- * Device input buffers must be readable up to the next multiple of 16 bytes
- * past the last block byte (the kernels stream 16-byte aligned chunks; the
- * bytes past a block are never interpreted).
+ * Device input buffers (blocks, images, logs, key and value arenas) must be
+ * readable up to LSM_INPUT_SLACK bytes past the next multiple of 16 bytes
+ * after their last byte: roundup16(n) + 32.  The kernels stream 16-byte
+ * aligned chunks, and key hashing / bound prefixes load 8-byte words at any
+ * key start (up to key_start + 20 for a key ending the buffer).  Bytes past a
+ * block or key are never interpreted.  lsm_dev_alloc pads by this much.
  *
  * Return convention: 0 = ok; negative = LSM_E* (argument error) or
  * -(1000 + hipError_t) for a HIP runtime error.
@@ -26,6 +29,7 @@ extern "C" {
 #endif
 
 #define LSM_ABI_VERSION 2
+#define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
 /* Record grammars (all fixed-width little-endian). */
 enum lsm_grammar {

@@ -253,6 +253,19 @@ int ora_bloom_test(const uint64_t *words, uint64_t m, uint64_t k, const uint8_t 
     return 1;
 }
 
+int ora_filter_test(const uint64_t *words, uint64_t nbits, uint64_t m, uint64_t k,
+                    const uint8_t *key, uint64_t len) {
+    uint64_t h[4];
+    ora_sum256(key, len, h);                       /* baseHashes, bloom.go:372 */
+    for (uint64_t i = 0; i < k; i++) {             /* bloom.go:373, no max(1,k) */
+        if (m == 0) return -1;                     /* location(): % 0 panics    */
+        uint64_t p = ora_location(h, i) % m;       /* bloom.go:139-141          */
+        if (p >= nbits) return 0;                  /* bitset.Test past length   */
+        if (!(words[p >> 6] >> (p & 63) & 1)) return 0;
+    }
+    return 1;
+}
+
 void ora_estimate_parameters(uint64_t n, double p, uint64_t *m, uint64_t *k) {
     double ln2 = log(2.0);
     *m = (uint64_t)ceil(-1.0 * (double)n * log(p) / pow(ln2, 2));

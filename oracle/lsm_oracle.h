@@ -105,6 +105,12 @@ void ora_bloom_add(uint64_t *words, uint64_t m, uint64_t k, const uint8_t *key, 
 /* Filter.Test bloom.go:371-379. */
 int ora_bloom_test(const uint64_t *words, uint64_t m, uint64_t k, const uint8_t *key,
                    uint64_t len);
+/* Filter.Test bloom.go:371-379 on a DECODED filter (ReadFrom :262-281 keeps
+ * m and k as stored, no max(1, .)): k == 0 -> 1; bitset.Test is false at and
+ * past the stored bit count nbits; m == 0 < k -> -1 (Go panics: location()'s
+ * `% arraySize` divides by zero). */
+int ora_filter_test(const uint64_t *words, uint64_t nbits, uint64_t m, uint64_t k,
+                    const uint8_t *key, uint64_t len);
 /* EstimateParameters bloom.go:145-149. */
 void ora_estimate_parameters(uint64_t n, double p, uint64_t *m, uint64_t *k);
 

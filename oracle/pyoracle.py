@@ -51,6 +51,7 @@ def lib():
         "ora_location": (u64, [vp, u64]),
         "ora_bloom_add": (None, [vp, u64, u64, vp, u64]),
         "ora_bloom_test": (ctypes.c_int, [vp, u64, u64, vp, u64]),
+        "ora_filter_test": (ctypes.c_int, [vp, u64, u64, u64, vp, u64]),
         "ora_estimate_parameters": (None, [u64, ctypes.c_double, vp, vp]),
         "ora_filter_block_size": (u64, [u64]),
         "ora_filter_encode": (u64, [vp, u64, u64, vp]),
@@ -201,7 +202,14 @@ class Bloom:
         if rc != 0:
             raise ValueError(f"filter decode failed ({rc})")
         f.words = words
+        f.nbits = int(nb.value)
         return f, int(nb.value), int(used.value)
+
+    def test_decoded(self, key):
+        """Filter.Test of a decoded filter: 1, 0, or -1 where Go panics."""
+        d = _bytes(key)
+        return int(lib().ora_filter_test(_p(self.words), self.nbits, self.m, self.k,
+                                         _p(d) if d.size else None, d.size))
 
 
 def estimate_parameters(n, p):

@@ -286,6 +286,46 @@ def test_config2_full_size(ctx):
         assert st == 0 and np.array_equal(d[b * 33:(b + 1) * 33], od)
 
 
+def test_bench_path_config2_full_size(ctx):
+    """Exactly what bench.py times (alloc_decode_offset + decode_into, DESC,
+    offset placement: decode_v2_kernel<KV,8>) on the full 100k config-2 batch:
+    every descriptor in closed form, 256 sampled blocks against the oracle
+    (kv/kv.go:77-115), and repeated launches into the same outputs."""
+    nblk = 100_000
+    buf, blk_off, blk_len = synth.uniform_kv_blocks(np.arange(nblk))
+    dev = ctx.torch_device
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.tensor(blk_off.view(np.int64), device=dev)
+    d_len = torch.tensor(blk_len.view(np.int32), device=dev)
+    r = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()))
+    r.desc.fill_(-1)
+    for _ in range(3):
+        lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r)
+    torch.cuda.synchronize()
+    assert int((r.status[:nblk] != 0).sum()) == 0
+    assert bool((r.nrec[:nblk] == 33).all())
+    # offset placement: block b's records at slots blk_off[b] / 8 = 512 b
+    idx = (torch.arange(nblk, device=dev)[:, None] * 512
+           + torch.arange(33, device=dev)[None, :]).reshape(-1)
+    d = r.desc[idx].cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+    want_off = (np.arange(nblk)[:, None] * 4096 + np.arange(33)[None, :] * 124).reshape(-1)
+    assert np.array_equal(d["rec_off"], want_off.astype(np.uint64))
+    assert (d["key_len"] == 16).all() and (d["val_len"] == 100).all()
+    sample = np.random.default_rng(2).choice(nblk, 256, replace=False)
+    for b in sample:
+        st, od, _ = ora.decode_block(1, buf, int(blk_off[b]), int(blk_len[b]))
+        assert st == 0 and np.array_equal(d[b * 33:(b + 1) * 33], od), b
+    # the bench's own post-run check accepts it and rejects a single bad record
+    import bench
+    import argparse
+    bench.lsmgpu = lsmgpu
+    args = argparse.Namespace(config="decode4k")
+    bench.verify_decode(args, r, d_off, d_len, nblk)
+    r.desc[512 * 777 + 5, 3] = 101
+    with pytest.raises(AssertionError):
+        bench.verify_decode(args, r, d_off, d_len, nblk)
+
+
 def test_config5_mixed_sample(ctx):
     buf, blk_off, blk_len, nrec = synth.mixed_kv_blocks(24 << 20, seed=11)
     dev = ctx.torch_device

@@ -61,3 +61,48 @@ def test_round_robin_shards_and_reductions(world):
         assert tot_recs == world * per * 33
         assert tot_bytes == world * per * 4092
         assert mx == world
+
+
+def _bench_dry(*extra):
+    """Run `python bench.py --dry-run ...` as the driver would (no WORLD_SIZE in
+    the environment) and return rank 0's JSON line and the parent's pid."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", *extra],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT)
+    out, err = p.communicate(timeout=240)
+    assert p.returncode == 0, err.decode()[-2000:]
+    lines = [ln for ln in out.decode().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.decode()
+    return json.loads(lines[0]), p.pid
+
+
+def test_launcher_gpus2_deals_config4_exactly():
+    """`bench.py --gpus 2` launches two rank processes itself (config 4: the
+    fixed 1,000,000-block batch dealt round-robin, block i -> rank i mod 2)."""
+    G = 1_000_000
+    j, parent = _bench_dry("--gpus", "2")
+    assert j["n_gpus"] == 2 and j["scaling"] == "strong" and j["global_blocks"] == G
+    assert j["blocks_per_rank"] == [G // 2, G // 2]
+    assert j["id_sum"] == G * (G - 1) // 2                       # every block once
+    assert j["id_sumsq"] == float((G - 1) * G * (2 * G - 1) // 6)
+    assert j["pid"] != parent                                     # rank 0 is a child
+
+
+def test_launcher_uneven_deal_and_weak_mode():
+    j, _ = _bench_dry("--gpus", "3", "--global-blocks", "10")
+    assert j["blocks_per_rank"] == [4, 3, 3] and j["id_sum"] == 45 and j["id_sumsq"] == 285.0
+    j, _ = _bench_dry("--gpus", "2", "--blocks", "50")
+    assert j["scaling"] == "weak" and j["blocks_per_rank"] == [50, 50] and j["id_sum"] == 99 * 50
+    j, _ = _bench_dry()
+    assert j["n_gpus"] == 1 and j["global_blocks"] == 100_000    # N=1: config 2
+
+
+def test_world_mismatch_is_refused():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"],
+                       capture_output=True, env=env, cwd=ROOT, timeout=120)
+    assert p.returncode != 0 and b"WORLD_SIZE=2" in p.stderr

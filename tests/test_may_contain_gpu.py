@@ -48,16 +48,17 @@ def _file(img):
 
 
 def expected(img, key):
+    """SSTable.MayContain (sstable.go:300-305) of a decoded image: the range
+    check, then Filter.Test of the decoded filter (bits past the stored bit
+    count read 0).  Where Go panics (m == 0 < k: location() divides by zero)
+    the ABI answers 0."""
     meta, mn, mx, f, nbits = _file(img)
     if meta.stage in (1, 2):
         return 0
     if mn > key or mx < key:
         return 0
-    if meta.filter_m == 0:
-        return 0
-    if meta.filter_k == 0:
-        return 1
-    return int(f.test(key)) if nbits >= meta.filter_m else None
+    r = f.test_decoded(key)
+    return 0 if r < 0 else r
 
 
 def test_may_contain_vs_oracle(ctx):
@@ -180,3 +181,74 @@ def test_may_contain_sorted_shared_long_prefixes(ctx):
     probes += [pre[:16] + b"%09d" % int(x) for x in rng.integers(0, 10**9, 50)]  # ties, then bytes
     assert all(bounds[i] < bounds[i + 1] for i in range(len(bounds) - 1))  # sorted, disjoint
     check(ctx, rng, images, probes)
+
+
+def _patch_nbits(img, nbits):
+    """The image with its stored bitset length (the u64be after m and k,
+    bloom.go:239-250 / bitset.ReadFrom) lowered: the filter block keeps its
+    length prefix, so the .sst framing is unchanged and only the bits at and
+    past nbits read as 0 (bitset.Test past its length)."""
+    img = img.copy()
+    mnl = int(np.frombuffer(img[:4].tobytes(), "<u4")[0])
+    mxl = int(np.frombuffer(img[4 + mnl:8 + mnl].tobytes(), "<u4")[0])
+    at = 8 + mnl + mxl + 8 + 16
+    img[at:at + 8] = np.frombuffer(struct.pack(">Q", nbits), np.uint8)
+    return img
+
+
+def _patch_min_key(img, new_min):
+    """Overwrite the header's MinKey bytes (same length): a file that decodes
+    cleanly with MinKey > MaxKey."""
+    img = img.copy()
+    assert int(np.frombuffer(img[:4].tobytes(), "<u4")[0]) == len(new_min)
+    img[4:4 + len(new_min)] = np.frombuffer(new_min, np.uint8)
+    return img
+
+
+def test_may_contain_min_greater_than_max_header(ctx):
+    """F0=[a,b], F1=[z,c] (corrupted MinKey > MaxKey), F2=[d,e].
+    The bound sequence is not sorted, so the grouped path must not be taken;
+    "dd" is in F2's range and Go tests F2's filter."""
+    rng = np.random.default_rng(5)
+    f0 = build([b"a", b"ab", b"b"], m=4096, k=3)
+    f1 = _patch_min_key(build([b"c"], m=4096, k=3), b"z")
+    f2 = build([b"d", b"dd", b"e"], m=4096, k=3)
+    probes = [b"a", b"b", b"c", b"d", b"dd", b"de", b"e", b"z", b"zz", b"", b"aa"]
+    check(ctx, rng, [f0, f1, f2], probes)
+    # the same shape inside a larger, otherwise sorted and disjoint level
+    imgs = [build([b"k%03d_%d" % (i, j) for j in range(4)], m=2048, k=2) for i in range(9)]
+    imgs[4] = _patch_min_key(imgs[4], b"k999_0")
+    probes = [b"k%03d_%d" % (i, j) for i in range(10) for j in range(5)]
+    check(ctx, rng, imgs, probes)
+
+
+def test_may_contain_truncated_bitset_and_k_zero(ctx):
+    """Stored bit count below m (bitset.Test is false past its length) on the
+    grouped path (sorted disjoint files) and the per-probe path (overlapping
+    files); k = 0 (Test is true) and m = 0 < k (Go panics; answered 0)."""
+    rng = np.random.default_rng(6)
+    sorted_imgs = []
+    for i in range(6):
+        keys = [b"r%02d_%05d" % (i, j) for j in range(400)]
+        img = build(keys, m=8192, k=4)
+        if i % 2 == 0:
+            img = _patch_nbits(img, [0, 64, 4000][i // 2])
+        sorted_imgs.append(img)
+    probes = [b"r%02d_%05d" % (i, j) for i in range(7) for j in range(0, 420, 7)]
+    check(ctx, rng, sorted_imgs, probes)                       # grouped path
+    overl = sorted_imgs[:3] + [build([b"r00_00000", b"r05_99999"], m=4096, k=3)]
+    check(ctx, rng, overl, probes)                             # per-probe path
+    for m in (0, 64):
+        k0 = build([b"r00_00001", b"r00_00300"], m=64, k=1)
+        # patch k to 0, and m (the u64be before k) to `m`
+        mnl = int(np.frombuffer(k0[:4].tobytes(), "<u4")[0])
+        at = 8 + 2 * mnl + 8
+        k0 = k0.copy()
+        k0[at:at + 8] = np.frombuffer(struct.pack(">Q", m), np.uint8)
+        k0[at + 8:at + 16] = np.frombuffer(struct.pack(">Q", 0), np.uint8)
+        check(ctx, rng, [k0] + sorted_imgs[1:], probes)
+    m0 = build([b"r00_00001", b"r00_00300"], m=64, k=2).copy()
+    mnl = int(np.frombuffer(m0[:4].tobytes(), "<u4")[0])
+    at = 8 + 2 * mnl + 8
+    m0[at:at + 8] = np.frombuffer(struct.pack(">Q", 0), np.uint8)  # m = 0, k = 2
+    check(ctx, rng, [m0] + sorted_imgs[1:], probes)
