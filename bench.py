@@ -227,6 +227,7 @@ def bench_decode(args, world, rank, local):
     d_len = torch.tensor(blk_len.view(np.int32), device=dev)
     r = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()),
                                    arena=args.arena)
+    args._d_in = d_in
     stream = torch.cuda.current_stream()
 
     wal_max = int(blk_len.max()) if args.config == "wal" else 0
@@ -307,6 +308,7 @@ def bench_decode(args, world, rank, local):
         "roofline": {
             "bound": "hbm",
             "kernel": ("lsm_wal_replay (seg + stitch + compact launches)" if args.config == "wal"
+                       else "decode_v2_kernel<KV,8,ARENA>" if args.arena
                        else "decode_v2_kernel<KV,8>"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -365,6 +367,18 @@ def verify_decode(args, r, d_off, d_len, nblk):
         if args.config in UNIFORM:
             recs = UNIFORM[args.config]["recs"]
             assert bool((n == recs).all()), "decode: nrec"
+            if getattr(args, "arena", False) and r.key_arena is not None:
+                # ARENA: block b's keys / values packed at blk_off[b], equal to
+                # the record fields of the input (kv.go:88-111 make + ReadFull)
+                slot = UNIFORM[args.config]["slot"]
+                rows = r.key_arena[: nblk * slot].view(nblk, slot)[b0:b1]
+                recs_in = args._d_in[: nblk * slot].view(nblk, slot)[b0:b1, : recs * 124]
+                recs_in = recs_in.reshape(b1 - b0, recs, 124)
+                assert torch.equal(rows[:, : recs * 16].reshape(b1 - b0, recs, 16),
+                                   recs_in[:, :, 4:20]), "arena: keys"
+                vrows = r.val_arena[: nblk * slot].view(nblk, slot)[b0:b1]
+                assert torch.equal(vrows[:, : recs * 100].reshape(b1 - b0, recs, 100),
+                                   recs_in[:, :, 24:124]), "arena: values"
             assert bool(((klen == 16) & (vlen == 100)).all()), "decode: record lengths"
             assert bool((rec_off == off[blk] + 124 * j).all()), "decode: record offsets"
 

@@ -1,18 +1,17 @@
 // decode.hip — batched record decode of length-prefixed blocks on gfx950.
 //
-// One wavefront owns one block (go-lsm's blocks are independent units; the
-// parallelism is across blocks).  The block is streamed into a
-// 4 KiB per-wave LDS ring in 1 KiB chunks (one coalesced 16 B/lane LDS-DMA
-// buffer load each, range-checked so a block never reads past its padded end).  The
-// record boundaries are a dependent chain (each record's position depends on
-// every earlier length, data.go:58-76), so the wave chases them with a
-// wave-uniform cursor: a window read (one ds_read_b128 per lane) exposes 1 KiB
-// of the block across the wave's registers, and every length field inside it
-// is two v_readlane plus a scalar funnel shift, i.e. one LDS round trip per
-// 1 KiB instead of one per field.  Thirty-two waves per CU chase
-// concurrently, which hides the LDS latency of the chain behind the HBM
-// stream.  Decoded records are staged one per lane and written as coalesced
-// 16-byte descriptors every 64 records.
+// One wavefront (and one workgroup) owns one block: go-lsm's blocks are
+// independent units, so the parallelism is across blocks.  The
+// block streams through an 8 KiB per-wave LDS ring of 1 KiB chunks, loaded by
+// LDS-DMA (buffer_load_dwordx4 ... lds, range-checked so a block never reads
+// past its padded end).  Record boundaries are a dependent chain (each
+// position depends on every earlier length, data.go:58-76): the wave verifies
+// 64 records at a time by speculative runs and chases the rest exactly on
+// the VALU (decode_range_v2).  Descriptors leave as coalesced 16-byte stores;
+// in ARENA mode the key and value bytes are gathered from the LDS ring into
+// packed arenas with 16-byte stores (the bytes Go's make()+ReadFull produce).
+// Also here: the whole-.sst decode (f1), WAL replay (f4) and the dense
+// compaction of decoded records.
 #include <stdlib.h>
 #include <string.h>
 
@@ -21,13 +20,8 @@
 namespace lsm {
 namespace {
 
-constexpr int kWavesPerWG = 4;
-constexpr uint32_t kRingBytes = 4096;
-constexpr uint32_t kRingWords = kRingBytes / 4;
 constexpr uint32_t kChunk = 1024;  // one b128 wave-load
-constexpr uint32_t kNChunk = kRingBytes / kChunk;
-constexpr uint32_t kSlotBytes = 4096;              // whole-block LDS slot
-constexpr uint32_t kSlotStride = kSlotBytes + 16;  // skewed: lanes hit different banks
+constexpr uint32_t kRingChunks = 8;  // 8 KiB ring: 4 KiB blocks fit whole, 64 KiB stream
 // Cache policy of the block loads: nt (streaming).  Each block byte is read
 // once; keeping the stream out of the L2/MALL's normal replacement measured
 // 80.5 -> 71.7 us for decode4k's memory pattern (tools/block_probe.py).
@@ -59,10 +53,6 @@ struct DecodeArgs {
     const uint64_t *arena_base;
     uint64_t *key_arena_off;
     uint64_t *val_arena_off;
-    uint32_t split;  // 1: blocks larger than the 4 KiB ring are left to decode_large_kernel
-    uint32_t dbg;    // diagnostics only (LSM_DECODE_DBG): bit 0 no speculative runs,
-                     // bit 2 stop after one record, bit 3 global verification of
-                     // streamed uniform blocks (A/B; off by default)
 };
 
 // Streams one block through this wave's LDS ring and serves u32 length
@@ -180,42 +170,6 @@ struct BlockReaderT {
         return lo;
     }
 };
-using BlockReader = BlockReaderT<kNChunk>;
-
-// Records staged one per lane until 64 are ready, then stored coalesced.
-struct RecordStage {
-    uint32_t off_lo, off_hi, klen, vlen, x_lo, x_hi;
-
-    __device__ __forceinline__ void put(uint32_t slot, uint64_t off, uint32_t k, uint32_t v,
-                                        uint64_t x) {
-        if (lane_id() == slot) {
-            off_lo = (uint32_t)off;
-            off_hi = (uint32_t)(off >> 32);
-            klen = k;
-            vlen = v;
-            x_lo = (uint32_t)x;
-            x_hi = (uint32_t)(x >> 32);
-        }
-    }
-};
-
-template <int G>
-__device__ __forceinline__ void flush(const DecodeArgs &a, const RecordStage &st, uint64_t base,
-                                      uint32_t first, uint32_t cnt) {
-    uint32_t lane = lane_id();
-    if (lane < cnt) {
-        uint64_t i = base + first + lane;
-        u32x4 d;
-        d.x = st.off_lo;
-        d.y = st.off_hi;
-        d.z = st.klen;
-        d.w = st.vlen;
-        a.desc[i] = d;
-        if (G == LSM_GRAMMAR_IDX && a.idx_value)
-            a.idx_value[i] = (int64_t)((uint64_t)st.x_hi << 32 | st.x_lo);
-    }
-}
-
 template <int G>
 struct MinRecord { static constexpr uint32_t R = G == LSM_GRAMMAR_V ? 4 : G == LSM_GRAMMAR_KV ? 8 : 12; };
 
@@ -235,288 +189,14 @@ __device__ __forceinline__ void record_slots(const DecodeArgs &a, uint32_t b, ui
     }
 }
 
-// Wave-per-block path: the whole wave chases one block (any size) through a
-// 4 KiB LDS ring with a wave-uniform (scalar) cursor.  Used for ARENA mode and
-// for blocks too large for a lane slot.
-template <int G, bool ARENA>
-__device__ void decode_block_wave(const DecodeArgs &a, uint32_t b, uint32_t *ring) {
-    const uint64_t off = uni64(a.blk_off[b]);
-    const uint32_t n = uni(a.blk_len[b]);
-    uint64_t base, cap;
-    record_slots<G>(a, b, off, n, base, cap);
-    base = uni64(base);
-    cap = uni64(cap);
-
-    BlockReader rd;
-    rd.init(ring, a.in, off, n);
-    RecordStage st{};
-
-    uint64_t kcur = 0, vcur = 0;
-    if (ARENA) {
-        kcur = a.arena_base ? uni64(a.arena_base[b]) : off;  // offset-addressed arenas
-        vcur = kcur;
-    }
-
-    uint32_t pos = 0, nr = 0;
-    int32_t status = LSM_OK;
-    for (;;) {
-        uint32_t rem = n - pos;
-        uint32_t klen = 0, vlen = 0;
-        uint64_t xval = 0;
-        uint32_t vp = pos;
-        if (G == LSM_GRAMMAR_V) {
-            // data.go:58-76
-            if (rem == 0) break;
-            if (rem < 4) { status = LSM_ST_TRUNC_LEN_PREFIX; break; }
-            vlen = rd.field(pos);
-            if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
-        } else if (G == LSM_GRAMMAR_KV) {
-            // wal.go:107 loop of kv.go:77-115
-            if (rem == 0) break;
-            if (rem < 4) { status = LSM_ST_TRUNC_LEN_PREFIX; break; }
-            klen = rd.field(pos);
-            if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; break; }
-            if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; break; }
-            vp = pos + 4 + klen;
-            uint32_t rem2 = n - vp;
-            if (rem2 < 4) { status = LSM_ST_TRUNC_VLEN; break; }
-            vlen = rd.field(vp);
-            if (vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; break; }
-            if (rem2 - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
-        } else {
-            // index.go:70-98
-            if (rem == 0) break;
-            if (rem < 4) { status = LSM_ST_IDX_OVERRUN; break; }
-            klen = rd.field(pos);
-            if ((uint64_t)rem < 12ull + klen) { status = LSM_ST_IDX_OVERRUN; break; }
-            vp = pos + 4 + klen;
-            uint32_t lo = rd.field(vp);
-            uint32_t hi = rd.field(vp + 4);
-            xval = (uint64_t)hi << 32 | lo;
-            vlen = 8;
-        }
-        if (nr >= cap) { status = LSM_ST_CAPACITY; break; }
-
-        const uint32_t slot = nr % kWave;
-        st.put(slot, off + pos, klen, vlen, xval);
-        if (ARENA) {
-            if (G != LSM_GRAMMAR_V && a.key_arena) {
-                wave_copy(rd.rsrc, rd.h + pos + 4, a.key_arena + kcur, klen);
-                if (a.key_arena_off && lane_id() == 0) a.key_arena_off[base + nr] = kcur;
-                kcur += klen;
-            }
-            if (G != LSM_GRAMMAR_IDX && a.val_arena) {
-                wave_copy(rd.rsrc, rd.h + vp + 4, a.val_arena + vcur, vlen);
-                if (a.val_arena_off && lane_id() == 0) a.val_arena_off[base + nr] = vcur;
-                vcur += vlen;
-            }
-        }
-        nr++;
-        if (slot == kWave - 1) flush<G>(a, st, base, nr - kWave, kWave);
-        pos = (G == LSM_GRAMMAR_IDX) ? vp + 8 : vp + 4 + vlen;
-    }
-    if (nr % kWave) flush<G>(a, st, base, nr - nr % kWave, nr % kWave);
-    if (lane_id() == 0) {
-        a.nrec[b] = nr;
-        a.status[b] = status;
-    }
-}
-
-// Speculative parallel runs (DESC mode).  After each exactly-decoded record of
-// size S (key length K, value length V), all 64 lanes test the hypothesis
-// "the next 64 records have the same K and V": lane i reads the length fields
-// at cur + i*S (and cur + i*S + 4 + K) straight from the LDS ring.  The
-// ballot's count of leading successes j is the verified run: records
-// [0, j) sit exactly where predicted (each check reads the record's own
-// fields), so j descriptors are stored coalesced and the cursor jumps j*S.
-// The first mismatching record is re-decoded by the exact scalar step, which
-// also produces the precise error status.  A block of equal-size records
-// (the common LSM case) costs one exact step and one run per 64 records.
-template <int G, uint32_t NCH = kNChunk>
-__device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
-                                  uint32_t n, bool staged = false) {
-    constexpr uint32_t kWords = NCH * kChunk / 4;
-    uint64_t base, cap;
-    record_slots<G>(a, b, off, n, base, cap);
-    base = uni64(base);
-    cap = uni64(cap);
-    const uint32_t lane = lane_id();
-
-    BlockReaderT<NCH> rd;
-    rd.init(ring, a.in, off, n);
-    if (staged) rd.hi_c = rd.landed = rd.nchunks < NCH ? rd.nchunks : NCH;  // DMA'd and landed
-#ifdef LSM_STAMPS
-    rd.ensure(rd.h);
-    stamp(1);
-#endif
-    auto lds_u32 = [&](uint32_t p) -> uint32_t {  // per-lane read, block position p
-        const uint32_t sb = rd.h + p;
-        const uint32_t w = sb >> 2;
-        return funnel(ring[w % kWords], ring[(w + 1) % kWords], sb);
-    };
-
-    // Wave-uniform field at block position p: two LDS dwords (a broadcast
-    // read), a funnel shift and one readfirstlane.  The bytes must be landed.
-    auto ufield = [&](uint32_t p) -> uint32_t {
-        const uint32_t sb = rd.h + p;
-        const uint32_t w = sb >> 2;
-        return uni(funnel(ring[w % kWords], ring[(w + 1) % kWords], sb));
-    };
-
-    // Exact-step records are staged one per lane and stored 64 at a time: a
-    // store between a ring refill and its counted wait is younger than the
-    // chunks in flight, so one store per record would make every wait drain
-    // the whole prefetch (vmcnt counts stores too).  Staged records occupy
-    // consecutive slots s_first.. (the stage is flushed before a run).
-    uint32_t s_pos = 0, s_k = 0, s_v = 0, s_xlo = 0, s_xhi = 0, ns = 0, s_first = 0;
-    auto flush_stage = [&]() {
-        if (ns && lane < ns) {
-            const uint64_t ro = off + s_pos;
-            u32x4 d;
-            d.x = (uint32_t)ro;
-            d.y = (uint32_t)(ro >> 32);
-            d.z = s_k;
-            d.w = s_v;
-            a.desc[base + s_first + lane] = d;
-            if (G == LSM_GRAMMAR_IDX && a.idx_value)
-                a.idx_value[base + s_first + lane] = (int64_t)((uint64_t)s_xhi << 32 | s_xlo);
-        }
-        ns = 0;
-    };
-    uint32_t pos = 0, nr = 0, miss = 0, skip = 0, kprev = 0;
-    int32_t status = LSM_OK;
-    for (;;) {
-        // ---- exact step at pos (same checks and order as the reference) ----
-        // Fields are read straight from the ring; the value length is read
-        // speculatively at the previous record's key length, in the same LDS
-        // round trip as the key length (keys of one length are the norm).
-        const uint32_t rem = n - pos;
-        uint32_t klen = 0, vlen = 0, vp = pos;
-        uint64_t xval = 0;
-        if (rem == 0) break;
-        if (rem < 4) {
-            status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
-            break;
-        }
-        rd.ensure(rd.h + pos);  // [pos, pos + 1 KiB) landed (and the ring topped up)
-        if (G == LSM_GRAMMAR_V) {
-            vlen = ufield(pos);
-            if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
-        } else if (G == LSM_GRAMMAR_KV) {
-            const bool spec_v = kprev <= kChunk - 12 && rem >= 8 + kprev;
-            klen = ufield(pos);
-            const uint32_t vguess = spec_v ? ufield(pos + 4 + kprev) : 0;
-            if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; break; }
-            if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; break; }
-            vp = pos + 4 + klen;
-            const uint32_t rem2 = n - vp;
-            if (rem2 < 4) { status = LSM_ST_TRUNC_VLEN; break; }
-            if (spec_v && klen == kprev) {
-                vlen = vguess;
-            } else {
-                if (vp + 4 - pos > kChunk) rd.ensure(rd.h + vp);
-                vlen = ufield(vp);
-            }
-            if (vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; break; }
-            if (rem2 - 4 < vlen) { status = LSM_ST_TRUNC_VAL; break; }
-            kprev = klen;
-        } else {
-            klen = ufield(pos);
-            if ((uint64_t)rem < 12ull + klen) { status = LSM_ST_IDX_OVERRUN; break; }
-            vp = pos + 4 + klen;
-            if (vp + 8 - pos > kChunk) rd.ensure(rd.h + vp);
-            xval = (uint64_t)ufield(vp + 4) << 32 | ufield(vp);
-            vlen = 8;
-        }
-        if (nr >= cap) { status = LSM_ST_CAPACITY; break; }
-        if (ns == 0) s_first = nr;
-        if (lane == ns) {
-            s_pos = pos;
-            s_k = klen;
-            s_v = vlen;
-            if (G == LSM_GRAMMAR_IDX) {
-                s_xlo = (uint32_t)xval;
-                s_xhi = (uint32_t)(xval >> 32);
-            }
-        }
-        if (++ns == kWave) flush_stage();
-        nr++;
-        const uint32_t S = G == LSM_GRAMMAR_V ? 4 + vlen : G == LSM_GRAMMAR_KV ? 8 + klen + vlen
-                                                                              : 12 + klen;
-        pos += S;
-
-        // ---- speculative runs of records shaped like the last one ----
-        // Back off after runs that verified nothing (blocks of varied record
-        // shapes, config 5): skip the next 1, 3, 7, 15 attempts.
-        if (skip || (a.dbg & 1)) {
-            if (skip) skip--;
-            continue;
-        }
-        flush_stage();
-        for (bool first = true;; first = false) {
-            if (pos >= n) break;
-            // wait for the span the run can verify (64 records): all of a block
-            // that fits the ring (its chunks were issued together), at most
-            // half the ring otherwise, so the younger half stays in flight
-            const uint32_t kSpanMax = (rd.nchunks <= NCH ? NCH : NCH / 2) * kChunk;
-            const uint64_t span = (uint64_t)S * kWave + 8;
-            rd.ensure(rd.h + pos, span < kSpanMax ? (uint32_t)span : kSpanMax);
-            uint32_t res = rd.landed * kChunk;  // resident stream end
-            if (res > rd.total) res = rd.total;
-            const uint32_t lim = (res - rd.h) < n ? (res - rd.h) : n;
-            const uint64_t pe = (uint64_t)pos + (uint64_t)(lane + 1) * S;  // record end
-            const uint32_t p = pos + lane * S;
-            bool ok = pe <= lim && (uint64_t)nr + lane < cap;
-            uint64_t x = 0;
-            if (ok) {
-                if (G == LSM_GRAMMAR_V) {
-                    ok = lds_u32(p) == vlen;
-                } else if (G == LSM_GRAMMAR_KV) {
-                    ok = (int)(lds_u32(p) == klen) & (int)(lds_u32(p + 4 + klen) == vlen);
-                } else {
-                    ok = lds_u32(p) == klen;
-                    x = (uint64_t)lds_u32(p + 8 + klen) << 32 | lds_u32(p + 4 + klen);
-                }
-            }
-            const uint64_t m = __ballot(ok);
-            const uint32_t j = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
-            if (lane < j) {
-                const uint64_t ro = off + p;
-                u32x4 d;
-                d.x = (uint32_t)ro;
-                d.y = (uint32_t)(ro >> 32);
-                d.z = klen;
-                d.w = vlen;
-                a.desc[base + nr + lane] = d;
-                if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + lane] = (int64_t)x;
-            }
-            nr += j;
-            pos += j * S;
-            if (first) {
-                if (j == 0) {
-                    miss = miss < 4 ? miss + 1 : 4;
-                    skip = (1u << miss) - 1;
-                } else {
-                    miss = 0;
-                }
-            }
-            if (j < 64) break;
-        }
-    }
-    flush_stage();
-    if (lane == 0) {
-        a.nrec[b] = nr;
-        a.status[b] = status;
-    }
-}
-
 // ---- v2: the chase with the fewest scalar instructions -------------------
 //
 // The exact step is a serial chain, and a wave-uniform chain runs on the CU's
-// one scalar unit, shared by all 32 resident waves: PMC on config 5 (record
+// one scalar unit, shared by all resident waves: PMC on config 5 (record
 // shapes vary, so speculative runs rarely verify) counted 107 SALU
-// instructions per record for decode_block_spec, 74% of the kernel time at one
-// SALU issue per cycle.  v2 keeps the same semantics with a leaner step:
+// instructions per record for the round-0 wave-uniform step, 74% of the
+// kernel time at one SALU issue per cycle.  v2 keeps the same semantics with
+// a leaner step:
 //  * one compare decides whether the bytes are landed (`lim`), the ring
 //    bookkeeping only runs when a step crosses it;
 //  * blocks that fit the ring are read without modulo arithmetic (LIN);
@@ -524,7 +204,11 @@ __device__ void decode_block_spec(const DecodeArgs &a, uint32_t b, uint32_t *rin
 //    round trip as the key length;
 //  * descriptors are staged branch-free (v_cndmask) and stored 64 at a time;
 //  * error statuses are only computed on the (one) failing record.
-// Speculative runs are unchanged.
+// Speculative runs: after an exact step of size S (key length K, value
+// length V) all 64 lanes test "the next 64 records have the same K and V"
+// straight from LDS; the ballot's count of leading successes is the verified
+// run (each check reads the record's own fields, so the verified records are
+// exactly the chase's), stored coalesced.
 // A wave-uniform value moved into a VGPR, so the arithmetic that depends on
 // it stays on the vector ALU (the compiler would otherwise keep a uniform
 // chain on the CU's single scalar unit).
@@ -534,40 +218,277 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
     return v;
 }
 
+// ---- ARENA: key and value bytes gathered from the LDS ring -----------------
+//
+// kv.go:88-111 / data.go:68-75 hand back freshly allocated key and value
+// slices; ARENA mode packs them per block, in record order, into a key arena
+// and a value arena.  A batch of records (a verified run, or the <= 64 staged
+// records of exact steps) occupies one contiguous range of each arena, so the
+// copy is output-driven: each lane assembles one 16-byte output chunk from
+// the record fields it covers (four funnel-shifted dwords, bytewise only
+// where a record boundary falls inside a dword) and stores it whole.  Only a
+// batch's first and last chunks, shared with the neighbouring batch or
+// block, are written byte by byte.
+template <uint32_t NCH, bool LIN>
+struct RingBytes {
+    const uint32_t *ring;
+    rsrc_t rs;          // the block in global memory (stream byte = rsrc offset)
+    uint32_t res_lo;    // stream bytes [res_lo, res_hi) are landed in the ring
+    uint32_t res_hi;
+    __device__ __forceinline__ uint32_t word(uint32_t w) const {
+        return LIN ? ring[w] : ring[w % (NCH * kChunk / 4)];
+    }
+    __device__ __forceinline__ uint32_t u32(uint32_t sb) const {
+        return funnel(word(sb >> 2), word((sb >> 2) + 1), sb);
+    }
+    __device__ __forceinline__ uint32_t u8(uint32_t sb) const {
+        return (word(sb >> 2) >> (8 * (sb & 3))) & 0xFFu;
+    }
+    // a field not (wholly) in the ring: read through the caches
+    __device__ __forceinline__ uint32_t g32(uint32_t sb) const {
+        const uint32_t a = sb & ~3u;
+        return funnel(ld_b32(rs, a), ld_b32(rs, a + 4), sb);
+    }
+    __device__ __forceinline__ uint32_t g8(uint32_t sb) const {
+        return (ld_b32(rs, sb & ~3u) >> (8 * (sb & 3))) & 0xFFu;
+    }
+};
+
+// Store 16 bytes at the 16-aligned dst; only bytes [lo, hi) are this batch's
+// (a batch's first and last chunk share 16 bytes with its neighbours).
+__device__ __forceinline__ void store_chunk(uint8_t *dst, u32x4 v, int lo, int hi) {
+    if (lo <= 0 && hi >= 16) {
+        *reinterpret_cast<u32x4 *>(dst) = v;
+        return;
+    }
+#pragma unroll 1
+    for (int t = lo < 0 ? 0 : lo; t < (hi < 16 ? hi : 16); t++) {
+        const uint32_t d = t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w;
+        dst[t] = (uint8_t)(d >> (8 * (t & 3)));
+    }
+}
+
+__device__ __forceinline__ void set_dword(u32x4 &v, uint32_t j, uint32_t w) {
+    v.x = j == 0 ? w : v.x;
+    v.y = j == 1 ? w : v.y;
+    v.z = j == 2 ? w : v.z;
+    v.w = j == 3 ? w : v.w;
+}
+
+// 16 bytes from stream byte sb: five consecutive source dwords, four funnels
+template <class F>
+__device__ __forceinline__ u32x4 load16(F word, uint32_t sb) {
+    const uint32_t w = sb >> 2;
+    const uint32_t d0 = word(w), d1 = word(w + 1), d2 = word(w + 2), d3 = word(w + 3),
+                   d4 = word(w + 4);
+    return u32x4{funnel(d0, d1, sb), funnel(d1, d2, sb), funnel(d2, d3, sb), funnel(d3, d4, sb)};
+}
+
+// A verified run: cnt records of stride S whose field of L bytes starts at
+// ring stream byte src0 + i*S (all landed), packed to out[0, cnt*L).
+template <uint32_t NCH, bool LIN>
+__device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, uint8_t *out,
+                                               uint32_t src0, uint32_t S, uint32_t L,
+                                               uint32_t cnt) {
+    const uint32_t T = cnt * L;  // <= the ring: a run lies inside the landed bytes
+    if (T == 0) return;
+    const uint32_t lead = (uint32_t)((uintptr_t)out & 15);
+    uint8_t *a0 = out - lead;
+    const uint32_t nch = (lead + T + 15) >> 4;
+    const float inv = 1.0f / (float)L;
+    auto rec = [&](uint32_t q) -> uint32_t {  // q / L, exact for q < 2^22
+        uint32_t r = (uint32_t)((float)q * inv);
+        r = r * L > q ? r - 1 : r;
+        return (r + 1) * L <= q ? r + 1 : r;
+    };
+    auto src = [&](uint32_t q) -> uint32_t {  // stream byte of output byte q
+        const uint32_t r = rec(q);
+        return src0 + r * S + (q - r * L);
+    };
+    auto word = [&](uint32_t w) -> uint32_t { return rb.word(w); };
+#pragma unroll 1
+    for (uint32_t c = lane_id(); c < nch; c += kWave) {
+        const int q0 = (int)(16 * c) - (int)lead;
+        u32x4 v{0, 0, 0, 0};
+        if (q0 >= 0 && q0 + 16 <= (int)T) {
+            const uint32_t r = rec((uint32_t)q0), o = (uint32_t)q0 - r * L;
+            if (o + 16 <= L) {  // the chunk lies in one field
+                v = load16(word, src0 + r * S + o);
+            } else {
+#pragma unroll 1
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t q = (uint32_t)q0 + 4 * j, rj = rec(q), oj = q - rj * L;
+                    uint32_t w = 0;
+                    if (oj + 4 <= L) {
+                        w = rb.u32(src0 + rj * S + oj);
+                    } else {
+#pragma unroll 1
+                        for (uint32_t t = 0; t < 4; t++) w |= rb.u8(src(q + t)) << (8 * t);
+                    }
+                    set_dword(v, j, w);
+                }
+            }
+        } else {  // the first or last chunk: only the batch's bytes
+#pragma unroll 1
+            for (int t = 0; t < 16; t++) {
+                const int q = q0 + t;
+                if (q >= 0 && q < (int)T) {
+                    const uint32_t b = rb.u8(src((uint32_t)q)) << (8 * (t & 3));
+                    set_dword(v, (uint32_t)t >> 2, (t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w) | b);
+                }
+            }
+        }
+        store_chunk(a0 + 16 * c, v, -q0, (int)T - q0);
+    }
+}
+
+// A staged batch: lane l < cnt holds a record field of len bytes at ring
+// stream byte src; the fields are packed in lane order to out[0, T).  A field
+// wholly landed in the ring is read from LDS, any other (a value longer than
+// the ring) through the caches.  tab: 129 dwords of LDS.  Returns T.
+template <uint32_t NCH, bool LIN>
+__device__ __forceinline__ uint32_t arena_emit_batch(const RingBytes<NCH, LIN> &rb, uint32_t *tab,
+                                                     uint8_t *out, uint32_t cnt, uint32_t src,
+                                                     uint32_t len, uint64_t *out_off,
+                                                     uint64_t cur) {
+    const uint32_t lane = lane_id();
+    const uint32_t l = lane < cnt ? len : 0u;
+    uint32_t T;
+    const uint32_t start = wave_excl_scan(l, &T);
+    if (out_off && lane < cnt) out_off[lane] = cur + start;
+    if (T == 0) return 0;
+    uint32_t *tstart = tab, *tsrc = tab + 65;
+    if (lane < cnt) {
+        tstart[lane] = start;
+        tsrc[lane] = src;
+    }
+    if (lane == 0) tstart[cnt] = T;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t lead = (uint32_t)((uintptr_t)out & 15);
+    uint8_t *a0 = out - lead;
+    const uint32_t nch = (lead + T + 15) >> 4;
+#pragma unroll 1
+    for (uint32_t c = lane; c < nch; c += kWave) {
+        const int q0 = (int)(16 * c) - (int)lead;
+        const uint32_t qf = q0 < 0 ? 0u : (uint32_t)q0;
+        // the last record whose packed range starts at or before qf
+        uint32_t lo = 0, hi = cnt;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tstart[mid] <= qf) lo = mid;
+            else hi = mid;
+        }
+        uint32_t r = lo, rs0 = tstart[r], rs1 = tstart[r + 1], rsrc = tsrc[r];
+        auto in_ring = [&]() { return rsrc >= rb.res_lo && rsrc + (rs1 - rs0) <= rb.res_hi; };
+        auto seek = [&](uint32_t q) {  // advance r to the record holding byte q
+            while (rs1 <= q) {
+                r++;
+                rs0 = rs1;
+                rs1 = tstart[r + 1];
+                rsrc = tsrc[r];
+            }
+        };
+        auto byte_at = [&](uint32_t q) -> uint32_t {
+            seek(q);
+            const uint32_t sb = rsrc + (q - rs0);
+            return in_ring() ? rb.u8(sb) : rb.g8(sb);
+        };
+        u32x4 v{0, 0, 0, 0};
+        if (q0 >= 0 && q0 + 16 <= (int)T && (uint32_t)q0 + 16 <= rs1) {
+            // the chunk lies in one field
+            const uint32_t sb = rsrc + ((uint32_t)q0 - rs0);
+            if (in_ring())
+                v = load16([&](uint32_t w) { return rb.word(w); }, sb);
+            else
+                v = u32x4{rb.g32(sb), rb.g32(sb + 4), rb.g32(sb + 8), rb.g32(sb + 12)};
+        } else {
+#pragma unroll 1
+            for (int t = 0; t < 16; t++) {
+                const int q = q0 + t;
+                if (q >= 0 && q < (int)T) {
+                    const uint32_t b = byte_at((uint32_t)q) << (8 * (t & 3));
+                    set_dword(v, (uint32_t)t >> 2, (t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w) | b);
+                }
+            }
+        }
+        store_chunk(a0 + 16 * c, v, -q0, (int)T - q0);
+    }
+    // the table is rewritten by the next batch: all reads done first
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return T;
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+
+// arena_emit_batch as one out-of-line call per batch: a staged flush has
+// several call sites in the chase, and inlining each multiplies the live
+// registers of the whole kernel.  The LDS pointers keep their address space
+// (ds_read, not flat loads).
+template <uint32_t NCH, bool LIN>
+__device__ __forceinline__ uint32_t arena_emit_batch_call(lds_u32_t *ring, rsrc_t rs, uint32_t res_lo,
+                                                       uint32_t res_hi, lds_u32_t *tab,
+                                                       uint8_t *out, uint32_t cnt, uint32_t src,
+                                                       uint32_t len, uint64_t *out_off,
+                                                       uint64_t cur) {
+    RingBytes<NCH, LIN> rb{(const uint32_t *)ring, rs, res_lo, res_hi};
+    return arena_emit_batch(rb, (uint32_t *)tab, out, cnt, src, len, out_off, cur);
+}
+
+// Arena cursors of one block (ARENA mode): the next free byte of each arena.
+struct ArenaCur {
+    uint64_t k, v;
+};
+
 // Decode the byte range [off, off + n) of a.in as one block whose records
 // go to slots base.. (capacity ncap); returns the record count, the status
 // and the position where the chase stopped.  Records that start at or past
 // `stop` are not decoded (a clean stop; stop = n decodes the whole range).
-template <int G, uint32_t NCH, bool LIN>
+// ARENA: keys and values are also packed into a.key_arena / a.val_arena from
+// the cursors `ac` (tab: the 129-dword LDS table of arena_emit_batch).
+template <int G, uint32_t NCH, bool LIN, bool ARENA = false>
 __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
                                 uint64_t base, uint32_t ncap, uint32_t &nr_out, int32_t &st_out,
-                                uint32_t stop, uint32_t &pos_out) {
-    constexpr uint32_t kWords = NCH * kChunk / 4;
+                                uint32_t stop, uint32_t &pos_out, ArenaCur ac = {},
+                                uint32_t *tab = nullptr) {
     const uint32_t lane = lane_id();
     BlockReaderT<NCH> rd;
     rd.init(ring, a.in, off, n);
+    RingBytes<NCH, LIN> rb{ring, rd.rsrc, 0, 0};
 
-    // Block bytes below `lim` (and at or above the last anchor) are landed.
-    uint32_t lim = 0;
-    auto need = [&](uint32_t p, uint32_t len) {
-        if ((uint64_t)p + len <= lim) return;
-        rd.ensure(rd.h + p, LIN ? rd.total : len);
-        lim = rd.landed >= rd.nchunks ? n : rd.landed * kChunk - rd.h;
-    };
-    auto word = [&](uint32_t w) -> uint32_t { return LIN ? ring[w] : ring[w % kWords]; };
+    auto word = [&](uint32_t w) -> uint32_t { return rb.word(w); };
     auto fld = [&](uint32_t p) -> uint32_t {  // wave-uniform u32 at block position p
-        const uint32_t sb = rd.h + p;
-        const uint32_t w = sb >> 2;
-        return uni(funnel(word(w), word(w + 1), sb));
+        return uni(rb.u32(rd.h + p));
     };
     auto lds_u32 = [&](uint32_t p) -> uint32_t {  // per-lane u32 at block position p
-        const uint32_t sb = rd.h + p;
-        const uint32_t w = sb >> 2;
-        return funnel(word(w), word(w + 1), sb);
+        return rb.u32(rd.h + p);
     };
 
     uint32_t s_pos = 0, s_k = 0, s_v = 0, s_xlo = 0, s_xhi = 0, ns = 0, s_first = 0;
     uint32_t pos = 0, nr = 0, kprev = 0xFFFFFFFFu, miss = 0, skip = 0;
+    // ARENA: the exact step's record (the last staged one) leaves its arena
+    // bytes together with the run that follows it (same K, V, stride)
+    uint32_t pend = 0, pend_pos = 0, pend_k = 0, pend_v = 0;
+    auto emit_run_arena = [&](uint32_t p0, uint32_t K, uint32_t V, uint32_t S, uint32_t cnt,
+                              uint64_t slot0) {
+        if (G != LSM_GRAMMAR_V && a.key_arena) {
+            arena_emit_run(rb, a.key_arena + ac.k, rd.h + p0 + 4, S, K, cnt);
+            if (a.key_arena_off)  // cnt <= 65: the pending record + a full run
+                for (uint32_t i = lane; i < cnt; i += kWave) a.key_arena_off[slot0 + i] = ac.k + i * K;
+            ac.k += (uint64_t)cnt * K;
+        }
+        if (G != LSM_GRAMMAR_IDX && a.val_arena) {
+            arena_emit_run(rb, a.val_arena + ac.v, rd.h + p0 + (G == LSM_GRAMMAR_KV ? 8 + K : 4u),
+                           S, V, cnt);
+            if (a.val_arena_off)
+                for (uint32_t i = lane; i < cnt; i += kWave)
+                    a.val_arena_off[slot0 + i] = ac.v + (uint64_t)i * V;
+            ac.v += (uint64_t)cnt * V;
+        }
+    };
     auto flush = [&]() {
         if (ns) {
             if (lane < ns) {
@@ -581,61 +502,49 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                 if (G == LSM_GRAMMAR_IDX && a.idx_value)
                     a.idx_value[base + s_first + lane] = (int64_t)((uint64_t)s_xhi << 32 | s_xlo);
             }
+            if (ARENA) {
+                lds_u32_t *lring = (lds_u32_t *)ring, *ltab = (lds_u32_t *)tab;
+                // keys, then values: one emitter body serves both arenas
+#pragma unroll 1
+                for (uint32_t f = G == LSM_GRAMMAR_V ? 1u : 0u;
+                     f < (G == LSM_GRAMMAR_IDX ? 1u : 2u); f++) {
+                    uint8_t *ar = f ? a.val_arena : a.key_arena;
+                    if (!ar) continue;
+                    uint64_t *ao = f ? a.val_arena_off : a.key_arena_off;
+                    const uint64_t cur = f ? ac.v : ac.k;
+                    const uint32_t src =
+                        rd.h + s_pos + (f == 0 ? 4u : G == LSM_GRAMMAR_KV ? 8 + s_k : 4u);
+                    const uint32_t t = arena_emit_batch_call<NCH, LIN>(
+                        lring, rb.rs, rb.res_lo, rb.res_hi, ltab, ar + cur, ns - pend, src,
+                        f ? s_v : s_k, ao ? ao + base + s_first : nullptr, cur);
+                    if (f) ac.v += t;
+                    else ac.k += t;
+                }
+            }
             ns = 0;
         }
     };
-    auto gverify = [&](uint32_t K, uint32_t V, uint32_t S) {
-        constexpr uint32_t T = 8;  // 64-record rounds per batch (a 64 KiB block of 124 B records in one)
-        const uint32_t cnt = (n - pos) / S;  // candidates wholly inside the block
-        uint32_t i0 = 0;
-        while (i0 < cnt) {
-            uint32_t kw0[T], kw1[T], vw0[T], vw1[T], sb[T];
-#pragma unroll
-            for (uint32_t t = 0; t < T; t++) {
-                const uint32_t i = i0 + t * kWave + lane;
-                sb[t] = rd.h + pos + i * S;  // no wrap: i < cnt keeps it inside the block
-                const uint32_t sk = (i < cnt ? sb[t] : 0u) & ~3u;
-                const uint32_t svv = (i < cnt ? sb[t] + (G == LSM_GRAMMAR_KV ? 4 + K : 0u) : 0u) & ~3u;
-                kw0[t] = ld_b32(rd.rsrc, sk);
-                kw1[t] = ld_b32(rd.rsrc, sk + 4);
-                if (G == LSM_GRAMMAR_KV) {
-                    vw0[t] = ld_b32(rd.rsrc, svv);
-                    vw1[t] = ld_b32(rd.rsrc, svv + 4);
-                }
+    // Block bytes below `lim` (and at or above the last anchor) are landed.
+    uint32_t lim = 0;
+    auto need = [&](uint32_t p, uint32_t len) {
+        if ((uint64_t)p + len <= lim) return;
+        // a streamed block recycles ring chunks: the staged records' arena
+        // bytes leave first
+        if (ARENA && !LIN) {
+            flush();
+            if (pend) {
+                emit_run_arena(pend_pos, pend_k, pend_v, 0, 1, base + nr - 1);
+                pend = 0;
             }
-            uint32_t f = T * kWave;
-#pragma unroll
-            for (uint32_t t = 0; t < T; t++) {
-                const uint32_t i = i0 + t * kWave + lane;
-                const uint32_t k = funnel(kw0[t], kw1[t], sb[t]);
-                bool ok = i < cnt && nr + i < ncap;
-                if (G == LSM_GRAMMAR_KV) {
-                    const uint32_t v = funnel(vw0[t], vw1[t], sb[t] + 4 + K);
-                    ok = ok && k == K && v == V;
-                } else {
-                    ok = ok && k == V;
-                }
-                const uint64_t m = __ballot(ok);
-                const uint32_t jt = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
-                if (f == T * kWave && jt < 64) f = t * kWave + jt;
-                if (ok && t * kWave + lane < f) {
-                    const uint64_t ro = off + (sb[t] - rd.h);
-                    u32x4 d;
-                    d.x = (uint32_t)ro;
-                    d.y = (uint32_t)(ro >> 32);
-                    d.z = K;
-                    d.w = V;
-                    a.desc[base + nr + i] = d;
-                }
-            }
-            const uint32_t take = f < cnt - i0 ? f : cnt - i0;
-            i0 += take;
-            if (take < T * kWave) break;
         }
-        const uint32_t got = i0 < cnt ? i0 : cnt;
-        nr += got;
-        pos += got * S;
+        rd.ensure(rd.h + p, LIN ? rd.total : len);
+        lim = rd.landed >= rd.nchunks ? n : rd.landed * kChunk - rd.h;
+        if (ARENA) {
+            rb.res_lo = (rd.hi_c > NCH ? rd.hi_c - NCH : 0u) * kChunk;
+            rb.res_hi = rd.landed * kChunk;
+        }
     };
+
     int32_t status = LSM_OK;
     for (;;) {
         // ---- exact step at pos (same checks and order as the reference) ----
@@ -697,7 +606,6 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
         if (nr == 0) stamp(1);
         nr++;
         pos += S;
-        if (a.dbg & 4) break;
 
         // ---- records of varying shape: the VALU chain ----
         // After a failed run (skip > 0) the following records are chased with
@@ -760,7 +668,15 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
             }
             continue;
         }
-        if (a.dbg & 1) continue;
+        // the exact record is still staged (not flushed as a 64th) and wholly
+        // in the ring (landed, and its start not recycled by the value-length
+        // refill of a streamed block)
+        if (ARENA && ns > 0 && pos <= lim && rd.h + pos - S >= rb.res_lo) {
+            pend = 1;
+            pend_pos = pos - S;
+            pend_k = K;
+            pend_v = V;
+        }
         flush();
         for (bool first = true;; first = false) {
             if (pos >= n) break;
@@ -797,6 +713,12 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                 a.desc[base + nr + lane] = d;
                 if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + lane] = (int64_t)xx;
             }
+            if (ARENA && j + pend) {
+                // the run's fields (and the pending exact record's, S bytes
+                // before it) are landed: straight from the ring
+                emit_run_arena(pos - pend * S, K, V, S, j + pend, base + nr - pend);
+                pend = 0;
+            }
             // the run ended at the landed limit, not at a mismatch
             const bool at_lim = j == 64 || (uint64_t)pos + (uint64_t)(j + 1) * S > lim;
             nr += j;
@@ -809,21 +731,13 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                     miss = 0;
                 }
             }
-            if (!LIN && at_lim && j >= 4 && G != LSM_GRAMMAR_IDX && (a.dbg & 8) && stop >= n) {
-                // A full run in a streamed block: test the same hypothesis on
-                // the rest of the block straight from global memory, 256
-                // records per batch with all their loads in flight (the ring
-                // keeps ~2 KiB in flight per wave, too little for 64 KiB
-                // blocks at 25 waves per CU).  Verified records are exactly
-                // the chase's records (each check reads the record's own
-                // fields); the first mismatch goes back to the exact step.
-                gverify(K, V, S);
-                stamp(2);
-                break;
-            }
             // a run cut short by the landed limit goes on once more bytes
             // have landed (no exact step in between); a mismatch ends it
             if (j < 64 && !(at_lim && j > 0)) break;
+        }
+        if (ARENA && pend) {  // no run followed (the block ended)
+            emit_run_arena(pend_pos, pend_k, pend_v, 0, 1, base + nr - 1);
+            pend = 0;
         }
     }
     flush();
@@ -832,16 +746,21 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     pos_out = pos;
 }
 
-template <int G, uint32_t NCH, bool LIN>
-__device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint64_t off,
-                                uint32_t n) {
+template <int G, uint32_t NCH, bool LIN, bool ARENA>
+__device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint32_t *tab,
+                                uint64_t off, uint32_t n) {
     uint64_t base, cap;
     record_slots<G>(a, b, off, n, base, cap);
     uint32_t nr, end;
     int32_t st;
-    decode_range_v2<G, NCH, LIN>(a, ring, off, n, uni64(base),
-                                 uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr, st, n,
-                                 end);
+    ArenaCur ac{};
+    if (ARENA) {  // A(b): arena_base[b], or offset-addressed arenas
+        ac.k = a.arena_base ? uni64(a.arena_base[b]) : off;
+        ac.v = ac.k;
+    }
+    decode_range_v2<G, NCH, LIN, ARENA>(a, ring, off, n, uni64(base),
+                                        uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr,
+                                        st, n, end, ac, tab);
     if (lane_id() == 0) {
         a.nrec[b] = nr;
         a.status[b] = st;
@@ -863,517 +782,18 @@ __device__ void decode_range_any(const DecodeArgs &a, uint32_t *ring, uint64_t o
 
 // One wave (and one workgroup) per block; NCH x 1 KiB ring plus a guard
 // dword so linear reads of a block's last field stay inside the array.
-template <int G, uint32_t NCH>
+template <int G, uint32_t NCH, bool ARENA>
 __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
+    __shared__ uint32_t tab[ARENA ? 129 : 1];
     const uint32_t b = blockIdx.x;
     stamp(0);
     const uint64_t off = uni64(a.blk_off[b]);
     const uint32_t n = uni(a.blk_len[b]);
-    if (a.split && (off & 15) + (uint64_t)n > NCH * kChunk) return;
     if (((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk)
-        decode_block_v2<G, NCH, true>(a, b, ring, off, n);
+        decode_block_v2<G, NCH, true, ARENA>(a, b, ring, tab, off, n);
     else
-        decode_block_v2<G, NCH, false>(a, b, ring, off, n);
-    stamp(3);
-}
-
-template <int G, uint32_t NCH>
-int launch_v2(const DecodeArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((decode_v2_kernel<G, NCH>), dim3(a.nblk), dim3(kWave), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
-// Each wave decodes K consecutive blocks one after the other; the metadata of
-// all K is fetched up front (one vector load per array), so only the block
-// DMA remains on each block's critical path.
-template <int G, uint32_t K, uint32_t WPG>
-__global__ __launch_bounds__(64 * WPG) void decode_spec_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[WPG][kRingWords];
-    const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint32_t b0 = uni((blockIdx.x * WPG + wave) * K);
-    if (b0 >= a.nblk) return;
-    const uint32_t lane = lane_id();
-    uint64_t moff = 0;
-    uint32_t mlen = 0;
-    if (lane < K && b0 + lane < a.nblk) {
-        moff = a.blk_off[b0 + lane];
-        mlen = a.blk_len[b0 + lane];
-    }
-    stamp(0);
-    for (uint32_t k = 0; k < K; k++) {
-        const uint32_t b = b0 + k;
-        if (b >= a.nblk) break;
-        const uint64_t off = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)moff, k) |
-                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(moff >> 32), k) << 32);
-        const uint32_t n = __builtin_amdgcn_readlane(mlen, k);
-        if (a.split && (off & 15) + (uint64_t)n > kRingBytes) continue;
-        decode_block_spec<G>(a, b, ring[wave], off, n);
-    }
-    stamp(3);
-}
-
-// ---- blocks larger than the 4 KiB ring ------------------------------------
-//
-// A 4 KiB ring keeps at most 3 KiB in flight per wave, which streams a 64 KiB
-// block at a fraction of the HBM rate (decode64k 0.56 of peak, config 5
-// 0.35).  Blocks with h + n > 4 KiB are therefore left by the small-block
-// kernel (a.split) to this persistent one: W one-wave workgroups, each with a
-// 16 KiB ring (up to 15 KiB in flight, 10 waves per CU by LDS), walk the
-// block list with stride W.  Lane l of wave w looks at block r0 + l*W and a
-// ballot picks the large ones, so a batch without large blocks costs one
-// metadata load per wave.
-constexpr uint32_t kLargeNCH = 16;
-
-template <int G, uint32_t NCH>
-__global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
-    const uint64_t W = gridDim.x;
-    const uint32_t lane = lane_id();
-    for (uint64_t r0 = blockIdx.x; r0 < a.nblk; r0 += W * kWave) {
-        const uint64_t b = r0 + lane * W;
-        uint64_t off = 0;
-        uint32_t n = 0;
-        bool big = false;
-        if (b < a.nblk) {
-            off = a.blk_off[b];
-            n = a.blk_len[b];
-            big = (off & 15) + (uint64_t)n > kRingBytes;
-        }
-        uint64_t m = __ballot(big);
-        while (m) {
-            const uint32_t l = uni((uint32_t)__builtin_ctzll(m));
-            m &= m - 1;
-            const uint64_t offj = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)off, l) |
-                                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(off >> 32), l) << 32);
-            const uint32_t nj = uni(__builtin_amdgcn_readlane(n, l));
-            decode_block_v2<G, NCH, false>(a, (uint32_t)(r0 + (uint64_t)l * W), ring, offj, nj);
-        }
-    }
-}
-
-template <int G, uint32_t NCH>
-int launch_large(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
-    // resident one-wave workgroups per CU: the 160 KiB LDS over the ring
-    constexpr uint32_t per_cu = 160 / NCH;
-    const uint32_t cus = ctx ? (uint32_t)lsm_ctx_num_cus(ctx) : 256u;
-    uint64_t grid = (uint64_t)cus * per_cu;
-    if (grid > a.nblk) grid = a.nblk;
-    if (grid == 0) return 0;
-    hipLaunchKernelGGL((decode_large_kernel<G, NCH>), dim3((uint32_t)grid), dim3(kWave), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
-// ---- group-per-block speculative path (DESC mode, blocks <= 4 KiB) --------
-//
-// A group of H lanes owns one block (64/H blocks per wave), staged whole in
-// an LDS slot by LDS-DMA.  Every round each lane t of a group reads the
-// length fields at pos + t*S', where S' (and K', V') is the shape of the
-// group's previous record, in one batch of independent LDS reads.  Lane 0's
-// position is always right; its fields are checked exactly (re-reading the
-// value length when its key length differs from K') and give the shape S of
-// the record at pos.  Lane t >= 1 is accepted iff S == S' and its own fields
-// equal (K, V) and the record fits: then the records before it all had shape
-// S and its position was right.  The group's leading run of accepted lanes
-// is emitted (coalesced descriptors) and the cursor jumps.  No scalar chase:
-// the control is per-lane VALU, and uniform blocks need two rounds per
-// group of H records.  Oversized blocks go to the wave path afterwards.
-template <int G, uint32_t H>
-__global__ __launch_bounds__(64) void decode_group_kernel(DecodeArgs a) {
-    constexpr uint32_t NB = kWave / H;  // blocks per wave
-    constexpr uint32_t kStride = kSlotBytes + 16;
-    __shared__ __attribute__((aligned(16))) uint32_t slots[NB * kStride / 4];
-    const uint32_t lane = lane_id();
-    const uint32_t grp = lane / H, t = lane % H;
-    const uint32_t b0 = blockIdx.x * NB;
-    const uint32_t b = b0 + grp;
-    const bool mine = b < a.nblk;
-    uint64_t off = 0;
-    uint32_t n = 0;
-    if (mine) {
-        off = a.blk_off[b];
-        n = a.blk_len[b];
-    }
-    const uint32_t h = (uint32_t)(off & 15);
-    const bool small = mine && (uint64_t)h + n <= kSlotBytes;
-    const uint64_t small_mask = __ballot(small);
-    for (uint32_t j = 0; j < NB; j++) {
-        if (!((small_mask >> (j * H)) & 1)) continue;
-        const uint64_t offj = uni64((uint32_t)__builtin_amdgcn_readlane((uint32_t)off, j * H) |
-                                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(off >> 32), j * H) << 32);
-        const uint32_t nj = __builtin_amdgcn_readlane(n, j * H);
-        const uint64_t a0 = offj & ~(uint64_t)15;
-        const uint32_t tot = (uint32_t)(((offj - a0) + nj + 15) & ~(uint64_t)15);
-        const rsrc_t r = make_rsrc(a.in + a0, tot);
-        const uint32_t nck = (tot + kChunk - 1) / kChunk;
-        for (uint32_t c = 0; c < nck; c++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                r, (__attribute__((address_space(3))) void *)&slots[(j * kStride + c * kChunk) / 4],
-                16, c * kChunk + lane * 16, 0, 0, kBlockLoadAux);
-    }
-    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-
-    const uint32_t sbase = grp * kStride + h;
-    auto rd = [&](uint32_t p) -> uint32_t {
-        const uint32_t sb = sbase + p;
-        const uint32_t *w = &slots[sb >> 2];
-        return funnel(w[0], w[1], sb);
-    };
-    uint64_t base = 0, cap = 0;
-    if (small) record_slots<G>(a, b, off, n, base, cap);
-    const uint32_t ncap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
-    const uint32_t glead = grp * H;  // group's lane 0
-
-    bool live = small;
-    int32_t status = LSM_OK;
-    uint32_t pos = 0, nr = 0;
-    uint32_t Kp = 0xFFFFFFFFu, Sp = 0xFFFFFFFFu;  // previous record's key length and size
-    while (__ballot(live)) {
-        uint32_t acc = 0, K = 0, V = 0, S = 0;
-        uint64_t x = 0;
-        const uint32_t p = pos + t * (Sp == 0xFFFFFFFFu ? 0u : Sp);
-        const uint32_t rem = n - pos;
-        if (live) {
-            // speculative field reads at p (independent of each other)
-            uint32_t kl = 0, vl;
-            if (G == LSM_GRAMMAR_V) {
-                vl = rd(p);
-            } else {
-                kl = rd(p);
-                vl = rd(p + 4 + (Kp == 0xFFFFFFFFu ? 0u : Kp));
-            }
-            // lane 0: exact record at pos
-            uint32_t k0 = kl, v0 = vl;
-            int32_t st0 = LSM_OK;
-            if (t == 0) {
-                if (rem == 0) {
-                    st0 = -1;  // clean end
-                } else if (rem < 4) {
-                    st0 = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN : LSM_ST_TRUNC_LEN_PREFIX;
-                } else if (G == LSM_GRAMMAR_V) {
-                    if (rem - 4 < v0) st0 = LSM_ST_TRUNC_VAL;
-                } else if (G == LSM_GRAMMAR_KV) {
-                    if (k0 > kKeyCap) st0 = LSM_ST_KEY_TOO_LONG;
-                    else if (rem - 4 < k0) st0 = LSM_ST_TRUNC_KEY;
-                    else {
-                        const uint32_t vp = pos + 4 + k0, rem2 = n - vp;
-                        if (rem2 < 4) st0 = LSM_ST_TRUNC_VLEN;
-                        else {
-                            if (k0 != Kp) v0 = rd(vp);
-                            if (v0 > kValCap) st0 = LSM_ST_VAL_TOO_LONG;
-                            else if (rem2 - 4 < v0) st0 = LSM_ST_TRUNC_VAL;
-                        }
-                    }
-                } else {
-                    if ((uint64_t)rem < 12ull + k0) st0 = LSM_ST_IDX_OVERRUN;
-                }
-                if (st0 == LSM_OK && nr >= ncap) st0 = LSM_ST_CAPACITY;
-            }
-            // broadcast lane 0's verdict and shape to its group
-            st0 = __shfl(st0, glead, kWave);
-            K = __shfl(k0, glead, kWave);
-            V = __shfl(v0, glead, kWave);
-            if (st0 != LSM_OK) {
-                if (st0 > 0) status = st0;
-                live = false;
-            } else {
-                S = G == LSM_GRAMMAR_V ? 4 + V : G == LSM_GRAMMAR_KV ? 8 + K + V : 12 + K;
-                bool ok;
-                if (t == 0) {
-                    ok = true;
-                } else {
-                    ok = (S == Sp) & ((uint64_t)p + S <= n) & (nr + t < ncap);
-                    if (G == LSM_GRAMMAR_V) ok = ok & (vl == V);
-                    else if (G == LSM_GRAMMAR_KV) ok = ok & (kl == K) & (vl == V);
-                    else ok = ok & (kl == K);
-                }
-                acc = ok;
-                if (G == LSM_GRAMMAR_IDX && ok) x = (uint64_t)rd(p + 8 + K) << 32 | rd(p + 4 + K);
-            }
-        }
-        // leading run of accepted lanes in each group
-        const uint64_t m = __ballot(acc);
-        constexpr uint64_t kGM = H == 64 ? ~0ull : ((1ull << (H % 64)) - 1);
-        const uint64_t gm = (m >> glead) & kGM;
-        const uint64_t inv = ~gm & kGM;
-        const uint32_t j = inv ? (uint32_t)__builtin_ctzll(inv) : H;
-        if (live && t < j) {
-            const uint64_t ro = off + p;
-            u32x4 d;
-            d.x = (uint32_t)ro;
-            d.y = (uint32_t)(ro >> 32);
-            d.z = G == LSM_GRAMMAR_V ? 0u : K;
-            d.w = G == LSM_GRAMMAR_IDX ? 8u : V;
-            a.desc[base + nr + t] = d;
-            if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + t] = (int64_t)x;
-        }
-        if (live) {
-            nr += j;
-            pos += j * S;
-            Kp = K;
-            Sp = S;
-        }
-    }
-    if (small && t == 0) {
-        a.nrec[b] = nr;
-        a.status[b] = status;
-    }
-    // Blocks too large for a slot: wave path with slot 0 as its ring.
-    const uint64_t big_mask = __ballot(mine && !small && t == 0);
-    for (uint32_t j = 0; j < NB; j++)
-        if ((big_mask >> (j * H)) & 1) {
-            const uint32_t bb = b0 + j;
-            decode_block_spec<G>(a, bb, slots, uni64(a.blk_off[bb]), uni(a.blk_len[bb]));
-        }
-}
-
-template <int G, uint32_t H>
-int launch_group(const DecodeArgs &a, hipStream_t s) {
-    constexpr uint32_t NB = kWave / H;
-    const uint32_t grid = (a.nblk + NB - 1) / NB;
-    hipLaunchKernelGGL((decode_group_kernel<G, H>), dim3(grid), dim3(kWave), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
-// ---- persistent, double-buffered speculative path (DESC mode, default) ----
-//
-// Each wave walks blocks w, w + W, w + 2W, ... (W = resident waves) with two
-// 4 KiB ring slots: block k+1's four 1 KiB LDS-DMAs are issued before block k
-// is decoded, and a static s_waitcnt vmcnt(4) (the four younger DMAs may stay
-// in flight) releases block k.  So every wave always has a block in flight
-// and the DMA latency hides behind the previous block's chase -- the
-// occupancy needed for HBM rate (Little's law: ~18 blocks per CU at ~3 us)
-// is reached with 20 waves per CU.  Metadata of block k+2 is prefetched with
-// scalar loads.  Blocks larger than the 4 KiB ring stream on through the
-// ring's own refills.
-__device__ __forceinline__ void stage_block(uint32_t *ring, const uint8_t *in, uint64_t off,
-                                            uint32_t n) {
-    const uint64_t a0 = off & ~(uint64_t)15;
-    uint64_t tot = ((off - a0) + n + 15) & ~(uint64_t)15;
-    if (tot > kRingBytes) tot = kRingBytes;  // first 4 KiB; larger blocks refill later
-    const rsrc_t r = make_rsrc(in + a0, (uint32_t)tot);
-    const uint32_t v = lane_id() * 16;
-#pragma unroll
-    for (uint32_t c = 0; c < kNChunk; c++)  // always 4 ops: OOB chunks read as 0
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            r, (__attribute__((address_space(3))) void *)&ring[c * (kChunk / 4)], 16, c * kChunk + v,
-            0, 0, kBlockLoadAux);
-}
-
-constexpr uint32_t kPipeWaves = 4;  // waves per workgroup (32 KiB LDS)
-
-template <int G>
-__global__ __launch_bounds__(256) void decode_pipe_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t slots[kPipeWaves][2][kRingWords];
-    const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint32_t W = gridDim.x * kPipeWaves;
-    uint32_t b = uni(blockIdx.x * kPipeWaves + wave);
-    if (b >= a.nblk) return;
-    uint64_t off = uni64(a.blk_off[b]);
-    uint32_t n = uni(a.blk_len[b]);
-    stage_block(slots[wave][0], a.in, off, n);
-    uint32_t nb = b + W;
-    uint64_t noff = 0;
-    uint32_t nn = 0;
-    if (nb < a.nblk) {
-        noff = uni64(a.blk_off[nb]);
-        nn = uni(a.blk_len[nb]);
-    }
-    for (uint32_t k = 0;; k++) {
-        uint32_t *cur = slots[wave][k & 1];
-        const bool more = nb < a.nblk;
-        if (more) {
-            stage_block(slots[wave][(k + 1) & 1], a.in, noff, nn);
-            __asm__ __volatile__("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        // prefetch metadata two blocks ahead
-        const uint32_t nnb = nb + W;
-        uint64_t poff = 0;
-        uint32_t pn = 0;
-        if (more && nnb < a.nblk) {
-            poff = uni64(a.blk_off[nnb]);
-            pn = uni(a.blk_len[nnb]);
-        }
-        decode_block_spec<G>(a, b, cur, off, n, true);
-        if (!more) break;
-        b = nb;
-        off = noff;
-        n = nn;
-        nb = nnb;
-        noff = poff;
-        nn = pn;
-    }
-}
-
-template <int G>
-int launch_pipe(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
-    // 5 workgroups (20 waves) per CU fit the LDS; a fixed residency-sized grid.
-    const uint32_t cus = ctx ? (uint32_t)lsm_ctx_num_cus(ctx) : 256u;
-    const uint32_t want = cus * 5;
-    const uint32_t need = (a.nblk + kPipeWaves - 1) / kPipeWaves;
-    const uint32_t grid = need < want ? need : want;
-    hipLaunchKernelGGL((decode_pipe_kernel<G>), dim3(grid), dim3(kWave * kPipeWaves), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
-template <int G, uint32_t K, uint32_t WPG = kWavesPerWG>
-int launch_spec(const DecodeArgs &a, hipStream_t s) {
-    const uint32_t waves = (a.nblk + K - 1) / K;
-    const uint32_t grid = (waves + WPG - 1) / WPG;
-    hipLaunchKernelGGL((decode_spec_kernel<G, K, WPG>), dim3(grid), dim3(kWave * WPG), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
-template <int G, bool ARENA>
-__global__ __launch_bounds__(256) void decode_blocks_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[kWavesPerWG][kRingWords];
-    const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint32_t b = uni(blockIdx.x * kWavesPerWG + wave);
-    if (b >= a.nblk) return;
-    decode_block_wave<G, ARENA>(a, b, ring[wave]);
-}
-
-// ---- lane-per-block path (DESC mode) ----------------------------------------
-//
-// The record chain is serial inside a block, so a wave-uniform chase is bound
-// by the CU's single scalar unit (~1 instruction/cycle/CU).  Here each lane
-// chases its own block instead: a one-wave workgroup owns kLaneBlocks blocks,
-// LDS-DMAs each (<= 4 KiB + alignment) into a private slot with four
-// coalesced 1 KiB loads, then every lane walks its block's length fields with
-// per-lane unaligned LDS reads (two ds_read_b32 + v_alignbyte per field) and
-// writes its descriptors.  Slots are skewed by 16 bytes so lanes walking
-// identically laid out blocks hit different banks.  Blocks that do not fit a
-// slot are decoded afterwards by the wave path.
-
-template <int G, uint32_t kLaneBlocks>
-__global__ __launch_bounds__(64) void decode_lanes_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t slots[kLaneBlocks * kSlotStride / 4];
-    stamp(0);
-    const uint32_t lane = lane_id();
-    const uint32_t b0 = blockIdx.x * kLaneBlocks;
-    const uint32_t b = b0 + lane;
-    const bool mine = lane < kLaneBlocks && b < a.nblk;
-    uint64_t off = 0;
-    uint32_t n = 0;
-    if (mine) {
-        off = a.blk_off[b];
-        n = a.blk_len[b];
-    }
-    const uint32_t h = (uint32_t)(off & 15);
-    const bool small = mine && (uint64_t)h + n <= kSlotBytes;
-    const uint64_t small_mask = __ballot(small);
-
-    // Stage every small block into its slot: 4 x 1 KiB LDS-DMA per block.
-    for (uint32_t j = 0; j < kLaneBlocks; j++) {
-        if (!((small_mask >> j) & 1)) continue;
-        const uint64_t offj = uni64(__shfl(off, j, kWave));
-        const uint32_t nj = uni(__shfl(n, j, kWave));
-        const uint64_t a0 = offj & ~(uint64_t)15;
-        const uint32_t tot = (uint32_t)(((offj - a0) + nj + 15) & ~(uint64_t)15);
-        const rsrc_t r = make_rsrc(a.in + a0, tot);
-        const uint32_t nck = (tot + kChunk - 1) / kChunk;
-        for (uint32_t c = 0; c < nck; c++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                r, (__attribute__((address_space(3))) void *)&slots[(j * kSlotStride + c * kChunk) / 4],
-                16, c * kChunk + lane * 16, 0, 0, kBlockLoadAux);
-    }
-    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(1);
-
-    if (small) {
-        // Byte address of this lane's slot; reads past the slot return
-        // another slot's bytes or 0 (LDS bounds) and are never accepted.
-        const uint32_t sbase = lane * kSlotStride + h;
-        auto rd = [&](uint32_t p) -> uint32_t {
-            const uint32_t sb = sbase + p;
-            const uint32_t *w = &slots[sb >> 2];
-            return funnel(w[0], w[1], sb);
-        };
-        uint64_t base, cap;
-        record_slots<G>(a, b, off, n, base, cap);
-        u32x4 *dp = a.desc + base;
-        int64_t *xp = a.idx_value ? a.idx_value + base : nullptr;
-        const uint32_t ncap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
-        uint32_t pos = 0, nr = 0;
-        // Straight-line record step; a failing check ends the lane's loop and
-        // the (rare) status is resolved once afterwards from pos.
-        for (;;) {
-            const uint32_t rem = n - pos;
-            uint32_t klen = 0, vlen, vp = pos, nxt;
-            bool ok;
-            if (G == LSM_GRAMMAR_V) {
-                vlen = rd(pos);
-                ok = (rem >= 4) & (rem - 4 >= vlen);
-                nxt = pos + 4 + vlen;
-            } else if (G == LSM_GRAMMAR_KV) {
-                klen = rd(pos);
-                vp = pos + 4 + klen;
-                vlen = rd(vp);
-                const uint32_t rem2 = n - vp;
-                ok = (rem >= 4) & (klen <= kKeyCap) & (rem - 4 >= klen) & (rem2 >= 4) &
-                     (vlen <= kValCap) & (rem2 - 4 >= vlen);
-                nxt = vp + 4 + vlen;
-            } else {
-                klen = rd(pos);
-                vp = pos + 4 + klen;
-                vlen = 8;
-                ok = (rem >= 12) & (rem - 12 >= klen);
-                nxt = vp + 8;
-            }
-            ok = ok & (nr < ncap);
-            if (!ok) break;
-            const uint64_t ro = off + pos;
-            u32x4 d;
-            d.x = (uint32_t)ro;
-            d.y = (uint32_t)(ro >> 32);
-            d.z = klen;
-            d.w = vlen;
-            dp[nr] = d;
-            if (G == LSM_GRAMMAR_IDX && xp) xp[nr] = (int64_t)((uint64_t)rd(vp + 4) << 32 | rd(vp));
-            nr++;
-            pos = nxt;
-        }
-        // Status of the stop at pos (same precedence as the reference).
-        int32_t status = LSM_OK;
-        const uint32_t rem = n - pos;
-        if (rem != 0) {
-            if (G == LSM_GRAMMAR_V) {
-                status = rem < 4 ? LSM_ST_TRUNC_LEN_PREFIX
-                       : rem - 4 < rd(pos) ? LSM_ST_TRUNC_VAL : LSM_ST_CAPACITY;
-            } else if (G == LSM_GRAMMAR_KV) {
-                if (rem < 4) status = LSM_ST_TRUNC_LEN_PREFIX;
-                else {
-                    const uint32_t klen = rd(pos);
-                    if (klen > kKeyCap) status = LSM_ST_KEY_TOO_LONG;
-                    else if (rem - 4 < klen) status = LSM_ST_TRUNC_KEY;
-                    else {
-                        const uint32_t vp = pos + 4 + klen, rem2 = n - vp;
-                        const uint32_t vlen = rem2 >= 4 ? rd(vp) : 0;
-                        status = rem2 < 4 ? LSM_ST_TRUNC_VLEN
-                               : vlen > kValCap ? LSM_ST_VAL_TOO_LONG
-                               : rem2 - 4 < vlen ? LSM_ST_TRUNC_VAL : LSM_ST_CAPACITY;
-                    }
-                }
-            } else {
-                status = (rem < 12 || rem - 12 < rd(pos)) ? LSM_ST_IDX_OVERRUN : LSM_ST_CAPACITY;
-            }
-        }
-        a.nrec[b] = nr;
-        a.status[b] = status;
-    }
-
-    stamp(2);
-    // Blocks too large for a slot: whole-wave streaming path, slot 0 as ring.
-    const uint64_t big_mask = __ballot(mine && !small);
-    for (uint32_t j = 0; j < kLaneBlocks; j++)
-        if ((big_mask >> j) & 1) decode_block_wave<G, false>(a, b0 + j, slots);
+        decode_block_v2<G, NCH, false, ARENA>(a, b, ring, tab, off, n);
     stamp(3);
 }
 
@@ -1474,242 +894,9 @@ int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void
     return 0;
 }
 
-// ---- streaming lane-per-block path (DESC mode, default) ------------------
-//
-// Each lane owns one block of any size and chases it through a per-wave LDS
-// ring of W rows; row r holds stream bytes [16r, 16r+16) of every lane's own
-// block, gathered by ONE global_load_lds_dwordx4 per row (per-lane source
-// address, lane L's 16 bytes land at row + 16L).  A round refills rows
-// [r_lo, r_lo + W) (r_lo = the lowest row any lane still needs), waits once,
-// then every lane consumes as many length fields as the window holds.  The
-// chase is a field-granular state machine so one long key never stalls the
-// window, and rows that every lane has jumped over are never loaded.
-template <int G, uint32_t BL, uint32_t W>
-__global__ __launch_bounds__(64) void decode_stream_kernel(DecodeArgs a) {
-    constexpr uint32_t kRow = BL * 16;  // bytes per ring row
-    __shared__ __attribute__((aligned(16))) uint32_t ring[W * kRow / 4];
-    stamp(0);
-    const uint32_t lane = lane_id();
-    const uint32_t b = blockIdx.x * BL + lane;
-    const bool mine = lane < BL && b < a.nblk;
-    uint64_t off = 0;
-    uint32_t n = 0;
-    if (mine) {
-        off = a.blk_off[b];
-        n = a.blk_len[b];
-    }
-    const uint64_t a0 = off & ~(uint64_t)15;
-    const uint32_t h = (uint32_t)(off - a0);
-    const uint8_t *g = a.in + a0;
-    const uint32_t rows = (uint32_t)(((uint64_t)h + n + 15) / 16);
-    uint64_t base = 0, cap = 0;
-    if (mine) record_slots<G>(a, b, off, n, base, cap);
-    u32x4 *dp = a.desc + base;
-    int64_t *xp = (G == LSM_GRAMMAR_IDX && a.idx_value) ? a.idx_value + base : nullptr;
-    const uint32_t ncap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
-
-    const uint32_t lane_w = lane * 4;  // this lane's dword inside a row
-    auto dword = [&](uint32_t i) -> uint32_t {  // stream dword i of this lane
-        return ring[((i >> 2) % W) * (kRow / 4) + lane_w + (i & 3)];
-    };
-
-    bool active = mine;
-    int32_t status = LSM_OK;
-    uint32_t pos = 0, vp = 0, klen = 0, phase = 0, nr = 0;
-    uint32_t r_lo = 0, r_loaded = 0;
-    for (;;) {
-        // Refill rows [max(r_loaded, r_lo), r_lo + W): one gather per row.
-        const uint32_t r1 = r_lo + W;
-        for (uint32_t r = r_loaded > r_lo ? r_loaded : r_lo; r < r1; r++) {
-            if (active && r < rows)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(g + 16 * (uint64_t)r),
-                    (__attribute__((address_space(3))) void *)&ring[(r % W) * (kRow / 4)], 16, 0, 0);
-        }
-        r_loaded = r1;
-        __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t win_end = 16 * r1;
-
-        // Consume every field the window holds.
-        while (active) {
-            const uint32_t fp = phase ? vp : pos;
-            const uint32_t rem = n - fp;
-            if (phase == 0 && rem == 0) { active = false; break; }  // clean end
-            const uint32_t need = (G == LSM_GRAMMAR_IDX && phase) ? 8 : 4;
-            if (rem < need) {
-                status = G == LSM_GRAMMAR_IDX ? LSM_ST_IDX_OVERRUN
-                       : phase ? LSM_ST_TRUNC_VLEN : LSM_ST_TRUNC_LEN_PREFIX;
-                active = false;
-                break;
-            }
-            const uint32_t sb = h + fp;
-            if (sb + need > win_end) break;  // next round
-            const uint32_t i = sb >> 2;
-            const uint32_t d0 = dword(i), d1 = dword(i + 1);
-            const uint32_t f = funnel(d0, d1, sb);
-            if (phase == 0 && G != LSM_GRAMMAR_V) {
-                klen = f;
-                if (G == LSM_GRAMMAR_KV) {
-                    if (klen > kKeyCap) { status = LSM_ST_KEY_TOO_LONG; active = false; break; }
-                    if (rem - 4 < klen) { status = LSM_ST_TRUNC_KEY; active = false; break; }
-                } else if ((uint64_t)rem < 12ull + klen) {
-                    status = LSM_ST_IDX_OVERRUN;
-                    active = false;
-                    break;
-                }
-                vp = pos + 4 + klen;
-                phase = 1;
-                continue;
-            }
-            // value length (V, KV) or index offset (IDX): the record is complete
-            uint32_t vlen;
-            uint64_t xval = 0;
-            if (G == LSM_GRAMMAR_IDX) {
-                xval = (uint64_t)funnel(d1, dword(i + 2), sb) << 32 | f;
-                vlen = 8;
-            } else {
-                vlen = f;
-                if (G == LSM_GRAMMAR_KV && vlen > kValCap) { status = LSM_ST_VAL_TOO_LONG; active = false; break; }
-                if (rem - 4 < vlen) { status = LSM_ST_TRUNC_VAL; active = false; break; }
-            }
-            if (nr >= ncap) { status = LSM_ST_CAPACITY; active = false; break; }
-            const uint64_t ro = off + pos;
-            u32x4 d;
-            d.x = (uint32_t)ro;
-            d.y = (uint32_t)(ro >> 32);
-            d.z = G == LSM_GRAMMAR_V ? 0u : klen;
-            d.w = vlen;
-            dp[nr] = d;
-            if (G == LSM_GRAMMAR_IDX && xp) xp[nr] = (int64_t)xval;
-            nr++;
-            const uint32_t rs = G == LSM_GRAMMAR_V ? pos : vp;
-            pos = G == LSM_GRAMMAR_IDX ? rs + 8 : rs + 4 + vlen;
-            phase = 0;
-        }
-        // Lowest row any lane still needs; all lanes done -> exit.
-        uint32_t need_row = active ? (h + (phase ? vp : pos)) >> 4 : 0xFFFFFFFFu;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t o = __shfl_xor(need_row, d, kWave);
-            need_row = o < need_row ? o : need_row;
-        }
-        r_lo = uni(need_row);
-        if (r_lo == 0xFFFFFFFFu) break;
-    }
-    stamp(2);
-    if (mine) {
-        a.nrec[b] = nr;
-        a.status[b] = status;
-    }
-    stamp(3);
-}
-
-template <int G, uint32_t BL, uint32_t W>
-int launch_stream(const DecodeArgs &a, hipStream_t s) {
-    uint32_t grid = (a.nblk + BL - 1) / BL;
-    hipLaunchKernelGGL((decode_stream_kernel<G, BL, W>), dim3(grid), dim3(kWave), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
-template <int G, uint32_t B>
-int launch_lanes(const DecodeArgs &a, hipStream_t s) {
-    uint32_t grid = (a.nblk + B - 1) / B;
-    hipLaunchKernelGGL((decode_lanes_kernel<G, B>), dim3(grid), dim3(kWave), 0, s, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    return 0;
-}
-
 template <int G, bool ARENA>
-int launch_decode(lsm_ctx *ctx, const DecodeArgs &a, hipStream_t s) {
-    if (!ARENA) {
-        // Default: wave-per-block with speculative parallel runs, one wave per
-        // workgroup (finer dispatch/retire granularity than 4-wave groups:
-        // 4413 vs 4250 GiB/s on decode4k with nt loads, same box).
-        // LSM_DECODE_KERNEL selects variants for A/B measurement.
-        static const int variant = [] {
-            const char *e = getenv("LSM_DECODE_KERNEL");
-            if (!e) return 0;
-            if (!strcmp(e, "stream64x16")) return 1;
-            if (!strcmp(e, "stream32x64")) return 2;
-            if (!strcmp(e, "stream64x32")) return 3;
-            if (!strcmp(e, "lanes")) return 9;
-            if (!strcmp(e, "stream32x32")) return 4;
-            if (!strcmp(e, "spec4")) return 10;
-            if (!strcmp(e, "spec")) return 30;
-            if (!strcmp(e, "large8")) return 40;
-            if (!strcmp(e, "v2split")) return 41;
-            if (!strcmp(e, "v2r4")) return 42;
-            if (!strcmp(e, "v2r6")) return 43;
-            if (!strcmp(e, "v2r5")) return 44;
-            if (!strcmp(e, "spec_w1")) return 31;
-            if (!strcmp(e, "spec_w2")) return 32;
-            if (!strcmp(e, "pipe")) return 33;
-            if (!strcmp(e, "group64")) return 20;
-            if (!strcmp(e, "group32")) return 21;
-            if (!strcmp(e, "group16")) return 22;
-            if (!strcmp(e, "spec2")) return 11;
-            if (!strcmp(e, "spec8")) return 12;
-            if (!strcmp(e, "spec16")) return 13;
-            return 0;
-        }();
-        switch (variant) {
-        // one wave per block, 8 KiB ring: decode4k equal to a 4 KiB ring,
-        // decode64k 0.71 vs 0.58 of HBM peak (more in flight per wave)
-        case 0: return launch_v2<G, 8>(a, s);
-        case 41: {
-            // v2 for blocks that fit the 4 KiB ring, then the deep-ring
-            // persistent kernel for the larger ones
-            DecodeArgs b = a;
-            b.split = 1;
-            const int rc = launch_v2<G, kNChunk>(b, s);
-            return rc ? rc : launch_large<G, kLargeNCH>(ctx, b, s);
-        }
-        case 42: return launch_v2<G, kNChunk>(a, s);
-        case 43: return launch_v2<G, 6>(a, s);
-        case 44: return launch_v2<G, 5>(a, s);
-        case 40: {
-            DecodeArgs b = a;
-            b.split = 1;
-            const int rc = launch_spec<G, 1, 1>(b, s);
-            return rc ? rc : launch_large<G, 8>(ctx, b, s);
-        }
-        case 33: return launch_pipe<G>(ctx, a, s);
-        case 30: return launch_spec<G, 1>(a, s);
-        case 31: return launch_spec<G, 1, 1>(a, s);
-        case 32: return launch_spec<G, 1, 2>(a, s);
-        case 20: return launch_group<G, 64>(a, s);
-        case 21: return launch_group<G, 32>(a, s);
-        case 22: return launch_group<G, 16>(a, s);
-        case 10: return launch_spec<G, 4>(a, s);
-        case 11: return launch_spec<G, 2>(a, s);
-        case 12: return launch_spec<G, 8>(a, s);
-        case 13: return launch_spec<G, 16>(a, s);
-        case 4: return launch_stream<G, 32, 32>(a, s);
-        case 1: return launch_stream<G, 64, 16>(a, s);
-        case 2: return launch_stream<G, 32, 64>(a, s);
-        case 3: return launch_stream<G, 64, 32>(a, s);
-        case 9: break;
-        default: return launch_stream<G, 32, 32>(a, s);
-        }
-        // Blocks per wave (LDS slots): 3 admits 13 one-wave workgroups per CU.
-        static const int lb = [] {
-            const char *e = getenv("LSM_LANE_BLOCKS");
-            return e ? atoi(e) : 3;
-        }();
-        switch (lb) {
-        case 3: return launch_lanes<G, 3>(a, s);
-        case 4: return launch_lanes<G, 4>(a, s);
-        case 8: return launch_lanes<G, 8>(a, s);
-        case 15: return launch_lanes<G, 15>(a, s);
-        case 7: return launch_lanes<G, 7>(a, s);
-        default: return launch_lanes<G, 3>(a, s);
-        }
-    } else {
-        uint32_t grid = (a.nblk + kWavesPerWG - 1) / kWavesPerWG;
-        hipLaunchKernelGGL((decode_blocks_kernel<G, ARENA>), dim3(grid),
-                           dim3(kWave * kWavesPerWG), 0, s, a);
-    }
+int launch_decode(const DecodeArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((decode_v2_kernel<G, kRingChunks, ARENA>), dim3(a.nblk), dim3(kWave), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -1994,14 +1181,14 @@ __global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
 // wal.Recover chases a whole log (~1.7 MB, ~44k records for a 2 MiB
 // memtable) as one serial chain; one wave per log would take milliseconds.
 // The log is cut into 16 KiB segments, one wave each:
-//   wal_seg_kernel: two waves per segment guess where its first record starts
-//     (the first position from which three records in a row have plausible
+//   wal_seg_lanes_kernel: the segment guesses where its first record starts
+//     (the first position from which two records in a row have plausible
 //     lengths).  A record is two length-prefixed fields, so a chain started
 //     at a value-length field looks just as plausible, one field out of
-//     phase, and never meets the true chain: wave 0 chases from the guess g,
-//     wave 1 from g + 4 + u32(g) (the record after the value if g was a
-//     value length).  Each chases to the first record starting in the next
-//     segment and writes its records to a scratch area of its own.
+//     phase, and never meets the true chain: phase 0 starts at the guess g,
+//     phase 1 at g + 4 + u32(g) (the record after the value if g was a
+//     value length).  Each phase is chased to the first record starting in
+//     the next segment, its records written to a scratch area of its own.
 //   wal_stitch_kernel: one wave per log walks the segments in order with the
 //     true chain position e (0 at the start).  A chain of the segment that
 //     starts at e is the serial chase's (same start, same deterministic
@@ -2010,10 +1197,7 @@ __global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
 //   wal_compact_kernel: each segment's records move to their final slots.
 // The result equals one serial chase for any input; guesses only decide how
 // much is chased twice.
-#ifndef LSM_WAL_SEG_KIB
-#define LSM_WAL_SEG_KIB 16  // other sizes: diagnostic builds only (an open parity item)
-#endif
-constexpr uint32_t kWalSeg = LSM_WAL_SEG_KIB * 1024;
+constexpr uint32_t kWalSeg = 16 * 1024;  // 12 and 8 KiB measured slower
 constexpr uint32_t kWalSegSlots = kWalSeg / 8 + 1;  // records starting in a segment
 
 struct WalSeg {
@@ -2044,86 +1228,7 @@ __device__ __forceinline__ void wal_slots(const WalArgs &a, uint32_t w, uint64_t
     }
 }
 
-__global__ __launch_bounds__(64) void wal_seg_kernel(WalArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
-    const uint32_t s = blockIdx.x >> 1, ph = blockIdx.x & 1, w = blockIdx.y, lane = lane_id();
-    const uint32_t len = uni(a.wal_len[w]);
-    const uint64_t off = uni64(a.wal_off[w]);
-    const uint64_t q = ((uint64_t)w * a.segs + s) * 2 + ph;
-    WalSeg &T = a.seg[q];
-    const uint32_t start = s * kWalSeg;
-    if (start >= len || len > a.max_len) {
-        if (lane == 0) T = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-        return;
-    }
-    uint32_t g = start;
-    if (s > 0) {
-        // stage up to 4 KiB of the segment head, then test 64 candidate
-        // starts per round: records of plausible lengths in a row (key <=
-        // 1 KiB, value <= 1 MiB, inside the log), at least two of them read
-        // within the staged bytes or one that ends the log; a guess only
-        // decides what the stitch must re-chase, never the result
-        const uint64_t a0 = (off + start) & ~(uint64_t)15;
-        const uint32_t h = (uint32_t)(off + start - a0);
-        const uint32_t W = len - start < kRingBytes - 16 ? len - start : kRingBytes - 16;
-        const rsrc_t r = make_rsrc(a.wal + a0, (h + W + 15) & ~15u);
-#pragma unroll
-        for (uint32_t c = 0; c < kNChunk; c++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                r, (__attribute__((address_space(3))) void *)&ring[c * (kChunk / 4)], 16,
-                c * kChunk + lane * 16, 0, 0, kBlockLoadAux);
-        __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-        auto rd = [&](uint32_t q) -> uint32_t {
-            const uint32_t sb = h + q;
-            return funnel(ring[sb >> 2], ring[(sb >> 2) + 1], sb);
-        };
-        const uint32_t rlen = W < 2048 ? W : 2048;
-        g = 0xFFFFFFFFu;
-        for (uint32_t t0 = 0; t0 < rlen && g == 0xFFFFFFFFu; t0 += kWave) {
-            const uint32_t p = t0 + lane;
-            bool ok = p < rlen;
-            uint32_t q = p, seen = 0;
-            for (int rec = 0; rec < 3 && ok; rec++) {
-                if ((uint64_t)start + q == len) { seen = 2; break; }  // ends the log exactly
-                if (q + 8 > W) break;
-                const uint32_t k = rd(q);
-                if (k > 1024 || (uint64_t)start + q + 8 + k > len) { ok = false; break; }
-                if (q + 8 + k > W) break;
-                const uint32_t v = rd(q + 4 + k);
-                if (v > (1u << 20) || (uint64_t)start + q + 8 + k + v > len) { ok = false; break; }
-                q += 8 + k + v;
-                seen++;
-            }
-            ok = ok && seen >= 2;
-            const uint64_t m = __ballot(ok);
-            if (m) g = start + t0 + (uint32_t)__builtin_ctzll(m);
-        }
-        if (g == 0xFFFFFFFFu) g = start;
-        if (ph == 1) {  // the other phase: g read as a value length
-            const uint32_t v = g - start + 4 <= W ? rd(g - start) : 0xFFFFFFFFu;
-            g = (uint64_t)g + 4 + v <= len ? g + 4 + v : len;
-        }
-    } else if (ph == 1) {
-        if (lane == 0) T = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};  // segment 0 starts at 0
-        return;
-    }
-    g = uni(g);
-    if (g >= len || g >= start + kWalSeg) {
-        if (lane == 0) T = WalSeg{g, g, 0, 0};
-        return;
-    }
-    const uint32_t stop = (start + kWalSeg < len ? start + kWalSeg : len) - g;
-    DecodeArgs d = {};
-    d.in = a.wal;
-    d.desc = a.scratch;
-    uint32_t nr = 0, endp = 0;
-    int32_t st = LSM_OK;
-    decode_range_any<LSM_GRAMMAR_KV, 8>(d, ring, off + g, len - g, q * kWalSegSlots, kWalSegSlots,
-                                        nr, st, stop, &endp);
-    if (lane == 0) T = WalSeg{g, g + endp, nr, st};
-}
-
-// Lane-parallel form of wal_seg_kernel (the default).  WAL records are small
+// Lane-parallel segment chase.  WAL records are small
 // (~40 B for go-lsm's benchmark) and vary in shape, so one wave chasing a
 // 16 KiB segment spends its time in ~400 serial exact steps.  Here the
 // segment [g, E) (g the segment's guess as above, E its end) is split into
@@ -2144,10 +1249,6 @@ __global__ __launch_bounds__(64) void wal_seg_kernel(WalArgs a) {
 // and measured 603 GiB/s on the wal bench; + 3.5 KiB (8 waves) 552 and + 4 KiB
 // (20,496 B: 7 waves) 542.  Reads past the tail go through the buffer resource.
 constexpr uint32_t kWalStage = kWalSeg + 1024;
-#ifndef LSM_WAL_DBG
-#define LSM_WAL_DBG 0  // timing diagnostics only: 1 skips the write-out, 2 phase 1
-#endif
-constexpr uint32_t kWalStage4k = kWalSeg + 4096;  // LSM_WAL_KERNEL=stage4k (A/B)
 
 struct WalLog {
     rsrc_t r;       // the log's bytes, offsets relative to the aligned base
@@ -2213,9 +1314,9 @@ struct WalLog {
 // One wave serves both phases of a segment: the shares' chains do not depend
 // on the segment's entry, only lane 0's does, so they are chased once and
 // stitched twice (from g and from g read as a value length).
-template <uint32_t STAGE>  // bytes copied to LDS (0: read through the caches)
 __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE ? STAGE / 4 + 4 : 4];
+    constexpr uint32_t STAGE = kWalStage;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 4];
     const uint32_t s = blockIdx.x, w = blockIdx.y, lane = lane_id();
     const uint32_t len = uni(a.wal_len[w]);
     const uint64_t off = uni64(a.wal_off[w]);
@@ -2230,10 +1331,10 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     L.h = (uint32_t)(off - base);
     L.len = len;
     L.r = make_rsrc(a.wal + base, (L.h + len + 15) & ~15u);
-    L.s0 = STAGE ? (L.h + start) & ~15u : 0xFFFFFFF0u;
+    L.s0 = (L.h + start) & ~15u;
     L.sz = STAGE;
     L.lds = stage;
-    if (STAGE) {
+    {
         // the segment + a tail (the loads are already all in flight: staging
         // by buffer_load ... lds measured no faster)
         for (uint32_t c = 0; c < STAGE / 16; c += kWave) {
@@ -2283,7 +1384,7 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     if (e0 != 0xFFFFFFFFu) L.chase(e0, se, c0, x0, st0);
     if (e1 != 0xFFFFFFFFu) L.chase(e1, se, c1, x1, st1);
     // 2. + 3. per phase: stitch from the entry, then write the accepted chains
-    for (uint32_t ph = 0; ph < ((LSM_WAL_DBG & 2) ? 1 : 2); ph++) {
+    for (uint32_t ph = 0; ph < 2; ph++) {
         const uint64_t q = q0 + ph;
         const uint32_t gp = ph ? g1 : g;
         if (ph == 1 && s == 0) {  // segment 0 starts at 0
@@ -2403,7 +1504,7 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         }
         uint32_t tot;
         const uint32_t pre = wave_excl_scan(acc_cnt, &tot);
-        if (acc_cnt && !(LSM_WAL_DBG & 1)) {
+        if (acc_cnt) {
             u32x4 *dst = a.scratch + q * kWalSegSlots + pre;
             uint32_t p = acc_entry;
             for (uint32_t i = 0; i < acc_cnt; i++) {
@@ -2698,20 +1799,14 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
     a.arena_base = out->arena_base;
     a.key_arena_off = out->key_arena_off;
     a.val_arena_off = out->val_arena_off;
-    a.split = 0;
-    static const uint32_t dbg = [] {
-        const char *e = getenv("LSM_DECODE_DBG");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    a.dbg = dbg;
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (grammar) {
-    case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true>(ctx, a, s)
-                                     : launch_decode<LSM_GRAMMAR_V, false>(ctx, a, s);
-    case LSM_GRAMMAR_KV: return arena ? launch_decode<LSM_GRAMMAR_KV, true>(ctx, a, s)
-                                      : launch_decode<LSM_GRAMMAR_KV, false>(ctx, a, s);
-    default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true>(ctx, a, s)
-                          : launch_decode<LSM_GRAMMAR_IDX, false>(ctx, a, s);
+    case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true>(a, s)
+                                     : launch_decode<LSM_GRAMMAR_V, false>(a, s);
+    case LSM_GRAMMAR_KV: return arena ? launch_decode<LSM_GRAMMAR_KV, true>(a, s)
+                                      : launch_decode<LSM_GRAMMAR_KV, false>(a, s);
+    default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true>(a, s)
+                          : launch_decode<LSM_GRAMMAR_IDX, false>(a, s);
     }
 }
 
@@ -2746,15 +1841,7 @@ extern "C" int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t
     a.seg = reinterpret_cast<WalSeg *>(ws + n * 2 * kWalSegSlots * 16);
     a.fin = reinterpret_cast<uint32_t *>(ws + n * 2 * (kWalSegSlots * 16 + sizeof(WalSeg)));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    static const char *wk = getenv("LSM_WAL_KERNEL");
-    if (wk && !strcmp(wk, "serial"))
-        hipLaunchKernelGGL(wal_seg_kernel, dim3(2 * a.segs, nwal), dim3(kWave), 0, s, a);
-    else if (wk && !strcmp(wk, "lanes"))  // shares read through the caches, no LDS copy
-        hipLaunchKernelGGL(wal_seg_lanes_kernel<0>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
-    else if (wk && !strcmp(wk, "stage4k"))
-        hipLaunchKernelGGL(wal_seg_lanes_kernel<kWalStage4k>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
-    else
-        hipLaunchKernelGGL(wal_seg_lanes_kernel<kWalStage>, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(wal_seg_lanes_kernel, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_stitch_kernel, dim3(nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_compact_kernel, dim3(a.segs, nwal), dim3(256), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
@@ -2793,7 +1880,7 @@ extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t
                                           (size_t)nfile * sizeof(SstWork));
     LSM_HIP_CHECK(hipMemsetAsync(a.fail, 0xFF, (size_t)nfile * 8, s));
     // parallel passes: ~kSstWgs workgroups over the batch, at most 64 per file
-    static const uint32_t kSstWgs = getenv("LSM_SST_WGS") ? (uint32_t)atoi(getenv("LSM_SST_WGS")) : 2048;
+    constexpr uint32_t kSstWgs = 2048;
     uint32_t g = (kSstWgs + nfile - 1) / nfile;
     if (g > 64) g = 64;
     if (g == 0) g = 1;

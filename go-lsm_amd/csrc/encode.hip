@@ -1282,7 +1282,7 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
                                                                  const lsm_sst_meta *meta,
                                                                  uint32_t nfile, const uint8_t *keys,
                                                                  const uint64_t *koff, uint64_t nkeys,
-                                                                 uint8_t *hit, uint32_t nobloom,
+                                                                 uint8_t *hit,
                                                                  const uint32_t *grouped) {
     __shared__ McFile tile[kMcTile];
     if (*grouped) return;  // the files are sorted and disjoint: mc_* kernels answer
@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
                     r = F.k == 0 || m != 0;
                     // Test's answer is the AND of all k bits (its early exit
                     // changes nothing): sixteen loads in flight at a time
-                    for (uint32_t j0 = 0; j0 < F.k && r && !nobloom; j0 += 16) {
+                    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
                         uint32_t bits = 1;
 #pragma unroll
                         for (uint32_t u = 0; u < 16; u++) {
@@ -1647,7 +1647,7 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nf
 // 1 the scatter wrote.  The hashes of the first probes are loaded before the
 // LDS fill.
 __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *img, uint32_t nfile, McWs w,
-                                                                 uint8_t *hit, uint32_t dbg) {
+                                                                 uint8_t *hit) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
     if (!w.flag[0]) return;
     const uint32_t f = blockIdx.x;
@@ -1693,7 +1693,6 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     const uint8_t *lb = fbytes + delta;
     const bool small = F.m <= (1ull << 30);
     const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
-    if (dbg & 1) return;  // diagnostics: the LDS fill only
     while (t < b1) {
         const uint32_t tn = t + kMcTestThreads;
         uint32_t in = 0;
@@ -1721,7 +1720,7 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
                         const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
                         uint32_t byte;
                         if (q < in_lds) byte = lb[q];
-                        else byte = (dbg & 2) ? 0xFFu : src[q];  // the tail past the LDS copy, from L2
+                        else byte = src[q];  // the tail past the LDS copy, from L2
                         bits &= byte >> (p & 7);
                     }
                 }
@@ -2062,10 +2061,7 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
     const uint64_t grid = (nkeys + kMcThreads - 1) / kMcThreads;
     if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    static const uint32_t nobloom = getenv("LSM_MC_NOBLOOM") ? 1u : 0u;  // diagnostics only
-    static const bool linear = getenv("LSM_MC_LINEAR") != nullptr;       // A/B: per-probe path only
-    static const uint32_t mcdbg = getenv("LSM_MC_DBG") ? (uint32_t)atoi(getenv("LSM_MC_DBG")) : 0u;
-    if (linear || nkeys > 0xFFFFFFFFull) {  // list entries are 32-bit
+    if (nkeys > 0xFFFFFFFFull) {  // list entries are 32-bit: the per-probe path
         LSM_HIP_CHECK(hipMemsetAsync(w.flag, 0, 4, s));
     } else {
         hipLaunchKernelGGL(mc_prep_kernel, dim3(1), dim3(256), 0, s, d_img, d_file_off, d_meta, nfile, w);
@@ -2076,10 +2072,10 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
         hipLaunchKernelGGL(mc_scatter_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, nfile, nkeys, w,
                            d_hit);
         hipLaunchKernelGGL(mc_test_kernel, dim3(nfile), dim3(kMcTestThreads), kMcLdsBytes, s,
-                           d_img, nfile, w, d_hit, mcdbg);
+                           d_img, nfile, w, d_hit);
     }
     hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(kMcThreads), 0, s, d_img,
-                       d_file_off, d_meta, nfile, d_keys, d_koff, nkeys, d_hit, nobloom,
+                       d_file_off, d_meta, nfile, d_keys, d_koff, nkeys, d_hit,
                        (const uint32_t *)w.flag);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;

@@ -955,9 +955,6 @@ extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec
     LSM_HIP_CHECK(hipStreamSynchronize(s));
     h_counts[0] = c4[0];
     h_counts[1] = c4[1];
-    if (getenv("LSM_MERGE_DBG"))
-        fprintf(stderr, "lsm_merge_kvs: %llu files, walk fast %llu slow %llu\n",
-                (unsigned long long)c4[1], (unsigned long long)c4[2], (unsigned long long)c4[3]);
     return 0;
 }
 

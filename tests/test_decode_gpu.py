@@ -362,3 +362,28 @@ def test_decode64k_full_size(ctx):
     want = (np.arange(nblk)[:, None] * 65536 + np.arange(recs)[None, :] * 124).reshape(-1)
     assert np.array_equal(d["rec_off"], want.astype(np.uint64))
     assert (d["key_len"] == 16).all() and (d["val_len"] == 100).all()
+
+
+@pytest.mark.parametrize("grammar", [0, 1, 2])
+def test_arena_uniform_runs(ctx, grammar):
+    """ARENA through the speculative-run emitter: blocks of equal-shape records
+    (key / value lengths 0-17 and 100, so runs, the exact step's record merged
+    into the run, fields shorter than a dword, 16-byte chunks straddling
+    records) at odd alignments, in blocks that fit the 8 KiB ring and in
+    streamed ones, plus a shape change mid-block (kv.go:88-111 materialized)."""
+    rng = np.random.default_rng(31 + grammar)
+    blocks = []
+    for k, v in [(0, 0), (0, 1), (1, 0), (3, 5), (16, 100), (17, 3), (2, 17), (5, 1)]:
+        # a fixed shape: key length k, value length v
+        kb, vb = bytes(range(7, 7 + k)), bytes((i * 37) & 255 for i in range(v))
+        if grammar == 0:
+            rec = struct.pack("<I", v) + vb
+        elif grammar == 1:
+            rec = struct.pack("<I", k) + kb + struct.pack("<I", v) + vb
+        else:
+            rec = struct.pack("<I", k) + kb + struct.pack("<q", v * 1000 - 7)
+        for reps in (1, 2, 63, 64, 65, 130, 700):
+            blocks.append(rec * reps)
+        blocks.append(rec * 40 + rand_records(rng, grammar, 3, kmax=9, vmax=30) + rec * 90)
+    run(ctx, grammar, blocks, arena=True, align_pad=11, seed=5)
+    run(ctx, grammar, blocks, arena=True, align_pad=11, seed=6, placement="offset")

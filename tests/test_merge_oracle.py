@@ -168,3 +168,25 @@ def test_goheap_tie_order_differs():
         groups += len(a)
         differ += int(np.sum(a != b))
     assert 0.02 < differ / groups < 0.5
+
+
+def test_goheap_winner_depends_on_larger_keys_pushed_later():
+    """Evidence for DESIGN.md §3 (f2 tie rule): under the reference's heap
+    (merge.go:45-80, container/heap up/down) the pair kept for key k15 changes
+    when only pairs with LARGER keys are appended after the group.  The winner
+    is therefore not a function of the group's own members and input
+    positions: any exact method must replay the heap's whole push/pop history
+    (a sequential O(n log n) chain), which is why the GPU merge implements
+    the stated input-order contract (merge.go:41, merge_test.go:25,53)."""
+    pre = [(b"k24", b"x0"), (b"k14", b"x1"), (b"k30", b"x2")]
+    group = [(b"k15", b"A"), (b"k15", b"B")]
+    ext = [(b"k24", b"y"), (b"k19", b"y"), (b"k21", b"y"), (b"k19", b"y")]
+
+    def kept(pairs, tie):
+        out, _ = ora.merge_pairs(pairs, 1, 1 << 21, tie)
+        return [pairs[i][1] for i in out if pairs[i][0] == b"k15"]
+
+    assert kept(pre + group, T[1]) == [b"B"]
+    assert kept(pre + group + ext, T[1]) == [b"A"]
+    # the input-order contract keeps the first pair either way
+    assert kept(pre + group, T[0]) == kept(pre + group + ext, T[0]) == [b"A"]
