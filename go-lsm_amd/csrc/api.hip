@@ -4,11 +4,6 @@
 
 #include "common.h"
 
-struct lsm_ctx {
-    int device;
-    int num_cus;
-};
-
 extern "C" int lsm_abi_version(void) { return LSM_ABI_VERSION; }
 
 extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {

@@ -12,6 +12,12 @@
         if (_e != hipSuccess) return -(1000 + (int)_e);     \
     } while (0)
 
+// One context per device and caller thread (include/lsm_gpu.h).
+struct lsm_ctx {
+    int device;
+    int num_cus;  // the persistent launches take one workgroup per CU
+};
+
 namespace lsm {
 
 constexpr int kWave = 64;

@@ -244,6 +244,24 @@ struct RingBytes {
     __device__ __forceinline__ uint32_t u8(uint32_t sb) const {
         return (word(sb >> 2) >> (8 * (sb & 3))) & 0xFFu;
     }
+    // stream bytes [sb, sb + 16) from two aligned 16-byte LDS lines: two
+    // ds_read_b128 (conflict-free when lanes take consecutive chunks; five
+    // ds_read_b32 at a 16-byte lane stride are 4-way bank conflicts)
+    __device__ __forceinline__ u32x4 u128(uint32_t sb) const {
+        constexpr uint32_t kB = NCH * kChunk;
+        const uint32_t a = sb & ~15u;
+        const uint32_t i0 = (LIN ? a : a % kB) >> 2, i1 = (LIN ? a + 16 : (a + 16) % kB) >> 2;
+        const u32x4 x = *reinterpret_cast<const u32x4 *>(&ring[i0]);
+        const u32x4 y = *reinterpret_cast<const u32x4 *>(&ring[i1]);
+        const uint32_t d = (sb >> 2) & 3;
+        const uint32_t d0 = d == 0 ? x.x : d == 1 ? x.y : d == 2 ? x.z : x.w;
+        const uint32_t d1 = d == 0 ? x.y : d == 1 ? x.z : d == 2 ? x.w : y.x;
+        const uint32_t d2 = d == 0 ? x.z : d == 1 ? x.w : d == 2 ? y.x : y.y;
+        const uint32_t d3 = d == 0 ? x.w : d == 1 ? y.x : d == 2 ? y.y : y.z;
+        const uint32_t d4 = d == 0 ? y.x : d == 1 ? y.y : d == 2 ? y.z : y.w;
+        return u32x4{funnel(d0, d1, sb), funnel(d1, d2, sb), funnel(d2, d3, sb),
+                     funnel(d3, d4, sb)};
+    }
     // a field not (wholly) in the ring: read through the caches
     __device__ __forceinline__ uint32_t g32(uint32_t sb) const {
         const uint32_t a = sb & ~3u;
@@ -275,70 +293,90 @@ __device__ __forceinline__ void set_dword(u32x4 &v, uint32_t j, uint32_t w) {
     v.w = j == 3 ? w : v.w;
 }
 
-// 16 bytes from stream byte sb: five consecutive source dwords, four funnels
-template <class F>
-__device__ __forceinline__ u32x4 load16(F word, uint32_t sb) {
-    const uint32_t w = sb >> 2;
-    const uint32_t d0 = word(w), d1 = word(w + 1), d2 = word(w + 2), d3 = word(w + 3),
-                   d4 = word(w + 4);
-    return u32x4{funnel(d0, d1, sb), funnel(d1, d2, sb), funnel(d2, d3, sb), funnel(d3, d4, sb)};
-}
-
 // A verified run: cnt records of stride S whose field of L bytes starts at
-// ring stream byte src0 + i*S (all landed), packed to out[0, cnt*L).
+// ring stream byte src0 + i*S (all landed), packed to out[0, cnt*L).  One
+// output dword per lane (consecutive lanes read consecutive ring dwords: no
+// bank conflicts, 256-byte coalesced stores), branch-free for L >= 4: the
+// dword's first byte lies in field r at offset o; if fewer than 4 of the
+// field's bytes remain (k < 4) the rest are the next field's first bytes.
 template <uint32_t NCH, bool LIN>
 __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, uint8_t *out,
                                                uint32_t src0, uint32_t S, uint32_t L,
                                                uint32_t cnt) {
     const uint32_t T = cnt * L;  // <= the ring: a run lies inside the landed bytes
     if (T == 0) return;
-    const uint32_t lead = (uint32_t)((uintptr_t)out & 15);
-    uint8_t *a0 = out - lead;
-    const uint32_t nch = (lead + T + 15) >> 4;
-    const float inv = 1.0f / (float)L;
-    auto rec = [&](uint32_t q) -> uint32_t {  // q / L, exact for q < 2^22
+    const uint32_t lead = (uint32_t)((uintptr_t)out & 3);
+    uint32_t *a0 = reinterpret_cast<uint32_t *>(out - lead);
+    const uint32_t nd = (lead + T + 3) >> 2;
+    // full-rate 24-bit products (v_mul_u32_u24): every operand here is < 2^24
+    auto mul24 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFFFu) * (y & 0xFFFFFFu); };
+    const float inv = __builtin_amdgcn_rcpf((float)L);
+    auto rec = [&](uint32_t q) -> uint32_t {  // q / L: q < 2^16, L < 2^14, r <= 65
         uint32_t r = (uint32_t)((float)q * inv);
-        r = r * L > q ? r - 1 : r;
-        return (r + 1) * L <= q ? r + 1 : r;
+        r = mul24(r, L) > q ? r - 1 : r;
+        return mul24(r + 1, L) <= q ? r + 1 : r;
     };
-    auto src = [&](uint32_t q) -> uint32_t {  // stream byte of output byte q
-        const uint32_t r = rec(q);
-        return src0 + r * S + (q - r * L);
-    };
-    auto word = [&](uint32_t w) -> uint32_t { return rb.word(w); };
+    // four dwords per lane per pass, all their LDS reads in flight together
+    // (ring reads are indexed modulo the ring, so lanes past the end read
+    // harmless bytes)
+    constexpr uint32_t U = 4;
 #pragma unroll 1
-    for (uint32_t c = lane_id(); c < nch; c += kWave) {
-        const int q0 = (int)(16 * c) - (int)lead;
-        u32x4 v{0, 0, 0, 0};
-        if (q0 >= 0 && q0 + 16 <= (int)T) {
-            const uint32_t r = rec((uint32_t)q0), o = (uint32_t)q0 - r * L;
-            if (o + 16 <= L) {  // the chunk lies in one field
-                v = load16(word, src0 + r * S + o);
-            } else {
-#pragma unroll 1
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t q = (uint32_t)q0 + 4 * j, rj = rec(q), oj = q - rj * L;
-                    uint32_t w = 0;
-                    if (oj + 4 <= L) {
-                        w = rb.u32(src0 + rj * S + oj);
-                    } else {
-#pragma unroll 1
-                        for (uint32_t t = 0; t < 4; t++) w |= rb.u8(src(q + t)) << (8 * t);
-                    }
-                    set_dword(v, j, w);
+    for (uint32_t w0 = 0; w0 < nd; w0 += U * kWave) {
+        uint32_t W[U], qv[U];
+        if (L >= 4) {
+            uint32_t kk[U], rr[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const int q = (int)(4 * (w0 + u * kWave + lane_id())) - (int)lead;
+                const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
+                const uint32_t r = rec(qc), o = qc - mul24(r, L);
+                qv[u] = (uint32_t)q;
+                kk[u] = L - o;
+                rr[u] = r;
+                W[u] = rb.u32(src0 + mul24(r, S) + o);
+            }
+            bool any = false;
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) any |= kk[u] < 4;
+            if (__ballot(any)) {  // a field boundary inside some lane's dword
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    const uint32_t B = rb.u32(src0 + mul24(rr[u] + 1, S)), k = kk[u];
+                    W[u] = k < 4 ? (W[u] & ((1u << (8 * k)) - 1)) | (B << (8 * k)) : W[u];
                 }
             }
-        } else {  // the first or last chunk: only the batch's bytes
-#pragma unroll 1
-            for (int t = 0; t < 16; t++) {
-                const int q = q0 + t;
-                if (q >= 0 && q < (int)T) {
-                    const uint32_t b = rb.u8(src((uint32_t)q)) << (8 * (t & 3));
-                    set_dword(v, (uint32_t)t >> 2, (t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w) | b);
+        } else {  // fields of 0-3 bytes: byte by byte
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const int q = (int)(4 * (w0 + u * kWave + lane_id())) - (int)lead;
+                const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
+                qv[u] = (uint32_t)q;
+                uint32_t x = 0;
+                for (uint32_t t = 0; t < 4; t++) {
+                    const uint32_t qq = qc + t;
+                    if (qq < T) {
+                        const uint32_t r = rec(qq);
+                        x |= rb.u8(src0 + mul24(r, S) + (qq - mul24(r, L))) << (8 * t);
+                    }
                 }
+                W[u] = x;
             }
         }
-        store_chunk(a0 + 16 * c, v, -q0, (int)T - q0);
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t w = w0 + u * kWave + lane_id();
+            if (w >= nd) continue;
+            const int q = (int)qv[u];
+            const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
+            const uint32_t sh = qc - (uint32_t)q;  // leading bytes before the run (first dword)
+            if (sh == 0 && qc + 4 <= T) {
+                a0[w] = W[u];
+            } else {  // the run's first or last dword, shared with its neighbours
+                uint8_t *b = reinterpret_cast<uint8_t *>(a0 + w);
+                for (uint32_t t = sh; t < 4 && (uint32_t)q + t < T; t++)
+                    b[t] = (uint8_t)(W[u] >> (8 * (t - sh)));
+            }
+        }
     }
 }
 
@@ -400,7 +438,7 @@ __device__ __forceinline__ uint32_t arena_emit_batch(const RingBytes<NCH, LIN> &
             // the chunk lies in one field
             const uint32_t sb = rsrc + ((uint32_t)q0 - rs0);
             if (in_ring())
-                v = load16([&](uint32_t w) { return rb.word(w); }, sb);
+                v = rb.u128(sb);
             else
                 v = u32x4{rb.g32(sb), rb.g32(sb + 4), rb.g32(sb + 8), rb.g32(sb + 12)};
         } else {
@@ -453,7 +491,11 @@ template <int G, uint32_t NCH, bool LIN, bool ARENA = false>
 __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
                                 uint64_t base, uint32_t ncap, uint32_t &nr_out, int32_t &st_out,
                                 uint32_t stop, uint32_t &pos_out, ArenaCur ac = {},
-                                uint32_t *tab = nullptr) {
+                                uint32_t *tab = nullptr, bool lin_rt = LIN) {
+    // the block fits the ring (read linearly, landed whole at the first
+    // step): a template constant, or for ARENA a runtime flag (the ring is
+    // then always indexed modulo its size, which is the same for such blocks)
+    const bool lin = ARENA ? lin_rt : LIN;
     const uint32_t lane = lane_id();
     BlockReaderT<NCH> rd;
     rd.init(ring, a.in, off, n);
@@ -474,19 +516,21 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     uint32_t pend = 0, pend_pos = 0, pend_k = 0, pend_v = 0;
     auto emit_run_arena = [&](uint32_t p0, uint32_t K, uint32_t V, uint32_t S, uint32_t cnt,
                               uint64_t slot0) {
-        if (G != LSM_GRAMMAR_V && a.key_arena) {
-            arena_emit_run(rb, a.key_arena + ac.k, rd.h + p0 + 4, S, K, cnt);
-            if (a.key_arena_off)  // cnt <= 65: the pending record + a full run
-                for (uint32_t i = lane; i < cnt; i += kWave) a.key_arena_off[slot0 + i] = ac.k + i * K;
-            ac.k += (uint64_t)cnt * K;
-        }
-        if (G != LSM_GRAMMAR_IDX && a.val_arena) {
-            arena_emit_run(rb, a.val_arena + ac.v, rd.h + p0 + (G == LSM_GRAMMAR_KV ? 8 + K : 4u),
-                           S, V, cnt);
-            if (a.val_arena_off)
-                for (uint32_t i = lane; i < cnt; i += kWave)
-                    a.val_arena_off[slot0 + i] = ac.v + (uint64_t)i * V;
-            ac.v += (uint64_t)cnt * V;
+        // keys, then values: one emitter body serves both arenas
+#pragma unroll 1
+        for (uint32_t f = G == LSM_GRAMMAR_V ? 1u : 0u; f < (G == LSM_GRAMMAR_IDX ? 1u : 2u);
+             f++) {
+            uint8_t *ar = f ? a.val_arena : a.key_arena;
+            if (!ar) continue;
+            uint64_t *ao = f ? a.val_arena_off : a.key_arena_off;
+            const uint64_t cur = f ? ac.v : ac.k;
+            const uint32_t L = f ? V : K;
+            arena_emit_run(rb, ar + cur, rd.h + p0 + (f == 0 ? 4u : G == LSM_GRAMMAR_KV ? 8 + K : 4u),
+                           S, L, cnt);
+            if (ao)  // cnt <= 65: the pending record + a full run
+                for (uint32_t i = lane; i < cnt; i += kWave) ao[slot0 + i] = cur + (uint64_t)i * L;
+            if (f) ac.v += (uint64_t)cnt * L;
+            else ac.k += (uint64_t)cnt * L;
         }
     };
     auto flush = [&]() {
@@ -530,14 +574,14 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
         if ((uint64_t)p + len <= lim) return;
         // a streamed block recycles ring chunks: the staged records' arena
         // bytes leave first
-        if (ARENA && !LIN) {
+        if (ARENA && !lin) {
             flush();
             if (pend) {
                 emit_run_arena(pend_pos, pend_k, pend_v, 0, 1, base + nr - 1);
                 pend = 0;
             }
         }
-        rd.ensure(rd.h + p, LIN ? rd.total : len);
+        rd.ensure(rd.h + p, lin ? rd.total : len);
         lim = rd.landed >= rd.nchunks ? n : rd.landed * kChunk - rd.h;
         if (ARENA) {
             rb.res_lo = (rd.hi_c > NCH ? rd.hi_c - NCH : 0u) * kChunk;
@@ -683,7 +727,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
             // wait for the span the run can verify (64 records): all of a
             // block that fits the ring, half the ring otherwise (the other
             // half stays in flight while the run is checked)
-            const uint32_t span_max = (LIN ? NCH : NCH / 2) * kChunk;
+            const uint32_t span_max = (lin ? NCH : NCH / 2) * kChunk;
             const uint64_t span = (uint64_t)S * kWave + 8;
             const uint32_t want = span < span_max ? (uint32_t)span : span_max;
             need(pos, n - pos < want ? n - pos : want);
@@ -748,7 +792,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
 
 template <int G, uint32_t NCH, bool LIN, bool ARENA>
 __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint32_t *tab,
-                                uint64_t off, uint32_t n) {
+                                uint64_t off, uint32_t n, bool lin_rt = LIN) {
     uint64_t base, cap;
     record_slots<G>(a, b, off, n, base, cap);
     uint32_t nr, end;
@@ -760,7 +804,7 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
     }
     decode_range_v2<G, NCH, LIN, ARENA>(a, ring, off, n, uni64(base),
                                         uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr,
-                                        st, n, end, ac, tab);
+                                        st, n, end, ac, tab, lin_rt);
     if (lane_id() == 0) {
         a.nrec[b] = nr;
         a.status[b] = st;
@@ -790,10 +834,17 @@ __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     stamp(0);
     const uint64_t off = uni64(a.blk_off[b]);
     const uint32_t n = uni(a.blk_len[b]);
-    if (((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk)
-        decode_block_v2<G, NCH, true, ARENA>(a, b, ring, tab, off, n);
-    else
-        decode_block_v2<G, NCH, false, ARENA>(a, b, ring, tab, off, n);
+    const bool lin = ((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk;
+    if (ARENA) {
+        // one instantiation, the ring form a runtime flag: with both forms
+        // inlined the register allocator needs 248 VGPRs (and spills) for
+        // what each alone does in 96
+        decode_block_v2<G, NCH, false, true>(a, b, ring, tab, off, n, lin);
+    } else if (lin) {
+        decode_block_v2<G, NCH, true, false>(a, b, ring, tab, off, n);
+    } else {
+        decode_block_v2<G, NCH, false, false>(a, b, ring, tab, off, n);
+    }
     stamp(3);
 }
 

@@ -576,12 +576,38 @@ __device__ __forceinline__ uint32_t be_dword(const uint32_t *bits, uint64_t q) {
 // inside the .sst): big-endian bytes, whole dwords inside the slice's byte
 // range and single bytes at its edges (the neighbouring bytes belong to the
 // other slice or to the filter prefix).  Native mode: u64 words to native.
-__device__ void store_filter_slice(const uint32_t *bits, uint64_t wlo, uint64_t whi,
+// Thread groups a body runs on: the whole workgroup, or the first waves of
+// one (sst_build_kernel's filter waves) with an LDS-counter barrier, so the
+// other waves keep streaming without joining the filter's barriers.
+struct WgGroup {
+    __device__ uint32_t tid() const { return threadIdx.x; }
+    __device__ uint32_t size() const { return blockDim.x; }
+    __device__ void sync() { __syncthreads(); }
+};
+
+struct WaveGroup {
+    uint32_t nw;    // waves 0 .. nw-1 of the workgroup
+    uint32_t *ctr;  // LDS arrival counter (zeroed before the group starts)
+    uint32_t gen;   // arrivals this wave has waited for
+    __device__ uint32_t tid() const { return threadIdx.x; }
+    __device__ uint32_t size() const { return nw * kWave; }
+    __device__ void sync() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        gen += nw;
+        if (lane_id() == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+};
+
+template <class Grp>
+__device__ void store_filter_slice(const Grp &g, const uint32_t *bits, uint64_t wlo, uint64_t whi,
                                    uint8_t *img_words, uint64_t *native) {
-    const uint32_t nthr = blockDim.x;
+    const uint32_t nthr = g.size();
     if (!img_words) {
         uint32_t *dst = reinterpret_cast<uint32_t *>(native + wlo);
-        for (uint64_t i = threadIdx.x; i < 2 * (whi - wlo); i += nthr) dst[i] = bits[i];
+        for (uint64_t i = g.tid(); i < 2 * (whi - wlo); i += nthr) dst[i] = bits[i];
         return;
     }
     const uint64_t len = 8 * (whi - wlo);
@@ -589,7 +615,7 @@ __device__ void store_filter_slice(const uint32_t *bits, uint64_t wlo, uint64_t 
     const uint32_t head = (uint32_t)(p0 & 3);
     uint32_t *dA = reinterpret_cast<uint32_t *>(p0 - head);
     const uint64_t ndw = (head + len + 3) / 4;
-    for (uint64_t d = threadIdx.x; d < ndw; d += nthr) {
+    for (uint64_t d = g.tid(); d < ndw; d += nthr) {
         const int64_t u0 = (int64_t)(4 * d) - head;
         if (u0 >= 0 && (uint64_t)u0 + 4 <= len) {
             const uint64_t q = (uint64_t)u0 >> 2;
@@ -652,129 +678,15 @@ __global__ __launch_bounds__(1024) void bloom_slices_kernel(BloomArgs a) {
     __syncthreads();
     const uint64_t wlo = lo / 64, whi = (hi + 63) / 64;
     if (a.bitmap) {
-        store_filter_slice(lds_bits, wlo, whi, nullptr, a.bitmap + (uint64_t)f * a.nwords);
+        store_filter_slice(WgGroup{}, lds_bits, wlo, whi, nullptr, a.bitmap + (uint64_t)f * a.nwords);
     } else {
         const uint64_t hdr = sst_header_bytes(a.koff, s, e);
-        store_filter_slice(lds_bits, wlo, whi, a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+        store_filter_slice(WgGroup{}, lds_bits, wlo, whi, a.out + uni64(a.file_off[f]) + hdr + 32,
+                           nullptr);
     }
 }
 
-// ---- binned bloom build (two slices, m < 2^32) ------------------------------
-//
-// go-lsm's 1.6 Mbit filter needs two 100 KiB LDS slices.  Instead of hashing
-// every key once per slice, bloom_bin_kernel hashes each key once (a grid
-// over all keys: full occupancy for the compute-bound sum256 + 16 Barrett
-// moduli) and writes its bit positions binned by slice: slice 0 fills the
-// file's k*n position area from the front, slice 1 from the back, so the two
-// bins never collide and need no capacity planning.  Each wave compacts its
-// positions in LDS (ballot + mbcnt) and reserves room with one atomicAdd per
-// bin.  bloom_apply_kernel then ORs each bin into its LDS slice and stores the
-// slice straight into the image as big-endian words.
-struct BloomBinArgs {
-    const uint8_t *keys;
-    const uint64_t *koff;
-    const uint64_t *file_start;
-    uint64_t m, mrecip;
-    uint32_t k;
-    uint32_t split;  // bit positions < split -> slice 0
-    uint32_t *pos;   // file f's k * (records of f) positions at f * k * maxr
-    uint32_t maxr;   // max_file_records
-    uint32_t *cnt;   // per file: {front count, back count}
-    uint8_t *out;
-    const uint64_t *file_off;
-    uint64_t nwords;
-};
-
-constexpr uint32_t kBinWaves = 4;
-constexpr uint32_t kBinBatch = 16;  // locations per staging round
-
-struct BinLds {
-    uint32_t s0[kBinBatch * kWave], s1[kBinBatch * kWave];
-};
-
-
-__global__ __launch_bounds__(64 * kBinWaves) void bloom_bin_kernel(BloomBinArgs a) {
-    __shared__ BinLds lds[kBinWaves];
-    const uint32_t f = blockIdx.x;
-    const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
-    const uint64_t c0 = s + (uint64_t)blockIdx.y * (kBinWaves * kWave) + (uint64_t)wave * kWave;
-    if (c0 >= e) return;
-    const uint32_t lane = lane_id();
-    const uint64_t i = c0 + lane;
-    const bool act = i < e;
-    uint64_t h[4];
-    {
-        const uint64_t ii = act ? i : e - 1;  // unconditional loads (no per-load drain)
-        const uint64_t k0 = a.koff[ii];
-        sum256(a.keys + k0, a.koff[ii + 1] - k0, h);
-    }
-    const uint64_t base = (uint64_t)f * a.k * a.maxr;
-    const uint64_t cap = (uint64_t)a.k * (e - s);
-    BinLds &L = lds[wave];
-    for (uint32_t j0 = 0; j0 < a.k; j0 += kBinBatch) {
-        const uint32_t jn = a.k - j0 < kBinBatch ? a.k - j0 : kBinBatch;
-        uint32_t n0 = 0, n1 = 0;
-        for (uint32_t j = 0; j < jn; j++) {
-            const uint32_t p =
-                act ? (uint32_t)mod_barrett(location(h[0], h[1], h[2], h[3], j0 + j), a.m, a.mrecip) : 0;
-            const bool in1 = p >= a.split;
-            const uint64_t b1 = __ballot(act && in1), b0 = __ballot(act && !in1);
-            if (act) {
-                if (in1) L.s1[n1 + mbcnt(b1)] = p;
-                else L.s0[n0 + mbcnt(b0)] = p;
-            }
-            n0 += (uint32_t)__builtin_popcountll(b0);
-            n1 += (uint32_t)__builtin_popcountll(b1);
-        }
-        uint32_t o0 = 0, o1 = 0;
-        if (lane == 0) {
-            if (n0) o0 = atomicAdd(&a.cnt[2 * f], n0);
-            if (n1) o1 = atomicAdd(&a.cnt[2 * f + 1], n1);
-        }
-        o0 = uni(o0);
-        o1 = uni(o1);
-        __builtin_amdgcn_wave_barrier();
-        __asm__ __volatile__("" ::: "memory");
-        for (uint32_t t = lane; t < n0; t += kWave) a.pos[base + o0 + t] = L.s0[t];
-        for (uint32_t t = lane; t < n1; t += kWave) a.pos[base + cap - o1 - n1 + t] = L.s1[t];
-        __builtin_amdgcn_wave_barrier();
-        __asm__ __volatile__("" ::: "memory");
-    }
-}
-
-__global__ __launch_bounds__(1024) void bloom_apply_kernel(BloomBinArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
-    const uint32_t f = blockIdx.x, sl = blockIdx.y;
-    const uint64_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
-    const uint32_t nw32 = (uint32_t)((hi - lo + 63) / 64) * 2;
-    for (uint32_t i = threadIdx.x; i < nw32; i += blockDim.x) lds_bits[i] = 0;
-    __syncthreads();
-    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
-    const uint64_t base = (uint64_t)f * a.k * a.maxr;
-    const uint64_t cap = (uint64_t)a.k * (e - s);
-    const uint32_t n = a.cnt[2 * f + sl];
-    const uint32_t *src = a.pos + (sl ? base + cap - n : base);
-    // 16 independent loads per thread in flight per round.  Loads past the
-    // bin are clamped to its last position (OR-ing a bit twice is harmless):
-    // an unconditional load needs no per-load wait, a guarded one would make
-    // the compiler drain vmcnt after each.
-    constexpr uint32_t kU = 16;
-    for (uint32_t t0 = threadIdx.x; t0 < n; t0 += kU * blockDim.x) {
-        uint32_t q[kU];
-#pragma unroll
-        for (uint32_t j = 0; j < kU; j++) {
-            const uint32_t t = t0 + j * blockDim.x;
-            q[j] = __builtin_nontemporal_load(&src[t < n ? t : n - 1]) - (uint32_t)lo;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kU; j++) atomicOr(&lds_bits[q[j] >> 5], 1u << (q[j] & 31));
-    }
-    __syncthreads();
-    const uint64_t hdr = sst_header_bytes(a.koff, s, e);
-    store_filter_slice(lds_bits, lo / 64, (hi + 63) / 64, a.out + uni64(a.file_off[f]) + hdr + 32,
-                       nullptr);
-}
+constexpr uint32_t kBinBatch = 8;  // locations per staging round
 
 // ---- per-file bloom build, hash once (one or two slices, m < 2^32) -----------
 //
@@ -800,30 +712,31 @@ struct BloomFileArgs {
     uint8_t *out;     // image mode
     const uint64_t *file_off;
     uint64_t *bitmap; // native mode (out == null)
-    uint32_t dbg;     // diagnostics only: bit 2 skips slice 1, bit 3 the slice-0 ORs
 };
 
-__global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
-    __shared__ uint32_t n1;
-    const uint32_t f = blockIdx.x;
+// The filter of file f by thread group g (lds_bits: the slice-0 LDS, n1: a
+// shared counter): the whole workgroup in bloom_file_kernel, the filter waves
+// in sst_build_kernel.
+template <class Grp>
+__device__ void bloom_file_body(Grp &g, const BloomFileArgs &a, uint32_t f, uint32_t *lds_bits,
+                                uint32_t &n1) {
     const uint32_t lane = lane_id();
     const uint64_t s = a.file_start ? uni64(a.file_start[f]) : 0;
     const uint64_t e = a.file_start ? uni64(a.file_start[f + 1]) : a.nkeys;
     const bool two = a.split < a.m;
     const uint64_t lo1 = two ? a.split : a.m;  // end of slice 0
     const uint32_t nw0 = (uint32_t)((lo1 + 63) / 64) * 2;
-    for (uint32_t i = threadIdx.x; i < nw0; i += blockDim.x) lds_bits[i] = 0;
-    if (threadIdx.x == 0) n1 = 0;
-    __syncthreads();
+    for (uint32_t i = g.tid(); i < nw0; i += g.size()) lds_bits[i] = 0;
+    if (g.tid() == 0) n1 = 0;
+    g.sync();
     uint32_t *list = two ? a.pos + (uint64_t)f * a.k * a.maxr : nullptr;
     // Two-stage load pipeline across rounds (a wave takes 64 keys per round,
     // rounds 1024 keys apart): while round r hashes, the first 16 key bytes
     // of round r+1 and the offsets of round r+2 are in flight.  Indices past
     // the filter are clamped to its last key (unconditional loads).
-    const uint32_t stride = blockDim.x;
+    const uint32_t stride = g.size();
     auto clampi = [&](uint64_t i) { return i < e ? i : e - 1; };
-    uint64_t i0 = s + (threadIdx.x & ~63u);
+    uint64_t i0 = s + (g.tid() & ~63u);
     uint64_t ka = 0, la = 0, fa0 = 0, fa1 = 0, kb = 0, lb = 0;
     if (i0 < e) {
         const uint64_t ii = clampi(i0 + lane);
@@ -868,7 +781,7 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
                                              (uint32_t)(a.mrecip >> 32));
                 loc[c] += (c == 0 || c == 3) ? st2 : st3;
                 const bool in1 = p >= (uint32_t)lo1;  // lo1 <= m <= 2^30
-                if (valid && !in1 && !(a.dbg & 8)) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
+                if (valid && !in1) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
                 pp[jj] = valid && in1 ? p : 0xFFFFFFFFu;
                 c1 += (uint32_t)(valid && in1);
             }
@@ -887,39 +800,52 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
             }
         }
     }
-    __syncthreads();
+    g.sync();
     if (a.out) {
         const uint64_t hdr = sst_header_bytes(a.koff, s, e);
-        store_filter_slice(lds_bits, 0, (lo1 + 63) / 64, a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+        store_filter_slice(g, lds_bits, 0, (lo1 + 63) / 64, a.out + uni64(a.file_off[f]) + hdr + 32,
+                           nullptr);
     } else {
-        store_filter_slice(lds_bits, 0, (lo1 + 63) / 64, nullptr, a.bitmap + (uint64_t)f * a.nwords);
+        store_filter_slice(g, lds_bits, 0, (lo1 + 63) / 64, nullptr, a.bitmap + (uint64_t)f * a.nwords);
     }
-    if (!two || (a.dbg & 4)) return;
-    // slice 1 from this workgroup's own list
+    if (!two) {
+        g.sync();  // the LDS slice is reused by the caller
+        return;
+    }
+    // slice 1 from this group's own list
     __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    g.sync();
     const uint32_t nw1 = (uint32_t)((a.m - lo1 + 63) / 64) * 2;
-    for (uint32_t i = threadIdx.x; i < nw1; i += blockDim.x) lds_bits[i] = 0;
-    __syncthreads();
+    for (uint32_t i = g.tid(); i < nw1; i += g.size()) lds_bits[i] = 0;
+    g.sync();
     const uint32_t n = n1;
     constexpr uint32_t kU = 16;
-    for (uint32_t t0 = threadIdx.x; t0 < n; t0 += kU * blockDim.x) {
+    for (uint32_t t0 = g.tid(); t0 < n; t0 += kU * g.size()) {
         uint32_t q[kU];
 #pragma unroll
         for (uint32_t j = 0; j < kU; j++) {
-            const uint32_t t = t0 + j * blockDim.x;
+            const uint32_t t = t0 + j * g.size();
             q[j] = __builtin_nontemporal_load(&list[t < n ? t : n - 1]) - (uint32_t)lo1;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kU; j++) atomicOr(&lds_bits[q[j] >> 5], 1u << (q[j] & 31));
     }
-    __syncthreads();
+    g.sync();
     if (a.out) {
         const uint64_t hdr = sst_header_bytes(a.koff, s, e);
-        store_filter_slice(lds_bits, lo1 / 64, a.nwords, a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+        store_filter_slice(g, lds_bits, lo1 / 64, a.nwords, a.out + uni64(a.file_off[f]) + hdr + 32,
+                           nullptr);
     } else {
-        store_filter_slice(lds_bits, lo1 / 64, a.nwords, nullptr, a.bitmap + (uint64_t)f * a.nwords);
+        store_filter_slice(g, lds_bits, lo1 / 64, a.nwords, nullptr, a.bitmap + (uint64_t)f * a.nwords);
     }
+    g.sync();  // the LDS slice is reused by the caller
+}
+
+__global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    __shared__ uint32_t n1;
+    WgGroup g;
+    bloom_file_body(g, a, blockIdx.x, lds_bits, n1);
 }
 
 // ---- .sst image writer ------------------------------------------------------
@@ -935,7 +861,6 @@ struct SstArgs {
     int64_t *footer;
     uint64_t m, nwords;
     uint32_t k;
-    uint32_t dbg;     // diagnostics only: bit 0 skips the V region, bit 1 the IDX region
     uint32_t skip_v;  // the V region is written from value views (lsm_build_sst_views)
 };
 
@@ -987,12 +912,31 @@ __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
     S.idx_base = (int64_t)L.data_off;
     S.rs = L.s;
     S.vrs = Vs;
-    if (!(a.dbg & 1) && !a.skip_v)
+    if (!a.skip_v)
         encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
                                         lds[wave].gather, nullptr, &lds[wave].ct);
-    if (!(a.dbg & 2))
-        encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
-                                          lds[wave].gather, nullptr, &lds[wave].ct);
+    encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
+                                      lds[wave].gather, nullptr, &lds[wave].ct);
+}
+
+// The V and IDX regions of records [c0, c0 + cnt) of file f by one wave
+// (lds: its gather buffer).
+__device__ void sst_region_chunk(const SstArgs &a, uint32_t f, uint64_t c0, uint32_t cnt,
+                                 RegionLds *lds) {
+    const SstLayout L = sst_layout(a, f);
+    uint8_t *img = a.out + uni64(a.file_off[f]);
+    const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
+    const uint64_t Kc = uni64(a.koff[c0]), Vc = uni64(a.voff[c0]);
+    RegionSrc S;
+    S.keys = a.keys; S.koff = a.koff; S.vals = a.vals; S.voff = a.voff;
+    S.idx_off = nullptr;
+    S.idx_base = (int64_t)L.data_off;
+    S.rs = L.s;
+    S.vrs = Vs;
+    encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
+                                    lds->gather, nullptr, &lds->ct);
+    encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
+                                      lds->gather, nullptr, &lds->ct);
 }
 
 // Data region (V grammar, sstable.go:159-175) of file blockIdx.x straight
@@ -1134,8 +1078,8 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
 // Header, filter-block prefix and footer of file blockIdx.x (one wave; byte
 // stores, since the neighbouring bytes belong to other kernels).  The filter
 // words themselves are stored by the bloom kernels.
-__global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) {
-    const uint32_t f = blockIdx.x;
+// Header, filter prefix and footer of file f by one wave.
+__device__ void sst_meta_body(const SstArgs &a, uint32_t f) {
     const SstLayout L = sst_layout(a, f);
     uint8_t *img = a.out + uni64(a.file_off[f]);
     const uint32_t lane = lane_id();
@@ -1164,6 +1108,112 @@ __global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) {
         const uint64_t vals[4] = {L.data_off, L.data_size, L.idx_off, L.idx_size};
         img[L.img - 32 + lane] = (uint8_t)(vals[lane / 8] >> (8 * (lane % 8)));
         if (a.footer && lane < 4) a.footer[4 * (uint64_t)f + lane] = (int64_t)vals[lane];
+    }
+}
+
+__global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body(a, blockIdx.x); }
+
+// ---- the fused .sst build ------------------------------------------------------
+//
+// SSTable.Add feeds each pair to the data block, the index block and the
+// bloom filter in one pass (sstable.go:322-326).  Here one persistent launch
+// (one 1024-thread workgroup per CU) builds every image, with two roles
+// side by side on each CU:
+//   * filter waves 0-7 build the filters of files blockIdx.x, +grid, ...:
+//     hash each key once, set the bits of the LDS slice, list the few past
+//     it, then the rest from the list (bloom_file_body on the wave group,
+//     LDS-counter barriers), then the header, filter prefix and footer;
+//   * region waves 8-15 take 64-record chunks of the V and IDX regions from
+//     a global counter (any file), DMA-gathered through their LDS buffers.
+// The filter is VALU-bound and the regions HBM-bound, so each CU does both
+// at once; filter waves that run out of files join the region work (their
+// buffers in the slice's LDS).  No workgroup waits on another.
+constexpr uint32_t kBuildWaves = 16;
+constexpr uint32_t kBuildBloomWaves = 8;
+constexpr uint32_t kBuildLdsBytes = 160 * 1024 - 256;  // dynamic; + the static counters
+constexpr uint32_t kBuildRegionBytes = (kBuildWaves - kBuildBloomWaves) * sizeof(RegionLds);
+constexpr uint32_t kBuildSliceBytes = (kBuildLdsBytes - kBuildRegionBytes) / 8 * 8;
+static_assert(kBuildSliceBytes >= kBuildBloomWaves * sizeof(RegionLds), "filter waves' buffers");
+constexpr uint32_t kBuildChunk = kWave;  // records per region task
+
+struct BuildWork {
+    uint64_t *chunk_base;  // nfile + 1: exclusive scan of ceil(records / kBuildChunk)
+    uint32_t *next;        // region task counter
+    uint32_t nfile;
+};
+
+// chunk_base and the task counter, one workgroup.
+__global__ __launch_bounds__(1024) void sst_build_prep_kernel(const uint64_t *file_start, BuildWork w) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) {
+        carry = 0;
+        *w.next = 0;
+    }
+    __syncthreads();
+    for (uint32_t f0 = 0; f0 < w.nfile; f0 += 1024) {
+        const uint32_t f = f0 + threadIdx.x;
+        uint64_t c = 0;
+        if (f < w.nfile) c = (file_start[f + 1] - file_start[f] + kBuildChunk - 1) / kBuildChunk;
+        uint64_t tot;
+        const uint64_t ex = wave_excl_scan64(c, &tot);
+        const uint32_t wv = threadIdx.x / kWave;
+        if (lane_id() == 0) wsum[wv] = tot;
+        __syncthreads();
+        uint64_t pre = carry;
+        for (uint32_t v = 0; v < wv; v++) pre += wsum[v];
+        if (f < w.nfile) w.chunk_base[f] = pre + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t t = carry;
+            for (uint32_t v = 0; v < 16; v++) t += wsum[v];
+            carry = t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) w.chunk_base[w.nfile] = carry;
+}
+
+// Region tasks until the counter runs out (one wave; lds: its buffer).
+__device__ void build_region_tasks(const SstArgs &a, const BuildWork &w, RegionLds *lds) {
+    const uint64_t total = uni64(w.chunk_base[w.nfile]);
+    for (;;) {
+        uint32_t t = 0;
+        if (lane_id() == 0) t = atomicAdd(w.next, 1u);
+        t = uni(t);
+        if (t >= total) return;
+        // the file holding task t: the last f with chunk_base[f] <= t
+        uint32_t lo = 0, hi = w.nfile;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (uni64(w.chunk_base[mid]) <= t) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t s = uni64(a.file_start[lo]), e = uni64(a.file_start[lo + 1]);
+        const uint64_t c0 = s + (t - uni64(w.chunk_base[lo])) * kBuildChunk;
+        const uint32_t cnt = (uint32_t)(e - c0 < kBuildChunk ? e - c0 : kBuildChunk);
+        sst_region_chunk(a, lo, c0, cnt, lds);
+    }
+}
+
+__global__ __launch_bounds__(1024) void sst_build_kernel(SstArgs a, BloomFileArgs b, BuildWork w) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    __shared__ uint32_t n1, bar;
+    const uint32_t wave = uni(threadIdx.x / kWave);
+    if (threadIdx.x == 0) bar = 0;
+    __syncthreads();  // the only workgroup-wide barrier: the roles never meet again
+    if (wave < kBuildBloomWaves) {
+        WaveGroup g{kBuildBloomWaves, &bar, 0};
+        uint32_t *bits = reinterpret_cast<uint32_t *>(lds_raw);
+        for (uint32_t f = blockIdx.x; f < w.nfile; f += gridDim.x) {
+            bloom_file_body(g, b, f, bits, n1);
+            if (wave == 0) sst_meta_body(a, f);
+        }
+        // no filters left: region work, the buffers in the slice's LDS
+        build_region_tasks(a, w, reinterpret_cast<RegionLds *>(lds_raw) + wave);
+    } else {
+        build_region_tasks(a, w, reinterpret_cast<RegionLds *>(lds_raw + kBuildSliceBytes) +
+                                     (wave - kBuildBloomWaves));
     }
 }
 
@@ -1859,24 +1909,28 @@ static uint32_t bloom_slices(uint64_t m) {
 }
 static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slices(m) <= 2; }
 
+// Filter bits kept in LDS by the fused build; a filter up to twice this is
+// built by it (the bits past the LDS slice go through a per-file list).
+static constexpr uint64_t kFusedCapBits = (uint64_t)kBuildSliceBytes * 8;
+static bool fused_build(uint64_t m) { return m <= (1ull << 30) && m <= 2 * kFusedCapBits; }
+
+// Workspace: [slice-1 position lists][fused build: chunk_base (nfile+1) | task counter]
+static uint64_t build_list_bytes(uint32_t nfile, uint32_t max_file_records, uint64_t m, uint32_t k) {
+    // the position list past the LDS slice: the fused build (m past its
+    // slice) and the two-slice hash-once filter of lsm_build_sst_views
+    const bool fused_list = fused_build(m) && m > kFusedCapBits;
+    const bool views_list = hash_once_bloom(m) && bloom_slices(m) >= 2;
+    if (!fused_list && !views_list) return 0;
+    const uint64_t kk = k ? k : 1;
+    return (kk * nfile * (uint64_t)max_file_records * 4 + 255) & ~255ull;
+}
+
 extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
                                                 uint64_t m, uint32_t k) {
-    if (!hash_once_bloom(m) || bloom_slices(m) < 2) return 16;
-    const uint64_t kk = k ? k : 1;
-    const uint64_t cnt = ((uint64_t)(nfile ? nfile : 1) * 2 * 4 + 255) & ~255ull;
-    return (size_t)(cnt + kk * nfile * (uint64_t)max_file_records * 4 + 16);
+    return (size_t)(build_list_bytes(nfile, max_file_records, m, k) + 8ull * (nfile + 1) + 16);
 }
 
 static uint64_t barrett_recip(uint64_t m) { return ~0ull / m; }
-
-// Diagnostics only (LSM_SST_DBG): skip parts of lsm_build_sst to time the rest.
-static uint32_t sst_dbg() {
-    static const uint32_t v = [] {
-        const char *e = getenv("LSM_SST_DBG");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    return v;
-}
 
 static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
                           const uint8_t *d_vals, const uint64_t *d_voff,
@@ -1894,17 +1948,59 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     const uint32_t kk = k ? k : 1;  // NewBloomFilter max(1, k) bloom.go:95-101
     const uint32_t chunks = (max_file_records + kSstChunkRecs - 1) / kSstChunkRecs;
 
+    SstArgs a;
+    a.keys = d_keys;
+    a.koff = d_koff;
+    a.vals = d_vals;
+    a.voff = d_voff;
+    a.file_start = d_file_start;
+    a.out = d_out;
+    a.file_off = d_file_off;
+    a.footer = d_footer;
+    a.m = m;
+    a.nwords = nwords;
+    a.k = kk;
+    a.skip_v = views != nullptr;
+
+    // The fused build (lsm_build_sst): filters and regions in one launch.
+    if (!views && fused_build(m)) {
+        const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
+        if (!d_workspace || ws_bytes < need) return LSM_ESPACE;
+        const uint64_t list_bytes = build_list_bytes(nfile, max_file_records, m, kk);
+        uint8_t *ws = static_cast<uint8_t *>(d_workspace);
+        BloomFileArgs b;
+        b.keys = d_keys;
+        b.koff = d_koff;
+        b.file_start = d_file_start;
+        b.nkeys = 0;
+        b.m = m;
+        b.mrecip = barrett_recip(m);
+        b.k = kk;
+        b.split = (uint32_t)(m < kFusedCapBits ? m : kFusedCapBits);
+        b.pos = reinterpret_cast<uint32_t *>(ws);
+        b.maxr = max_file_records;
+        b.nwords = nwords;
+        b.out = d_out;
+        b.file_off = d_file_off;
+        b.bitmap = nullptr;
+        BuildWork w;
+        w.chunk_base = reinterpret_cast<uint64_t *>(ws + list_bytes);
+        w.next = reinterpret_cast<uint32_t *>(ws + list_bytes + 8ull * (nfile + 1));
+        w.nfile = nfile;
+        hipLaunchKernelGGL(sst_build_prep_kernel, dim3(1), dim3(1024), 0, s, d_file_start, w);
+        // one workgroup per CU (the LDS admits one): every CU hashes and streams
+        const uint32_t grid = (uint32_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
+        hipLaunchKernelGGL(sst_build_kernel, dim3(grid), dim3(1024), (size_t)kBuildLdsBytes, s, a, b, w);
+        LSM_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
+
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
     if (hash_once_bloom(m)) {
         const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
         if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
-        // LSM_BLOOM_PATH=1 selects the two-kernel binned variant (A/B only).
-        static const int path = [] {
-            const char *e = getenv("LSM_BLOOM_PATH");
-            return e ? atoi(e) : 0;
-        }();
-        if (path == 0 || bloom_slices(m) < 2) {
+        {
             BloomFileArgs b;
             b.keys = d_keys;
             b.koff = d_koff;
@@ -1920,32 +2016,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
             b.out = d_out;
             b.file_off = d_file_off;
             b.bitmap = nullptr;
-            b.dbg = sst_dbg();
             hipLaunchKernelGGL(bloom_file_kernel, dim3(nfile), dim3(1024), (size_t)(sb / 8), s, b);
-            LSM_HIP_CHECK(hipGetLastError());
-        } else {
-            BloomBinArgs b;
-            b.keys = d_keys;
-            b.koff = d_koff;
-            b.file_start = d_file_start;
-            b.m = m;
-            b.mrecip = barrett_recip(m);
-            b.k = kk;
-            b.split = (uint32_t)sb;
-            b.maxr = max_file_records;
-            const size_t cnt_bytes = ((size_t)nfile * 2 * 4 + 255) & ~(size_t)255;
-            b.cnt = static_cast<uint32_t *>(d_workspace);
-            b.pos = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) + cnt_bytes);
-            b.out = d_out;
-            b.file_off = d_file_off;
-            b.nwords = nwords;
-            LSM_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)nfile * 2 * 4, s));
-            const uint32_t bchunks = (max_file_records + kBinWaves * kWave - 1) / (kBinWaves * kWave);
-            if (bchunks) {
-                hipLaunchKernelGGL(bloom_bin_kernel, dim3(nfile, bchunks), dim3(kBinWaves * kWave), 0, s, b);
-                LSM_HIP_CHECK(hipGetLastError());
-            }
-            hipLaunchKernelGGL(bloom_apply_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, b);
             LSM_HIP_CHECK(hipGetLastError());
         }
     } else {
@@ -1968,20 +2039,6 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     }
 
 
-    SstArgs a;
-    a.keys = d_keys;
-    a.koff = d_koff;
-    a.vals = d_vals;
-    a.voff = d_voff;
-    a.file_start = d_file_start;
-    a.out = d_out;
-    a.file_off = d_file_off;
-    a.footer = d_footer;
-    a.m = m;
-    a.nwords = nwords;
-    a.k = kk;
-    a.dbg = sst_dbg();
-    a.skip_v = views != nullptr;
     if (chunks) {
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, chunks), dim3(256), 0, s, a);
         LSM_HIP_CHECK(hipGetLastError());

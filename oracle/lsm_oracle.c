@@ -617,3 +617,43 @@ uint64_t ora_merge_kvs(const uint8_t *bytes, const uint64_t *koff, const uint32_
     free(tmp);
     return cnt;
 }
+
+/* ---- batched SSTable.MayContain (CPU baseline) -------- */
+
+static int go_strcmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    uint64_t n = la < lb ? la : lb;
+    int c = n ? memcmp(a, b, n) : 0;
+    if (c) return c;
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
+
+void ora_may_contain_batch(const uint8_t *img, const uint64_t *file_off, const ora_sst_meta *meta,
+                           uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
+                           uint64_t k1, uint8_t *hit) {
+    for (uint64_t i = k0; i < k1; i++) {
+        const uint8_t *key = keys + koff[i];
+        const uint64_t kl = koff[i + 1] - koff[i];
+        for (uint32_t f = 0; f < nfile; f++) {
+            const ora_sst_meta *M = &meta[f];
+            const uint8_t *base = img + file_off[f];
+            uint8_t r = 0;
+            if (M->stage != 1 && M->stage != 2 &&
+                /* sstable.go:301: MinKey > key || MaxKey < key -> false */
+                go_strcmp(base + M->min_key_off, M->min_key_len, key, kl) <= 0 &&
+                go_strcmp(base + M->max_key_off, M->max_key_len, key, kl) >= 0) {
+                /* Filter.Test bloom.go:371-379, bits read from the stored words */
+                uint64_t h[4];
+                ora_sum256(key, kl, h);
+                r = 1;
+                for (uint64_t j = 0; j < M->filter_k && r; j++) {
+                    if (M->filter_m == 0) { r = 0; break; } /* Go panics; the ABI answers 0 */
+                    const uint64_t q = ora_location(h, j) % M->filter_m;
+                    if (q >= M->filter_nbits) { r = 0; break; }
+                    const uint8_t byte = base[M->filter_words_off + 8 * (q >> 6) + 7 - ((q & 63) >> 3)];
+                    r = (byte >> (q & 7)) & 1;
+                }
+            }
+            hit[(i - k0) * nfile + f] = r;
+        }
+    }
+}

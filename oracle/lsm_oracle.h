@@ -156,6 +156,13 @@ typedef struct {
 int ora_sst_decode(const uint8_t *file, uint64_t n, ora_sst_meta *meta, ora_desc *idx_desc,
                    int64_t *idx_val, uint64_t idx_cap, ora_desc *data_desc, uint64_t data_cap);
 
+/* Batched SSTable.MayContain (sstable.go:300-305) of keys [k0, k1) against
+ * nfile decoded images: hit[(i - k0) * nfile + f].  Each (key, file) test
+ * hashes the key again, as Filter.Test does per file. */
+void ora_may_contain_batch(const uint8_t *img, const uint64_t *file_off, const ora_sst_meta *meta,
+                           uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
+                           uint64_t k1, uint8_t *hit);
+
 /* ---- compaction merge ----------------------------- */
 
 enum { ORA_TIE_INPUT = 0, ORA_TIE_GOHEAP = 1 };

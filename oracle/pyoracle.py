@@ -52,6 +52,7 @@ def lib():
         "ora_bloom_add": (None, [vp, u64, u64, vp, u64]),
         "ora_bloom_test": (ctypes.c_int, [vp, u64, u64, vp, u64]),
         "ora_filter_test": (ctypes.c_int, [vp, u64, u64, u64, vp, u64]),
+        "ora_may_contain_batch": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp]),
         "ora_estimate_parameters": (None, [u64, ctypes.c_double, vp, vp]),
         "ora_filter_block_size": (u64, [u64]),
         "ora_filter_encode": (u64, [vp, u64, u64, vp]),
@@ -291,3 +292,18 @@ def bench_decode_golike(grammar, buf, blk_off, blk_len, threads=1):
     blk_len = np.ascontiguousarray(blk_len, dtype=np.uint32)
     return lib().ora_bench_decode_golike(grammar, _p(buf), _p(blk_off), _p(blk_len),
                                          blk_off.size, threads)
+
+
+def may_contain_batch(img, file_off, metas, keys, koff, k0, k1):
+    """Batched SSTable.MayContain of keys [k0, k1) -> uint8 (k1-k0, nfile).
+    metas: the files' SstMeta (a ctypes array or list)."""
+    img = _bytes(img)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
+    keys = _bytes(keys) if len(keys) else np.zeros(1, np.uint8)
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    nfile = len(metas)
+    arr = metas if isinstance(metas, ctypes.Array) else (SstMeta * nfile)(*metas)
+    hit = np.zeros((k1 - k0, max(nfile, 1)), np.uint8)
+    lib().ora_may_contain_batch(_p(img), _p(file_off), ctypes.cast(arr, vp), nfile, _p(keys),
+                                _p(koff), k0, k1, _p(hit))
+    return hit
