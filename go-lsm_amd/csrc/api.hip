@@ -20,11 +20,25 @@ extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
     if (!c) return LSM_ENOMEM;
     c->device = device;
     c->num_cus = prop.multiProcessorCount;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        lsm_ctx_destroy(c);
+        return -(1000 + (int)e);
+    }
     *out = c;
     return 0;
 }
 
 extern "C" int lsm_ctx_destroy(lsm_ctx *ctx) {
+    if (!ctx) return 0;
+    if (hipSetDevice(ctx->device) == hipSuccess) {
+        if (ctx->join) (void)hipEventDestroy(ctx->join);
+        if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+        if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    }
     free(ctx);
     return 0;
 }

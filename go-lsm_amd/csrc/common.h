@@ -12,10 +12,15 @@
         if (_e != hipSuccess) return -(1000 + (int)_e);     \
     } while (0)
 
-// One context per device and caller thread (include/lsm_gpu.h).
+// One context per device and caller thread (include/lsm_gpu.h): the device,
+// its CU count, and a side stream with fork / join events for a call that
+// runs two independent kernels at once (lsm_build_sst: the VALU-bound filters
+// beside the HBM-bound regions, co-resident on the CUs).
 struct lsm_ctx {
     int device;
-    int num_cus;  // the persistent launches take one workgroup per CU
+    int num_cus;
+    hipStream_t side;
+    hipEvent_t fork, join;
 };
 
 namespace lsm {

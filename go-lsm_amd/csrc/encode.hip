@@ -389,9 +389,10 @@ __device__ bool encode_chunk_staged(const RegionSrc &S, uint64_t c0, uint32_t cn
 constexpr uint32_t kGatherDwords = 1856;  // 7.25 KiB per wave
 constexpr uint32_t kGatherMaskWords = kWave;  // one per lane; >= 2 * ceil(kGatherDwords / 64)
 
-template <int G>
+template <int G, uint32_t GD = kGatherDwords>
 __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint8_t *dst,
                                     uint32_t *lds) {
+    static_assert(kGatherMaskWords >= 2 * ((GD + 63) / 64), "one mask bit per image dword");
     static_assert(G != LSM_GRAMMAR_KV, "one payload per record");
     constexpr uint32_t pre = G == LSM_GRAMMAR_V ? 4 : 12;
     const uint32_t lane = lane_id();
@@ -411,13 +412,13 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
     tot64 = uni64(tot64);  // wave-uniform: keeps the loops below scalar
     const uint32_t ph = (uint32_t)(Sc & 3);
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
-    if (tot64 + 64 > 4ull * kGatherDwords) return false;
+    if (tot64 + 64 > 4ull * GD) return false;
     const uint32_t tot = (uint32_t)tot64, P = (uint32_t)P64;
     const uint32_t nD = (tot + ph + 3) >> 2;
     const int32_t T = (int32_t)ph - (int32_t)head;
     const uint32_t sh = (uint32_t)T & 3;
     const uint32_t OD = 8 + (((uint32_t)(-(T - (int32_t)sh)) >> 2) & 3);
-    if (OD + ((nD + 63) & ~63u) + 8 > kGatherDwords) return false;
+    if (OD + ((nD + 63) & ~63u) + 8 > GD) return false;
 
     // gather: image dword D covers chunk bytes [4D - ph, 4D - ph + 4)
     const uint32_t sbytes = (uint32_t)(soff[c0 + cnt] - Sc);  // wave-uniform load below
@@ -428,7 +429,7 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
     // in an LDS mask, and window i (dwords [64i, 64i+64)) reads its 64-bit
     // word once -- a lane's record is the running count plus a masked
     // popcount (mbcnt), no search.
-    uint32_t *mask = lds + kGatherDwords;  // kGatherMaskWords after the image
+    uint32_t *mask = lds + GD;  // kGatherMaskWords after the image
     for (uint32_t w = lane; w < kGatherMaskWords; w += kWave) mask[w] = 0;
     __builtin_amdgcn_wave_barrier();
     __asm__ __volatile__("" ::: "memory");
@@ -507,17 +508,19 @@ union RegionLds {  // V / IDX only: no KV stage
     uint32_t gather[kGatherDwords + kGatherMaskWords];
 };
 
+
 // Chunk encoder dispatch: DMA gather (V / IDX), LDS-staged (KV), then the
 // global-source fallback for chunks too large for LDS.  The three LDS views
 // alias one per-wave buffer.
-template <int G>
+template <int G, uint32_t GD = kGatherDwords>
 __device__ __forceinline__ void encode_chunk_any(const RegionSrc &S, uint64_t c0, uint32_t cnt,
                                                  uint8_t *dst, uint32_t *gather, StageLds *st,
                                                  ChunkTable *ct) {
     if (G == LSM_GRAMMAR_KV) {
         if (encode_chunk_staged<LSM_GRAMMAR_KV>(S, c0, cnt, dst, st)) return;
     } else {
-        if (encode_chunk_gather<G == LSM_GRAMMAR_KV ? LSM_GRAMMAR_V : G>(S, c0, cnt, dst, gather))
+        if (encode_chunk_gather<G == LSM_GRAMMAR_KV ? LSM_GRAMMAR_V : G, GD>(S, c0, cnt, dst,
+                                                                             gather))
             return;
     }
     encode_chunk<G>(S, c0, cnt, dst, ct);
@@ -576,29 +579,11 @@ __device__ __forceinline__ uint32_t be_dword(const uint32_t *bits, uint64_t q) {
 // inside the .sst): big-endian bytes, whole dwords inside the slice's byte
 // range and single bytes at its edges (the neighbouring bytes belong to the
 // other slice or to the filter prefix).  Native mode: u64 words to native.
-// Thread groups a body runs on: the whole workgroup, or the first waves of
-// one (sst_build_kernel's filter waves) with an LDS-counter barrier, so the
-// other waves keep streaming without joining the filter's barriers.
+// The thread group a filter body runs on (the whole workgroup).
 struct WgGroup {
     __device__ uint32_t tid() const { return threadIdx.x; }
     __device__ uint32_t size() const { return blockDim.x; }
     __device__ void sync() { __syncthreads(); }
-};
-
-struct WaveGroup {
-    uint32_t nw;    // waves 0 .. nw-1 of the workgroup
-    uint32_t *ctr;  // LDS arrival counter (zeroed before the group starts)
-    uint32_t gen;   // arrivals this wave has waited for
-    __device__ uint32_t tid() const { return threadIdx.x; }
-    __device__ uint32_t size() const { return nw * kWave; }
-    __device__ void sync() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        gen += nw;
-        if (lane_id() == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
-            __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
 };
 
 template <class Grp>
@@ -706,6 +691,7 @@ struct BloomFileArgs {
     uint64_t m, mrecip;
     uint32_t k;
     uint32_t split;   // slice 0 = bits [0, split); split >= m: one slice
+    uint32_t c64;     // 2^64 mod m (m <= 2^30)
     uint32_t *pos;    // slice-1 list of filter f at f * k * maxr (two slices only)
     uint32_t maxr;
     uint64_t nwords;
@@ -767,8 +753,16 @@ __device__ void bloom_file_body(Grp &g, const BloomFileArgs &a, uint32_t f, uint
         // by class c = j%4 the multiplier is h2, h3, h3, h2, so each class is
         // an arithmetic progression with step 4*h2 or 4*h3 -- additions only
         // (64-bit multiplies are quarter-rate).
+        // The residues mod m follow the progressions too: r += (step mod m),
+        // less (2^64 mod m) when the 64-bit addition wraps -- 32-bit adds and
+        // v_min instead of a Barrett reduction per location (m <= 2^30).
         uint64_t loc[4] = {h[0], h[1] + h[3], h[0] + (h[3] << 1), h[1] + h[2] + (h[2] << 1)};
         const uint64_t st2 = h[2] << 2, st3 = h[3] << 2;
+        const uint32_t m32 = (uint32_t)a.m, rl = (uint32_t)a.mrecip, rh = (uint32_t)(a.mrecip >> 32);
+        uint32_t res[4];
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) res[c] = mod_small(loc[c], m32, rl, rh);
+        const uint32_t d2 = mod_small(st2, m32, rl, rh), d3 = mod_small(st3, m32, rl, rh);
         for (uint32_t j0 = 0; j0 < a.k; j0 += kBinBatch) {
             uint32_t pp[kBinBatch];
             uint32_t c1 = 0;
@@ -777,9 +771,17 @@ __device__ void bloom_file_body(Grp &g, const BloomFileArgs &a, uint32_t f, uint
                 const uint32_t j = j0 + jj;
                 const bool valid = act && j < a.k;
                 const uint32_t c = jj & 3;  // j0 is a multiple of 4
-                const uint32_t p = mod_small(loc[c], (uint32_t)a.m, (uint32_t)a.mrecip,
-                                             (uint32_t)(a.mrecip >> 32));
-                loc[c] += (c == 0 || c == 3) ? st2 : st3;
+                const uint32_t p = res[c];
+                {
+                    const bool a2 = c == 0 || c == 3;
+                    const uint64_t nl = loc[c] + (a2 ? st2 : st3);
+                    const bool carry = nl < loc[c];
+                    loc[c] = nl;
+                    uint32_t t = res[c] + (a2 ? d2 : d3);
+                    t = min(t, t - m32);
+                    const uint32_t u = t - a.c64;
+                    res[c] = carry ? min(u, u + m32) : t;
+                }
                 const bool in1 = p >= (uint32_t)lo1;  // lo1 <= m <= 2^30
                 if (valid && !in1) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
                 pp[jj] = valid && in1 ? p : 0xFFFFFFFFu;
@@ -895,14 +897,18 @@ constexpr uint32_t kSstChunkRecs = kSstWaves * kWave;  // records per workgroup
 
 // Data region (V grammar) and index region (IDX grammar) of file blockIdx.x,
 // records chunk blockIdx.y.
+constexpr uint32_t kRegWaveRecs = kWave;                   // records per wave
+constexpr uint32_t kRegChunkRecs = kSstWaves * kRegWaveRecs;  // records per workgroup
+
 __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
     __shared__ RegionLds lds[kSstWaves];
     const uint32_t f = blockIdx.x;
     const SstLayout L = sst_layout(a, f);
     const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kSstChunkRecs + (uint64_t)wave * kWave;
+    const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kRegChunkRecs + (uint64_t)wave * kRegWaveRecs;
     if (c0 >= L.e) return;
-    const uint32_t cnt = (uint32_t)((L.e - c0) < (uint64_t)kWave ? (L.e - c0) : kWave);
+    const uint32_t cnt =
+        (uint32_t)((L.e - c0) < (uint64_t)kRegWaveRecs ? (L.e - c0) : kRegWaveRecs);
     uint8_t *img = a.out + uni64(a.file_off[f]);
     const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
     const uint64_t Kc = uni64(a.koff[c0]), Vc = uni64(a.voff[c0]);
@@ -913,30 +919,12 @@ __global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
     S.rs = L.s;
     S.vrs = Vs;
     if (!a.skip_v)
-        encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
-                                        lds[wave].gather, nullptr, &lds[wave].ct);
-    encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
-                                      lds[wave].gather, nullptr, &lds[wave].ct);
-}
-
-// The V and IDX regions of records [c0, c0 + cnt) of file f by one wave
-// (lds: its gather buffer).
-__device__ void sst_region_chunk(const SstArgs &a, uint32_t f, uint64_t c0, uint32_t cnt,
-                                 RegionLds *lds) {
-    const SstLayout L = sst_layout(a, f);
-    uint8_t *img = a.out + uni64(a.file_off[f]);
-    const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
-    const uint64_t Kc = uni64(a.koff[c0]), Vc = uni64(a.voff[c0]);
-    RegionSrc S;
-    S.keys = a.keys; S.koff = a.koff; S.vals = a.vals; S.voff = a.voff;
-    S.idx_off = nullptr;
-    S.idx_base = (int64_t)L.data_off;
-    S.rs = L.s;
-    S.vrs = Vs;
-    encode_chunk_any<LSM_GRAMMAR_V>(S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs),
-                                    lds->gather, nullptr, &lds->ct);
-    encode_chunk_any<LSM_GRAMMAR_IDX>(S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks),
-                                      lds->gather, nullptr, &lds->ct);
+        encode_chunk_any<LSM_GRAMMAR_V>(
+            S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs), lds[wave].gather, nullptr,
+            &lds[wave].ct);
+    encode_chunk_any<LSM_GRAMMAR_IDX>(
+        S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks), lds[wave].gather, nullptr,
+        &lds[wave].ct);
 }
 
 // Data region (V grammar, sstable.go:159-175) of file blockIdx.x straight
@@ -1075,10 +1063,9 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
     }
 }
 
-// Header, filter-block prefix and footer of file blockIdx.x (one wave; byte
-// stores, since the neighbouring bytes belong to other kernels).  The filter
-// words themselves are stored by the bloom kernels.
-// Header, filter prefix and footer of file f by one wave.
+// Header, filter-block prefix and footer of file f (one wave; byte stores,
+// since the neighbouring bytes belong to other kernels).  The filter words
+// themselves are stored by the bloom kernels.
 __device__ void sst_meta_body(const SstArgs &a, uint32_t f) {
     const SstLayout L = sst_layout(a, f);
     uint8_t *img = a.out + uni64(a.file_off[f]);
@@ -1113,109 +1100,6 @@ __device__ void sst_meta_body(const SstArgs &a, uint32_t f) {
 
 __global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body(a, blockIdx.x); }
 
-// ---- the fused .sst build ------------------------------------------------------
-//
-// SSTable.Add feeds each pair to the data block, the index block and the
-// bloom filter in one pass (sstable.go:322-326).  Here one persistent launch
-// (one 1024-thread workgroup per CU) builds every image, with two roles
-// side by side on each CU:
-//   * filter waves 0-7 build the filters of files blockIdx.x, +grid, ...:
-//     hash each key once, set the bits of the LDS slice, list the few past
-//     it, then the rest from the list (bloom_file_body on the wave group,
-//     LDS-counter barriers), then the header, filter prefix and footer;
-//   * region waves 8-15 take 64-record chunks of the V and IDX regions from
-//     a global counter (any file), DMA-gathered through their LDS buffers.
-// The filter is VALU-bound and the regions HBM-bound, so each CU does both
-// at once; filter waves that run out of files join the region work (their
-// buffers in the slice's LDS).  No workgroup waits on another.
-constexpr uint32_t kBuildWaves = 16;
-constexpr uint32_t kBuildBloomWaves = 8;
-constexpr uint32_t kBuildLdsBytes = 160 * 1024 - 256;  // dynamic; + the static counters
-constexpr uint32_t kBuildRegionBytes = (kBuildWaves - kBuildBloomWaves) * sizeof(RegionLds);
-constexpr uint32_t kBuildSliceBytes = (kBuildLdsBytes - kBuildRegionBytes) / 8 * 8;
-static_assert(kBuildSliceBytes >= kBuildBloomWaves * sizeof(RegionLds), "filter waves' buffers");
-constexpr uint32_t kBuildChunk = kWave;  // records per region task
-
-struct BuildWork {
-    uint64_t *chunk_base;  // nfile + 1: exclusive scan of ceil(records / kBuildChunk)
-    uint32_t *next;        // region task counter
-    uint32_t nfile;
-};
-
-// chunk_base and the task counter, one workgroup.
-__global__ __launch_bounds__(1024) void sst_build_prep_kernel(const uint64_t *file_start, BuildWork w) {
-    __shared__ uint64_t wsum[16];
-    __shared__ uint64_t carry;
-    if (threadIdx.x == 0) {
-        carry = 0;
-        *w.next = 0;
-    }
-    __syncthreads();
-    for (uint32_t f0 = 0; f0 < w.nfile; f0 += 1024) {
-        const uint32_t f = f0 + threadIdx.x;
-        uint64_t c = 0;
-        if (f < w.nfile) c = (file_start[f + 1] - file_start[f] + kBuildChunk - 1) / kBuildChunk;
-        uint64_t tot;
-        const uint64_t ex = wave_excl_scan64(c, &tot);
-        const uint32_t wv = threadIdx.x / kWave;
-        if (lane_id() == 0) wsum[wv] = tot;
-        __syncthreads();
-        uint64_t pre = carry;
-        for (uint32_t v = 0; v < wv; v++) pre += wsum[v];
-        if (f < w.nfile) w.chunk_base[f] = pre + ex;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint64_t t = carry;
-            for (uint32_t v = 0; v < 16; v++) t += wsum[v];
-            carry = t;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) w.chunk_base[w.nfile] = carry;
-}
-
-// Region tasks until the counter runs out (one wave; lds: its buffer).
-__device__ void build_region_tasks(const SstArgs &a, const BuildWork &w, RegionLds *lds) {
-    const uint64_t total = uni64(w.chunk_base[w.nfile]);
-    for (;;) {
-        uint32_t t = 0;
-        if (lane_id() == 0) t = atomicAdd(w.next, 1u);
-        t = uni(t);
-        if (t >= total) return;
-        // the file holding task t: the last f with chunk_base[f] <= t
-        uint32_t lo = 0, hi = w.nfile;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (uni64(w.chunk_base[mid]) <= t) lo = mid;
-            else hi = mid;
-        }
-        const uint64_t s = uni64(a.file_start[lo]), e = uni64(a.file_start[lo + 1]);
-        const uint64_t c0 = s + (t - uni64(w.chunk_base[lo])) * kBuildChunk;
-        const uint32_t cnt = (uint32_t)(e - c0 < kBuildChunk ? e - c0 : kBuildChunk);
-        sst_region_chunk(a, lo, c0, cnt, lds);
-    }
-}
-
-__global__ __launch_bounds__(1024) void sst_build_kernel(SstArgs a, BloomFileArgs b, BuildWork w) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
-    __shared__ uint32_t n1, bar;
-    const uint32_t wave = uni(threadIdx.x / kWave);
-    if (threadIdx.x == 0) bar = 0;
-    __syncthreads();  // the only workgroup-wide barrier: the roles never meet again
-    if (wave < kBuildBloomWaves) {
-        WaveGroup g{kBuildBloomWaves, &bar, 0};
-        uint32_t *bits = reinterpret_cast<uint32_t *>(lds_raw);
-        for (uint32_t f = blockIdx.x; f < w.nfile; f += gridDim.x) {
-            bloom_file_body(g, b, f, bits, n1);
-            if (wave == 0) sst_meta_body(a, f);
-        }
-        // no filters left: region work, the buffers in the slice's LDS
-        build_region_tasks(a, w, reinterpret_cast<RegionLds *>(lds_raw) + wave);
-    } else {
-        build_region_tasks(a, w, reinterpret_cast<RegionLds *>(lds_raw + kBuildSliceBytes) +
-                                     (wave - kBuildBloomWaves));
-    }
-}
 
 // ---- probe / hash ----------------------------------------------------------
 
@@ -1909,25 +1793,12 @@ static uint32_t bloom_slices(uint64_t m) {
 }
 static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slices(m) <= 2; }
 
-// Filter bits kept in LDS by the fused build; a filter up to twice this is
-// built by it (the bits past the LDS slice go through a per-file list).
-static constexpr uint64_t kFusedCapBits = (uint64_t)kBuildSliceBytes * 8;
-static bool fused_build(uint64_t m) { return m <= (1ull << 30) && m <= 2 * kFusedCapBits; }
-
-// Workspace: [slice-1 position lists][fused build: chunk_base (nfile+1) | task counter]
-static uint64_t build_list_bytes(uint32_t nfile, uint32_t max_file_records, uint64_t m, uint32_t k) {
-    // the position list past the LDS slice: the fused build (m past its
-    // slice) and the two-slice hash-once filter of lsm_build_sst_views
-    const bool fused_list = fused_build(m) && m > kFusedCapBits;
-    const bool views_list = hash_once_bloom(m) && bloom_slices(m) >= 2;
-    if (!fused_list && !views_list) return 0;
-    const uint64_t kk = k ? k : 1;
-    return (kk * nfile * (uint64_t)max_file_records * 4 + 255) & ~255ull;
-}
-
 extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
                                                 uint64_t m, uint32_t k) {
-    return (size_t)(build_list_bytes(nfile, max_file_records, m, k) + 8ull * (nfile + 1) + 16);
+    // the slice-1 position lists of the two-slice hash-once filter
+    if (!hash_once_bloom(m) || bloom_slices(m) < 2) return 16;
+    const uint64_t kk = k ? k : 1;
+    return (size_t)(kk * nfile * (uint64_t)max_file_records * 4 + 16);
 }
 
 static uint64_t barrett_recip(uint64_t m) { return ~0ull / m; }
@@ -1962,41 +1833,9 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     a.k = kk;
     a.skip_v = views != nullptr;
 
-    // The fused build (lsm_build_sst): filters and regions in one launch.
-    if (!views && fused_build(m)) {
-        const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
-        if (!d_workspace || ws_bytes < need) return LSM_ESPACE;
-        const uint64_t list_bytes = build_list_bytes(nfile, max_file_records, m, kk);
-        uint8_t *ws = static_cast<uint8_t *>(d_workspace);
-        BloomFileArgs b;
-        b.keys = d_keys;
-        b.koff = d_koff;
-        b.file_start = d_file_start;
-        b.nkeys = 0;
-        b.m = m;
-        b.mrecip = barrett_recip(m);
-        b.k = kk;
-        b.split = (uint32_t)(m < kFusedCapBits ? m : kFusedCapBits);
-        b.pos = reinterpret_cast<uint32_t *>(ws);
-        b.maxr = max_file_records;
-        b.nwords = nwords;
-        b.out = d_out;
-        b.file_off = d_file_off;
-        b.bitmap = nullptr;
-        BuildWork w;
-        w.chunk_base = reinterpret_cast<uint64_t *>(ws + list_bytes);
-        w.next = reinterpret_cast<uint32_t *>(ws + list_bytes + 8ull * (nfile + 1));
-        w.nfile = nfile;
-        hipLaunchKernelGGL(sst_build_prep_kernel, dim3(1), dim3(1024), 0, s, d_file_start, w);
-        // one workgroup per CU (the LDS admits one): every CU hashes and streams
-        const uint32_t grid = (uint32_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
-        hipLaunchKernelGGL(sst_build_kernel, dim3(grid), dim3(1024), (size_t)kBuildLdsBytes, s, a, b, w);
-        LSM_HIP_CHECK(hipGetLastError());
-        return 0;
-    }
-
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
+    bool forked = false;
     if (hash_once_bloom(m)) {
         const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
         if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
@@ -2009,6 +1848,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
             b.m = m;
             b.mrecip = barrett_recip(m);
             b.k = kk;
+            b.c64 = (uint32_t)((~0ull % m + 1) % m);
             b.split = (uint32_t)sb;
             b.pos = static_cast<uint32_t *>(d_workspace);
             b.maxr = max_file_records;
@@ -2016,8 +1856,15 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
             b.out = d_out;
             b.file_off = d_file_off;
             b.bitmap = nullptr;
+            // fork: the filters first on the caller's stream (each
+            // workgroup needs 100 KiB of a CU's LDS, so they must be placed
+            // before the regions fill the CUs), the regions and the framing
+            // on the side stream beside them; joined below
+            LSM_HIP_CHECK(hipEventRecord(ctx->fork, s));
             hipLaunchKernelGGL(bloom_file_kernel, dim3(nfile), dim3(1024), (size_t)(sb / 8), s, b);
             LSM_HIP_CHECK(hipGetLastError());
+            LSM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->fork, 0));
+            forked = true;
         }
     } else {
         BloomArgs b;
@@ -2039,17 +1886,23 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     }
 
 
+    hipStream_t rs = forked ? ctx->side : s;  // the regions' stream
     if (chunks) {
-        hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, chunks), dim3(256), 0, s, a);
+        const uint32_t rchunks = (max_file_records + kRegChunkRecs - 1) / kRegChunkRecs;
+        hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rchunks), dim3(256), 0, rs, a);
         LSM_HIP_CHECK(hipGetLastError());
         if (views) {
-            hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, s, a,
+            hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, rs, a,
                                *views);
             LSM_HIP_CHECK(hipGetLastError());
         }
     }
-    hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, rs, a);
     LSM_HIP_CHECK(hipGetLastError());
+    if (forked) {  // join: the caller's stream waits for the regions
+        LSM_HIP_CHECK(hipEventRecord(ctx->join, ctx->side));
+        LSM_HIP_CHECK(hipStreamWaitEvent(s, ctx->join, 0));
+    }
     return 0;
 }
 
