@@ -59,12 +59,7 @@ struct DecodeArgs {
 // fields at wave-uniform block positions.
 //
 // Ring: NCH x 1 KiB chunks, filled by LDS-DMA (buffer_load_dwordx4 ... lds:
-// no VGPR staging).  Window: each lane holds 16 raw bytes of a 1 KiB, 16-byte
-// aligned slice of the stream (one ds_read_b128); a field at stream byte s is
-// two v_readlane of the lanes/dwords covering [s, s+4) plus a scalar funnel
-// shift, so a 4 KiB block costs ~5 LDS round trips instead of one per record.
-// NCH = 4 (4 KiB) for blocks that fit whole; blocks larger than that stream
-// through a 16 KiB ring (decode_large_kernel) with up to 15 KiB in flight.
+// no VGPR staging), read by the chase with ds_read at block positions.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_le(uint32_t k) {
     // s_waitcnt takes an immediate: one arm per count (N <= 16).
@@ -79,7 +74,6 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t k) {
 
 template <uint32_t NCH>
 struct BlockReaderT {
-    static constexpr uint32_t kBytes = NCH * kChunk;
     uint32_t *ring;
     rsrc_t rsrc;
     uint32_t h;        // block start inside its first 16-byte line
@@ -87,9 +81,6 @@ struct BlockReaderT {
     uint32_t nchunks;  // chunks covering [0, total)
     uint32_t hi_c;     // chunks [.., hi_c) have been issued into the ring
     uint32_t landed;   // chunks [.., landed) are known to be in LDS
-    uint32_t wb;       // window base (stream byte, 16-aligned)
-    u32x4 raw;         // lane j: stream bytes [wb + 16j, wb + 16j + 16)
-    bool have_win;
 
     __device__ void init(uint32_t *ring_, const uint8_t *in, uint64_t off, uint32_t n) {
         ring = ring_;
@@ -101,8 +92,6 @@ struct BlockReaderT {
         rsrc = make_rsrc(in + a0, total);
         hi_c = 0;
         landed = 0;
-        have_win = false;
-        wb = 0;
     }
 
     // Make stream bytes [s0, s0 + want) resident (clamped to the block and
@@ -139,36 +128,6 @@ struct BlockReaderT {
         landed = need_hi;
     }
 
-    __device__ __forceinline__ void load_window(uint32_t s) {
-        wb = s & ~15u;
-        ensure(wb);
-        const uint32_t w = ((wb + lane_id() * 16) % kBytes) / 4;
-        raw = *reinterpret_cast<const u32x4 *>(&ring[w]);
-        have_win = true;
-    }
-
-    // Dword d of lane l of the window (d, l wave-uniform).
-    __device__ __forceinline__ uint32_t pick(uint32_t d, uint32_t l) const {
-        uint32_t v0 = __builtin_amdgcn_readlane(raw.x, l);
-        uint32_t v1 = __builtin_amdgcn_readlane(raw.y, l);
-        uint32_t v2 = __builtin_amdgcn_readlane(raw.z, l);
-        uint32_t v3 = __builtin_amdgcn_readlane(raw.w, l);
-        return d == 0 ? v0 : d == 1 ? v1 : d == 2 ? v2 : v3;
-    }
-
-    // Little-endian u32 at block position p (wave-uniform).
-    __device__ __forceinline__ uint32_t field(uint32_t p) {
-        const uint32_t s = h + p;
-        if (!have_win || s - wb > kChunk - 4) load_window(s);
-        const uint32_t o = s - wb;
-        const uint32_t l = o >> 4, d = (o >> 2) & 3, sh = o & 3;
-        uint32_t lo = pick(d, l);
-        if (sh) {
-            const uint32_t hi = pick((d + 1) & 3, l + (d == 3));
-            lo = (lo >> (8 * sh)) | (hi << (32 - 8 * sh));
-        }
-        return lo;
-    }
 };
 template <int G>
 struct MinRecord { static constexpr uint32_t R = G == LSM_GRAMMAR_V ? 4 : G == LSM_GRAMMAR_KV ? 8 : 12; };
@@ -316,6 +275,46 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
         r = mul24(r, L) > q ? r - 1 : r;
         return mul24(r + 1, L) <= q ? r + 1 : r;
     };
+    if (L >= 16) {
+        // fields of 16+ bytes: one 16-byte output chunk per lane (two
+        // ds_read_b128 per field it touches, one dwordx4 store); a chunk
+        // holds at most one field boundary, at byte k: bytes [k, 16) are the
+        // next field's first bytes, shifted in branch-free
+        const uint32_t lead16 = (uint32_t)((uintptr_t)out & 15);
+        uint8_t *b0 = out - lead16;
+        const uint32_t nc = (lead16 + T + 15) >> 4;
+        const uint32_t npass = (nc + kWave - 1) / kWave;  // every lane runs each pass
+#pragma unroll 1
+        for (uint32_t pass = 0; pass < npass; pass++) {
+            const uint32_t c = pass * kWave + lane_id();
+            const bool act = c < nc;
+            const int q = (int)(16 * c) - (int)lead16;
+            const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
+            const uint32_t r = rec(qc), o = qc - mul24(r, L), k = L - o;
+            u32x4 v = rb.u128(src0 + mul24(r, S) + o);
+            if (__ballot(act && k < 16)) {
+                const u32x4 B = rb.u128(src0 + mul24(r + 1, S));
+                // B shifted to start at byte k: dword d of it = bytes
+                // [4d + t, 4d + t + 4) of {0, 0, 0, 0, B}, t = 16 - k
+                const uint32_t t = 16 - (k < 16 ? k : 16), m = t >> 2, sh = t & 3;
+                auto W = [&](uint32_t i) -> uint32_t {  // {0,0,0,0,B.x,B.y,B.z,B.w}[i]
+                    return i == 4 ? B.x : i == 5 ? B.y : i == 6 ? B.z : i == 7 ? B.w : 0u;
+                };
+                uint32_t o4[4];
+#pragma unroll
+                for (uint32_t d = 0; d < 4; d++) {
+                    const uint32_t bs = funnel(W(d + m), W(d + m + 1), sh);
+                    const uint32_t a = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+                    const int kd = (int)k - 4 * (int)d;  // bytes of this dword from A
+                    const uint32_t mask = kd >= 4 ? ~0u : kd <= 0 ? 0u : (1u << (8 * kd)) - 1;
+                    o4[d] = (a & mask) | (bs & ~mask);
+                }
+                if (k < 16) v = u32x4{o4[0], o4[1], o4[2], o4[3]};
+            }
+            if (act) store_chunk(b0 + 16 * c, v, -q, (int)T - q);
+        }
+        return;
+    }
     // four dwords per lane per pass, all their LDS reads in flight together
     // (ring reads are indexed modulo the ring, so lanes past the end read
     // harmless bytes)
