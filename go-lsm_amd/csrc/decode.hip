@@ -254,10 +254,15 @@ __device__ __forceinline__ void set_dword(u32x4 &v, uint32_t j, uint32_t w) {
 
 // A verified run: cnt records of stride S whose field of L bytes starts at
 // ring stream byte src0 + i*S (all landed), packed to out[0, cnt*L).  One
-// output dword per lane (consecutive lanes read consecutive ring dwords: no
-// bank conflicts, 256-byte coalesced stores), branch-free for L >= 4: the
-// dword's first byte lies in field r at offset o; if fewer than 4 of the
-// field's bytes remain (k < 4) the rest are the next field's first bytes.
+// output dword per lane per step (consecutive lanes read consecutive ring
+// dwords: no bank conflicts; 256-byte coalesced stores), with as few VALU
+// operations per dword
+// as the shape allows: the field index by one FMA (q / L rounded from
+// q + 1/2, exact for q < 2^16), the second ring dword only where some lane's
+// source is unaligned, the next field's bytes only where a field boundary
+// falls inside some lane's dword (k < 4), bytes singly only in the run's
+// first and last dword.  Ring reads are indexed modulo the ring, so lanes
+// past the end read harmless bytes.
 template <uint32_t NCH, bool LIN>
 __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, uint8_t *out,
                                                uint32_t src0, uint32_t S, uint32_t L,
@@ -269,87 +274,41 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
     const uint32_t nd = (lead + T + 3) >> 2;
     // full-rate 24-bit products (v_mul_u32_u24): every operand here is < 2^24
     auto mul24 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFFFu) * (y & 0xFFFFFFu); };
-    const float inv = __builtin_amdgcn_rcpf((float)L);
-    auto rec = [&](uint32_t q) -> uint32_t {  // q / L: q < 2^16, L < 2^14, r <= 65
-        uint32_t r = (uint32_t)((float)q * inv);
-        r = mul24(r, L) > q ? r - 1 : r;
-        return mul24(r + 1, L) <= q ? r + 1 : r;
+    const float inv = 1.0f / (float)L, hinv = 0.5f * inv;  // once per run
+    auto rec = [&](uint32_t q) -> uint32_t {  // floor(q / L), q < 2^16
+        return (uint32_t)__builtin_fmaf((float)q, inv, hinv);
     };
-    if (L >= 16) {
-        // fields of 16+ bytes: one 16-byte output chunk per lane (two
-        // ds_read_b128 per field it touches, one dwordx4 store); a chunk
-        // holds at most one field boundary, at byte k: bytes [k, 16) are the
-        // next field's first bytes, shifted in branch-free
-        const uint32_t lead16 = (uint32_t)((uintptr_t)out & 15);
-        uint8_t *b0 = out - lead16;
-        const uint32_t nc = (lead16 + T + 15) >> 4;
-        const uint32_t npass = (nc + kWave - 1) / kWave;  // every lane runs each pass
-#pragma unroll 1
-        for (uint32_t pass = 0; pass < npass; pass++) {
-            const uint32_t c = pass * kWave + lane_id();
-            const bool act = c < nc;
-            const int q = (int)(16 * c) - (int)lead16;
-            const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
-            const uint32_t r = rec(qc), o = qc - mul24(r, L), k = L - o;
-            u32x4 v = rb.u128(src0 + mul24(r, S) + o);
-            if (__ballot(act && k < 16)) {
-                const u32x4 B = rb.u128(src0 + mul24(r + 1, S));
-                // B shifted to start at byte k: dword d of it = bytes
-                // [4d + t, 4d + t + 4) of {0, 0, 0, 0, B}, t = 16 - k
-                const uint32_t t = 16 - (k < 16 ? k : 16), m = t >> 2, sh = t & 3;
-                auto W = [&](uint32_t i) -> uint32_t {  // {0,0,0,0,B.x,B.y,B.z,B.w}[i]
-                    return i == 4 ? B.x : i == 5 ? B.y : i == 6 ? B.z : i == 7 ? B.w : 0u;
-                };
-                uint32_t o4[4];
-#pragma unroll
-                for (uint32_t d = 0; d < 4; d++) {
-                    const uint32_t bs = funnel(W(d + m), W(d + m + 1), sh);
-                    const uint32_t a = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-                    const int kd = (int)k - 4 * (int)d;  // bytes of this dword from A
-                    const uint32_t mask = kd >= 4 ? ~0u : kd <= 0 ? 0u : (1u << (8 * kd)) - 1;
-                    o4[d] = (a & mask) | (bs & ~mask);
-                }
-                if (k < 16) v = u32x4{o4[0], o4[1], o4[2], o4[3]};
-            }
-            if (act) store_chunk(b0 + 16 * c, v, -q, (int)T - q);
-        }
-        return;
-    }
-    // four dwords per lane per pass, all their LDS reads in flight together
-    // (ring reads are indexed modulo the ring, so lanes past the end read
-    // harmless bytes)
-    constexpr uint32_t U = 4;
+    constexpr uint32_t U = 1;  // dwords per lane per step (2 and 4 measured no faster)
+    const uint32_t lane = lane_id();
 #pragma unroll 1
     for (uint32_t w0 = 0; w0 < nd; w0 += U * kWave) {
-        uint32_t W[U], qv[U];
-        if (L >= 4) {
-            uint32_t kk[U], rr[U];
+        uint32_t W[U], sb[U], kk[U], rr[U];
+        int qv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const int q = (int)(4 * (w0 + u * kWave + lane)) - (int)lead;
+            const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
+            const uint32_t r = rec(qc), o = qc - mul24(r, L);
+            qv[u] = q;
+            rr[u] = r;
+            kk[u] = L - o;
+            sb[u] = src0 + mul24(r, S) + o;
+            W[u] = rb.word(sb[u] >> 2);
+        }
+        bool unal = false, cross = false;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            unal |= (sb[u] & 3) != 0;
+            cross |= kk[u] < 4;
+        }
+        if (__ballot(unal)) {
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) W[u] = funnel(W[u], rb.word((sb[u] >> 2) + 1), sb[u]);
+        }
+        if (L < 4) {  // fields of 0-3 bytes: byte by byte
 #pragma unroll
             for (uint32_t u = 0; u < U; u++) {
-                const int q = (int)(4 * (w0 + u * kWave + lane_id())) - (int)lead;
-                const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
-                const uint32_t r = rec(qc), o = qc - mul24(r, L);
-                qv[u] = (uint32_t)q;
-                kk[u] = L - o;
-                rr[u] = r;
-                W[u] = rb.u32(src0 + mul24(r, S) + o);
-            }
-            bool any = false;
-#pragma unroll
-            for (uint32_t u = 0; u < U; u++) any |= kk[u] < 4;
-            if (__ballot(any)) {  // a field boundary inside some lane's dword
-#pragma unroll
-                for (uint32_t u = 0; u < U; u++) {
-                    const uint32_t B = rb.u32(src0 + mul24(rr[u] + 1, S)), k = kk[u];
-                    W[u] = k < 4 ? (W[u] & ((1u << (8 * k)) - 1)) | (B << (8 * k)) : W[u];
-                }
-            }
-        } else {  // fields of 0-3 bytes: byte by byte
-#pragma unroll
-            for (uint32_t u = 0; u < U; u++) {
-                const int q = (int)(4 * (w0 + u * kWave + lane_id())) - (int)lead;
-                const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
-                qv[u] = (uint32_t)q;
+                const uint32_t qc = qv[u] < 0 ? 0u : (uint32_t)qv[u];
                 uint32_t x = 0;
                 for (uint32_t t = 0; t < 4; t++) {
                     const uint32_t qq = qc + t;
@@ -360,19 +319,23 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
                 }
                 W[u] = x;
             }
+        } else if (__ballot(cross)) {  // a field boundary inside some lane's dword
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t B = rb.u32(src0 + mul24(rr[u] + 1, S)), k = kk[u];
+                W[u] = k < 4 ? (W[u] & ((1u << (8 * k)) - 1)) | (B << (8 * k)) : W[u];
+            }
         }
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
-            const uint32_t w = w0 + u * kWave + lane_id();
-            if (w >= nd) continue;
-            const int q = (int)qv[u];
-            const uint32_t qc = q < 0 ? 0u : (uint32_t)q;
-            const uint32_t sh = qc - (uint32_t)q;  // leading bytes before the run (first dword)
-            if (sh == 0 && qc + 4 <= T) {
+            const uint32_t w = w0 + u * kWave + lane;
+            const int q = qv[u];
+            if (q >= 0 && (uint32_t)q + 4 <= T) {
                 a0[w] = W[u];
-            } else {  // the run's first or last dword, shared with its neighbours
+            } else if (w < nd) {  // the run's first or last dword, shared with its neighbours
+                const uint32_t sh = q < 0 ? (uint32_t)(-q) : 0u;  // bytes before the run
                 uint8_t *b = reinterpret_cast<uint8_t *>(a0 + w);
-                for (uint32_t t = sh; t < 4 && (uint32_t)q + t < T; t++)
+                for (uint32_t t = sh; t < 4 && (uint32_t)(q + (int)t) < T; t++)
                     b[t] = (uint8_t)(W[u] >> (8 * (t - sh)));
             }
         }
