@@ -58,6 +58,8 @@ def parse(argv=None):
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-timing output check (diagnostic library variants only)")
     ap.add_argument("--e2e", action="store_true",
                     help="host-resident blocks: pinned H2D -> decode -> compact -> D2H "
                          "(the PCIe-inclusive rate recorded in DESIGN.md; not the headline)")

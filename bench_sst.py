@@ -91,7 +91,59 @@ def bench_sst(args, world, rank, local):
                      "kernel_ms_median": round(float(np.median(times)), 5),
                      "kernel_ms_min": round(float(times.min()), 5)},
     }
+    if not args.no_verify:
+        verify_sst(ctx, batch, sb, keys, koff)
+    out["config"]["verified"] = False if args.no_verify else ("every image parsed by lsm_decode_sst, V/IDX regions equal to the "
+                                 "input, every 16th key present in its file's filter")
     return out, (keys, koff, vals, voff, starts, sb.file_size)
+
+
+def verify_sst(ctx, batch, sb, keys, koff):
+    """Check the timed output on the device, through the product's own f1
+    and f3 paths (their parity is tested against the oracle): every image
+    parses (SSTable.DecodeFrom stage ok, index and data counts equal the file's
+    records), its V region holds [u32 vlen][value] of exactly the input's
+    values, its IDX region [u32 klen][key][i64 offset] the input's keys and
+    their records' offsets, and every 16th key tests present in its own file's
+    filter (a bloom filter has no false negatives).  Fails the line on any
+    difference."""
+    nf = len(sb.file_start) - 1
+    r = lsmgpu.decode_sst(ctx, sb.out, sb.file_off, sb.file_size)
+    meta = r.meta_numpy()
+    cnt = np.diff(sb.file_start.astype(np.int64))
+    bad = np.nonzero((meta["stage"] != 0) | (meta["status"] != 0) |
+                     (meta["ndata"] != cnt) | (meta["nidx"] != cnt))[0]
+    if bad.size:
+        raise SystemExit(f"bench_sst: {bad.size} images fail to decode (first {int(bad[0])}: "
+                         f"stage {int(meta['stage'][bad[0]])})")
+    kl, vl = int(koff[1] - koff[0]), int(batch.voff_host[1] - batch.voff_host[0])
+    img = sb.out
+    dev = img.device
+    le = lambda x: torch.tensor(list(int(x).to_bytes(4, "little")), dtype=torch.uint8, device=dev)
+    for f in range(nf):
+        s, e = int(sb.file_start[f]), int(sb.file_start[f + 1])
+        n, base = e - s, int(sb.file_off[f])
+        d0, i0 = base + int(meta["data_off"][f]), base + int(meta["idx_off"][f])
+        V = img[d0:d0 + n * (4 + vl)].view(n, 4 + vl)
+        I = img[i0:i0 + n * (12 + kl)].view(n, 12 + kl)
+        off = int(meta["data_off"][f]) + (4 + vl) * torch.arange(n, dtype=torch.int64, device=dev)
+        ok = (bool((V[:, :4] == le(vl)).all()) and
+              torch.equal(V[:, 4:], batch.vals[s * vl:e * vl].view(n, vl)) and
+              bool((I[:, :4] == le(kl)).all()) and
+              torch.equal(I[:, 4:4 + kl], batch.keys[s * kl:e * kl].view(n, kl)) and
+              torch.equal(I[:, 4 + kl:].contiguous().view(torch.int64).view(-1), off))
+        if not ok:
+            raise SystemExit(f"bench_sst: image {f} differs from the input")
+    sample = np.arange(0, len(koff) - 1, 16)
+    ks = keys.reshape(-1, kl)[sample].reshape(-1)
+    probe = lsmgpu.batch_to_device(ctx, ks, np.arange(sample.size + 1, dtype=np.uint64) * kl,
+                                   np.zeros(16, np.uint8), np.zeros(sample.size + 1, np.uint64))
+    hit = lsmgpu.may_contain(ctx, img, r, probe)
+    fidx = torch.from_numpy(np.searchsorted(sb.file_start[1:].astype(np.int64), sample,
+                                            side="right")).to(dev)
+    own = hit[torch.arange(sample.size, device=dev), fidx]
+    if not bool((own == 1).all()):
+        raise SystemExit(f"bench_sst: {int((own != 1).sum())} sampled keys missing from their filter")
 
 
 def cpu_baseline_sst(args, data):

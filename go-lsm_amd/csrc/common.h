@@ -36,6 +36,20 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
 
+// Global-memory views.  A pointer rebuilt from an integer loses the
+// compiler's address-space inference and is accessed with FLAT instructions,
+// which also count in lgkmcnt: every later LDS wait would wait for them.
+template <class T>
+using gptr_t = __attribute__((address_space(1))) T *;
+template <class T>
+__device__ __forceinline__ gptr_t<T> gbl(T *p) {
+    return (gptr_t<T>)p;
+}
+template <class T>
+__device__ __forceinline__ gptr_t<T> gbl_at(uintptr_t a) {
+    return (gptr_t<T>)reinterpret_cast<T *>(a);
+}
+
 // Wave-uniform value: lets hipcc keep it in an SGPR (T20 in the HIP guide).
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
@@ -132,7 +146,7 @@ __device__ __forceinline__ void wave_copy(rsrc_t r, uint32_t src, uint8_t *dst, 
     if (len == 0) return;
     uintptr_t d0 = reinterpret_cast<uintptr_t>(dst);
     uint32_t head = (uint32_t)(d0 & 3);
-    uint32_t *dA = reinterpret_cast<uint32_t *>(d0 - head);
+    gptr_t<uint32_t> dA = gbl_at<uint32_t>(d0 - head);
     uint32_t ndw = (head + len + 3) >> 2;
     for (uint32_t j = lane_id(); j < ndw; j += kWave) {
         uint32_t S = src - head + 4 * j;  // may wrap below 0: OOB loads return 0
@@ -144,7 +158,7 @@ __device__ __forceinline__ void wave_copy(rsrc_t r, uint32_t src, uint8_t *dst, 
         if (lo_b == 0 && hi_b == 4) {
             dA[j] = v;
         } else {
-            uint8_t *db = reinterpret_cast<uint8_t *>(dA + j);
+            gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + j);
             for (uint32_t t = lo_b; t < hi_b; t++) db[t] = (uint8_t)(v >> (8 * t));
         }
     }

@@ -109,7 +109,7 @@ __device__ void encode_chunk(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint
 
     const uintptr_t Ob = reinterpret_cast<uintptr_t>(dst);
     const uint32_t head = (uint32_t)(Ob & 3);
-    uint32_t *dA = reinterpret_cast<uint32_t *>(Ob - head);
+    gptr_t<uint32_t> dA = gbl_at<uint32_t>(Ob - head);
     const uint64_t ndw = (head + tot + 3) >> 2;
 
     uint32_t r = 0;             // this lane's record cursor
@@ -146,7 +146,7 @@ __device__ void encode_chunk(const RegionSrc &S, uint64_t c0, uint32_t cnt, uint
         }
         // Slow path (length fields, record boundaries, chunk edges): byte by byte.
         uint32_t rr = r;
-        uint8_t *db = reinterpret_cast<uint8_t *>(dA + d);
+        gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + d);
         for (uint32_t t = 0; t < 4; t++) {
             const int64_t u = u0 + t;
             if (u < 0 || (uint64_t)u >= tot) continue;
@@ -310,7 +310,7 @@ __device__ bool encode_chunk_staged(const RegionSrc &S, uint64_t c0, uint32_t cn
     const StagedTable &t = L->tb;
     const uintptr_t Ob = reinterpret_cast<uintptr_t>(dst);
     const uint32_t head = (uint32_t)(Ob & 15);
-    u32x4 *dA = reinterpret_cast<u32x4 *>(Ob - head);
+    gptr_t<u32x4> dA = gbl_at<u32x4>(Ob - head);
     const uint32_t nseg = (head + tot + 15) >> 4;
     uint32_t r = 0;
     for (uint32_t e = lane; e < nseg; e += kWave) {
@@ -353,7 +353,7 @@ __device__ bool encode_chunk_staged(const RegionSrc &S, uint64_t c0, uint32_t cn
             dA[e] = out;
         } else {
             // chunk-edge segment: only this chunk's bytes, one at a time
-            uint8_t *db = reinterpret_cast<uint8_t *>(dA + e);
+            gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + e);
             uint32_t rb = r;
             for (uint32_t b = 0; b < 16; b++) {
                 const int32_t u = u0 + (int32_t)b;
@@ -469,7 +469,7 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
     __asm__ __volatile__("" ::: "memory");
 
     // store: segment e = global bytes [dA + 16e, +16) = chunk bytes [16e - head, +16)
-    u32x4 *dA = reinterpret_cast<u32x4 *>(reinterpret_cast<uintptr_t>(dst) - head);
+    gptr_t<u32x4> dA = gbl_at<u32x4>(reinterpret_cast<uintptr_t>(dst) - head);
     const uint32_t nseg = (head + tot + 15) >> 4;
     const uint32_t q0 = OD + (uint32_t)((T - (int32_t)sh) >> 2);  // dword of segment 0
     for (uint32_t e = lane; e < nseg; e += kWave) {
@@ -485,7 +485,7 @@ __device__ bool encode_chunk_gather(const RegionSrc &S, uint64_t c0, uint32_t cn
             o.w = funnel(a.w, a4, sh);
             dA[e] = o;
         } else {
-            uint8_t *db = reinterpret_cast<uint8_t *>(dA + e);
+            gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + e);
             for (uint32_t b = 0; b < 16; b++) {
                 const int32_t u = u0 + (int32_t)b;
                 if (u >= 0 && (uint32_t)u < tot) db[b] = ob[u];
@@ -503,12 +503,6 @@ union EncodeLds {
     ChunkTable ct;
     uint32_t gather[kGatherDwords + kGatherMaskWords];
 };
-union RegionLds {  // V / IDX only: no KV stage
-    ChunkTable ct;
-    uint32_t gather[kGatherDwords + kGatherMaskWords];
-};
-
-
 // Chunk encoder dispatch: DMA gather (V / IDX), LDS-staged (KV), then the
 // global-source fallback for chunks too large for LDS.  The three LDS views
 // alias one per-wave buffer.
@@ -598,7 +592,7 @@ __device__ void store_filter_slice(const Grp &g, const uint32_t *bits, uint64_t 
     const uint64_t len = 8 * (whi - wlo);
     const uintptr_t p0 = reinterpret_cast<uintptr_t>(img_words + 8 * wlo);
     const uint32_t head = (uint32_t)(p0 & 3);
-    uint32_t *dA = reinterpret_cast<uint32_t *>(p0 - head);
+    gptr_t<uint32_t> dA = gbl_at<uint32_t>(p0 - head);
     const uint64_t ndw = (head + len + 3) / 4;
     for (uint64_t d = g.tid(); d < ndw; d += nthr) {
         const int64_t u0 = (int64_t)(4 * d) - head;
@@ -609,7 +603,7 @@ __device__ void store_filter_slice(const Grp &g, const uint32_t *bits, uint64_t 
             const uint32_t hi = sh ? be_dword(bits, q + 1) : 0;
             dA[d] = funnel(lo, hi, sh);
         } else {
-            uint8_t *db = reinterpret_cast<uint8_t *>(dA + d);
+            gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + d);
             for (uint32_t b = 0; b < 4; b++) {
                 const int64_t u = u0 + b;
                 if (u < 0 || (uint64_t)u >= len) continue;
@@ -763,6 +757,9 @@ __device__ void bloom_file_body(Grp &g, const BloomFileArgs &a, uint32_t f, uint
 #pragma unroll
         for (uint32_t c = 0; c < 4; c++) res[c] = mod_small(loc[c], m32, rl, rh);
         const uint32_t d2 = mod_small(st2, m32, rl, rh), d3 = mod_small(st3, m32, rl, rh);
+        // the steps less 2^64 mod m, for a step whose 64-bit add wraps
+        const uint32_t w2 = d2 >= a.c64 ? d2 - a.c64 : d2 + m32 - a.c64;
+        const uint32_t w3 = d3 >= a.c64 ? d3 - a.c64 : d3 + m32 - a.c64;
         for (uint32_t j0 = 0; j0 < a.k; j0 += kBinBatch) {
             uint32_t pp[kBinBatch];
             uint32_t c1 = 0;
@@ -772,15 +769,13 @@ __device__ void bloom_file_body(Grp &g, const BloomFileArgs &a, uint32_t f, uint
                 const bool valid = act && j < a.k;
                 const uint32_t c = jj & 3;  // j0 is a multiple of 4
                 const uint32_t p = res[c];
-                {
+                if (j + 4 < a.k) {  // wave-uniform: the class's next location
                     const bool a2 = c == 0 || c == 3;
-                    const uint64_t nl = loc[c] + (a2 ? st2 : st3);
-                    const bool carry = nl < loc[c];
+                    uint64_t nl;
+                    const bool carry = __builtin_add_overflow(loc[c], a2 ? st2 : st3, &nl);
                     loc[c] = nl;
-                    uint32_t t = res[c] + (a2 ? d2 : d3);
-                    t = min(t, t - m32);
-                    const uint32_t u = t - a.c64;
-                    res[c] = carry ? min(u, u + m32) : t;
+                    const uint32_t t = res[c] + (carry ? (a2 ? w2 : w3) : (a2 ? d2 : d3));
+                    res[c] = min(t, t - m32);
                 }
                 const bool in1 = p >= (uint32_t)lo1;  // lo1 <= m <= 2^30
                 if (valid && !in1) atomicOr(&lds_bits[p >> 5], 1u << (p & 31));
@@ -895,36 +890,230 @@ __device__ __forceinline__ SstLayout sst_layout(const SstArgs &a, uint32_t f) {
 constexpr int kSstWaves = 4;
 constexpr uint32_t kSstChunkRecs = kSstWaves * kWave;  // records per workgroup
 
-// Data region (V grammar) and index region (IDX grammar) of file blockIdx.x,
-// records chunk blockIdx.y.
-constexpr uint32_t kRegWaveRecs = kWave;                   // records per wave
-constexpr uint32_t kRegChunkRecs = kSstWaves * kRegWaveRecs;  // records per workgroup
+// ---- .sst regions: pipelined two-region gather ------------------------------
+//
+// Data region (V grammar, [u32 vlen][value], sstable.go:159-175) and index
+// region (IDX grammar, [u32 klen][key][i64 off], index.go:30-58) of file
+// blockIdx.x.  One wave writes kRegWaveChunks consecutive 64-record chunks.
+// Both region images of a chunk are DMA-gathered into the wave's LDS buffer
+// together (encode_chunk_gather's dword-phase layout, one memory round trip
+// for both), the next chunk's record offsets are loaded while they land, and
+// the chunk's stores are still in flight when the next chunk's gathers are
+// issued.  A chunk whose images do not fit the buffer takes the one-region
+// encoders.
+constexpr uint32_t kRegWaves = 2;         // waves per workgroup
+constexpr uint32_t kRegWaveChunks = 4;    // 64-record chunks per wave
+constexpr uint32_t kRegBufDwords = 2432;  // both images of a chunk (9.5 KiB)
+constexpr uint32_t kRegSpanRecs = kRegWaves * kRegWaveChunks * kWave;  // records per workgroup
+constexpr uint32_t kRegMaxImage = 32 * kGatherMaskWords;  // dwords one mask covers
 
-__global__ __launch_bounds__(256) void sst_regions_kernel(SstArgs a) {
-    __shared__ RegionLds lds[kSstWaves];
+// Per-lane record offsets of a chunk (record c0 + lane): value bounds (V
+// payload, and the IDX offset) and key bounds (IDX payload).
+struct ChunkOffs {
+    uint64_t v0, v1, k0, k1;
+};
+
+__device__ __forceinline__ ChunkOffs load_offs(const SstArgs &a, uint64_t c0, uint32_t cnt) {
+    ChunkOffs o{0, 0, 0, 0};
+    if (lane_id() < cnt) {
+        const uint64_t i = c0 + lane_id();
+        o.v0 = a.voff[i];
+        o.v1 = a.voff[i + 1];
+        o.k0 = a.koff[i];
+        o.k1 = a.koff[i + 1];
+    }
+    return o;
+}
+
+__device__ __forceinline__ uint64_t lane64(uint64_t v, uint32_t l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+}
+
+// One region image of a chunk in the LDS buffer: image dword D (at buffer
+// dword base + OD + D) covers chunk bytes [4D - ph, 4D - ph + 4).
+struct RegionPlan {
+    uint32_t P, len;  // per lane: chunk-relative record start, payload length
+    uint64_t xo;      // per lane: IDX offset
+    uint32_t cnt, tot, ph, head, sh, OD, nD, base, sbytes;  // wave-uniform
+    uint64_t Sc;      // wave-uniform: source offset of the first payload byte
+    uint8_t *dst;
+};
+
+// Lays out region G of the chunk at buffer dword `base`; false if it does not
+// fit below `cap` (or one mask word set does not cover it).
+template <int G>
+__device__ __forceinline__ bool region_plan(RegionPlan &R, const ChunkOffs &o, uint32_t cnt,
+                                            uint8_t *dst, uint32_t base, uint32_t cap,
+                                            int64_t xo_base) {
+    constexpr uint32_t pre = G == LSM_GRAMMAR_V ? 4 : 12;
+    const uint32_t lane = lane_id();
+    const uint64_t p0 = G == LSM_GRAMMAR_V ? o.v0 : o.k0, p1 = G == LSM_GRAMMAR_V ? o.v1 : o.k1;
+    const uint64_t len = lane < cnt ? p1 - p0 : 0;
+    uint64_t tot64;
+    const uint64_t P64 = wave_excl_scan64(lane < cnt ? pre + len : 0, &tot64);
+    tot64 = uni64(tot64);
+    R.cnt = cnt;
+    R.dst = dst;
+    R.base = base;
+    R.Sc = lane64(p0, 0);
+    R.sbytes = 0;
+    if (tot64 + 64 > 4ull * cap) return false;
+    R.len = (uint32_t)len;
+    R.P = (uint32_t)P64;
+    R.tot = (uint32_t)tot64;
+    R.xo = G == LSM_GRAMMAR_IDX ? (uint64_t)(xo_base + (int64_t)(4 * lane) + (int64_t)o.v0) : 0;
+    R.sbytes = uni((uint32_t)(lane64(p1, cnt - 1) - R.Sc));
+    R.ph = (uint32_t)(R.Sc & 3);
+    R.head = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15);
+    R.nD = (R.tot + R.ph + 3) >> 2;
+    const int32_t T = (int32_t)R.ph - (int32_t)R.head;
+    R.sh = (uint32_t)T & 3;
+    R.OD = 8 + (((uint32_t)(-(T - (int32_t)R.sh)) >> 2) & 3);
+    return R.nD <= kRegMaxImage && base + R.OD + ((R.nD + 63) & ~63u) + 8 <= cap;
+}
+
+// Issues the DMA gather of a planned region (see encode_chunk_gather).
+template <int G>
+__device__ __forceinline__ void region_issue(const RegionPlan &R, uint32_t *buf, uint32_t *mask,
+                                             const uint8_t *sbase) {
+    constexpr uint32_t pre = G == LSM_GRAMMAR_V ? 4 : 12;
+    const uint32_t lane = lane_id();
+    mask[lane] = 0;  // kGatherMaskWords == kWave
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    if (lane >= 1 && lane < R.cnt) {
+        const uint32_t et = (R.P + R.ph + 3) >> 2;
+        atomicOr(&mask[et >> 5], 1u << (et & 31));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    const uint32_t mv = mask[lane];
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    const rsrc_t rs = make_rsrc(sbase + (R.Sc - R.ph), uni((R.sbytes + R.ph + 3) & ~3u));
+    uint32_t rb = 0;
+    for (uint32_t i = 0; i * kWave < R.nD; i++) {
+        const int32_t x0 = 256 * (int32_t)i + 4 * (int32_t)lane - (int32_t)R.ph;
+        const uint64_t M = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(mv, 2 * i + 1) << 32 |
+                           (uint32_t)__builtin_amdgcn_readlane(mv, 2 * i);
+        const uint32_t r = rb + mbcnt(M) + (uint32_t)((M >> lane) & 1);
+        rb += (uint32_t)__builtin_popcountll(M);
+        const uint32_t voff = (uint32_t)(x0 - (int32_t)(pre * r) - 4 + (int32_t)R.ph);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void *)&buf[R.base + R.OD + i * kWave], 4, voff,
+            0, 0, 2);
+    }
+}
+
+// After the gather landed: the fixed fields, then the aligned 16-byte stores
+// (chunk-edge segments by dwords where whole and bytes at the ends).
+template <int G>
+__device__ __forceinline__ void region_finish(const RegionPlan &R, uint32_t *buf) {
+    const uint32_t lane = lane_id();
+    uint8_t *ob = reinterpret_cast<uint8_t *>(buf + R.base + R.OD) + R.ph;
+    if (lane < R.cnt) {
+#pragma unroll
+        for (uint32_t b = 0; b < 4; b++) ob[R.P + b] = (uint8_t)(R.len >> (8 * b));
+        if (G == LSM_GRAMMAR_IDX) {
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) ob[R.P + 4 + R.len + b] = (uint8_t)(R.xo >> (8 * b));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+    gptr_t<u32x4> dA = gbl_at<u32x4>(reinterpret_cast<uintptr_t>(R.dst) - R.head);
+    const uint32_t nseg = (R.head + R.tot + 15) >> 4;
+    const uint32_t *img = buf + R.base;
+    const uint32_t q0 = R.OD + (uint32_t)(((int32_t)R.ph - (int32_t)R.head - (int32_t)R.sh) >> 2);
+    const int32_t tot = (int32_t)R.tot;
+    for (uint32_t e = lane; e < nseg; e += kWave) {
+        const int32_t u0 = 16 * (int32_t)e - (int32_t)R.head;
+        if (u0 >= 0 && u0 + 16 <= tot) {
+            const uint32_t q = q0 + 4 * e;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(&img[q]);
+            const uint32_t v4 = img[q + 4];
+            u32x4 o;
+            o.x = funnel(v.x, v.y, R.sh);
+            o.y = funnel(v.y, v.z, R.sh);
+            o.z = funnel(v.z, v.w, R.sh);
+            o.w = funnel(v.w, v4, R.sh);
+            dA[e] = o;
+        } else {
+            gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + e);
+            for (uint32_t k = 0; k < 4; k++) {
+                const int32_t u = u0 + 4 * (int32_t)k;
+                if (u >= 0 && u + 4 <= tot) {
+                    const uint32_t q = q0 + 4 * e + k;
+                    *(gptr_t<uint32_t>)(db + 4 * k) = funnel(img[q], img[q + 1], R.sh);
+                } else {
+                    for (uint32_t b = 0; b < 4; b++)
+                        if (u + (int32_t)b >= 0 && u + (int32_t)b < tot) db[4 * k + b] = ob[u + b];
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ __volatile__("" ::: "memory");
+}
+
+__global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kRegWaves][kRegBufDwords + kGatherMaskWords];
     const uint32_t f = blockIdx.x;
     const SstLayout L = sst_layout(a, f);
     const uint32_t wave = uni(threadIdx.x / kWave);
-    const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kRegChunkRecs + (uint64_t)wave * kRegWaveRecs;
+    uint64_t c0 = L.s + (uint64_t)blockIdx.y * kRegSpanRecs + (uint64_t)wave * kRegWaveChunks * kWave;
     if (c0 >= L.e) return;
-    const uint32_t cnt =
-        (uint32_t)((L.e - c0) < (uint64_t)kRegWaveRecs ? (L.e - c0) : kRegWaveRecs);
+    const uint64_t cend = L.e - c0 < (uint64_t)kRegWaveChunks * kWave ? L.e : c0 + kRegWaveChunks * kWave;
+    uint32_t *buf = lds[wave];
+    uint32_t *mask = buf + kRegBufDwords;
     uint8_t *img = a.out + uni64(a.file_off[f]);
     const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
-    const uint64_t Kc = uni64(a.koff[c0]), Vc = uni64(a.voff[c0]);
-    RegionSrc S;
-    S.keys = a.keys; S.koff = a.koff; S.vals = a.vals; S.voff = a.voff;
-    S.idx_off = nullptr;
-    S.idx_base = (int64_t)L.data_off;
-    S.rs = L.s;
-    S.vrs = Vs;
-    if (!a.skip_v)
-        encode_chunk_any<LSM_GRAMMAR_V>(
-            S, c0, cnt, img + L.data_off + 4 * (c0 - L.s) + (Vc - Vs), lds[wave].gather, nullptr,
-            &lds[wave].ct);
-    encode_chunk_any<LSM_GRAMMAR_IDX>(
-        S, c0, cnt, img + L.idx_off + 12 * (c0 - L.s) + (Kc - Ks), lds[wave].gather, nullptr,
-        &lds[wave].ct);
+    auto count = [&](uint64_t c) { return (uint32_t)(cend - c < (uint64_t)kWave ? cend - c : kWave); };
+    ChunkOffs off = load_offs(a, c0, count(c0));
+    for (;;) {
+        const uint32_t cnt = count(c0);
+        const uint64_t rel = c0 - L.s;
+        const uint64_t Vc = lane64(off.v0, 0), Kc = lane64(off.k0, 0);
+        uint8_t *dV = img + L.data_off + 4 * rel + (Vc - Vs);
+        uint8_t *dI = img + L.idx_off + 12 * rel + (Kc - Ks);
+        // IDX offset of record i: data_off + 4 (i - s) + V(i) - V(s) (sstable.go:164-175)
+        const int64_t xo_base = (int64_t)L.data_off + (int64_t)(4 * rel) - (int64_t)Vs;
+        RegionPlan pv, pi;
+        bool ok = true;
+        uint32_t ibase = 0;
+        if (!a.skip_v) {
+            ok = region_plan<LSM_GRAMMAR_V>(pv, off, cnt, dV, 0, kRegBufDwords, 0);
+            ibase = (pv.OD + pv.nD + 8 + 63) & ~63u;
+        }
+        ok = ok && region_plan<LSM_GRAMMAR_IDX>(pi, off, cnt, dI, ibase, kRegBufDwords, xo_base);
+        const uint64_t cn = c0 + kWave;
+        const bool more = cn < cend;
+        if (ok) {
+            if (!a.skip_v) region_issue<LSM_GRAMMAR_V>(pv, buf, mask, a.vals);
+            region_issue<LSM_GRAMMAR_IDX>(pi, buf, mask, a.keys);
+            const ChunkOffs nxt = more ? load_offs(a, cn, count(cn)) : off;
+            // The DMA writes are invisible to the compiler's LDS tracking.
+            __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!a.skip_v) region_finish<LSM_GRAMMAR_V>(pv, buf);
+            region_finish<LSM_GRAMMAR_IDX>(pi, buf);
+            off = nxt;
+        } else {
+            // a chunk with records too large for one buffer: region by region
+            RegionSrc S;
+            S.keys = a.keys; S.koff = a.koff; S.vals = a.vals; S.voff = a.voff;
+            S.idx_off = nullptr;
+            S.idx_base = (int64_t)L.data_off;
+            S.rs = L.s;
+            S.vrs = Vs;
+            ChunkTable *ct = reinterpret_cast<ChunkTable *>(buf);
+            if (!a.skip_v) encode_chunk_any<LSM_GRAMMAR_V, kRegMaxImage>(S, c0, cnt, dV, buf, nullptr, ct);
+            encode_chunk_any<LSM_GRAMMAR_IDX, kRegMaxImage>(S, c0, cnt, dI, buf, nullptr, ct);
+            if (more) off = load_offs(a, cn, count(cn));
+        }
+        if (!more) break;
+        c0 = cn;
+    }
 }
 
 // Data region (V grammar, sstable.go:159-175) of file blockIdx.x straight
@@ -945,7 +1134,7 @@ constexpr uint32_t kVvMap = 1024;
 
 __device__ __forceinline__ uint32_t ld_any32(const uint8_t *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const gptr_t<const uint32_t> q = gbl_at<const uint32_t>(a & ~(uintptr_t)3);
     return funnel(q[0], q[1], (uint32_t)a);
 }
 
@@ -995,7 +1184,8 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
     vv_sync();
     const uint64_t A = s_dst[w][0], B = s_dst[w][cnt], X = A & ~(uint64_t)15;
     const uint64_t nch = (B - X + 15) / 16;
-    uint8_t *out = a.out;
+    const gptr_t<uint8_t> out = gbl(a.out);
+    const gptr_t<const uint8_t> vb = gbl(v.bytes);
     for (uint64_t P = 0; P < nch; P += kVvMap) {
         const uint32_t np = (uint32_t)(nch - P < kVvMap ? nch - P : kVvMap);
         // 1. chunks whose first byte lies in my record
@@ -1019,7 +1209,7 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
                 if (x >= e0 && x + 16 <= e1) {
                     regular = true;
                     const uintptr_t sa = reinterpret_cast<uintptr_t>(v.bytes + s_src[w][r] + (x - e0));
-                    const uint32_t *q = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+                    const gptr_t<const uint32_t> q = gbl_at<const uint32_t>(sa & ~(uintptr_t)3);
                     const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
                     const uint32_t sh = (uint32_t)sa;
                     u32x4 o;
@@ -1027,7 +1217,7 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
                     o.y = funnel(q1, q2, sh);
                     o.z = funnel(q2, q3, sh);
                     o.w = funnel(q3, q4, sh);
-                    *reinterpret_cast<u32x4 *>(out + x) = o;
+                    *(gptr_t<u32x4>)(out + x) = o;
                 }
             }
             const bool irr = c < np && !regular;
@@ -1047,7 +1237,7 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
             while (r + 1 < cnt && xd >= s_dst[w][r + 1]) r++;
             const uint64_t e0 = s_dst[w][r] + 4;
             if (xd >= A && xd + 4 <= B && xd >= e0 && xd + 4 <= s_dst[w][r + 1]) {
-                *reinterpret_cast<uint32_t *>(out + xd) = ld_any32(v.bytes + s_src[w][r] + (xd - e0));
+                *(gptr_t<uint32_t>)(out + xd) = ld_any32(v.bytes + s_src[w][r] + (xd - e0));
             } else {
                 for (uint32_t u = 0; u < 4; u++) {
                     const uint64_t b = xd + u;
@@ -1055,7 +1245,7 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
                     while (b >= s_dst[w][r + 1]) r++;
                     const uint64_t t = b - s_dst[w][r];  // byte t of record r
                     out[b] = t < 4 ? (uint8_t)(s_vl[w][r] >> (8 * t))
-                                   : v.bytes[s_src[w][r] + (t - 4)];
+                                   : vb[s_src[w][r] + (t - 4)];
                 }
             }
         }
@@ -1624,7 +1814,7 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     }
     __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const uint8_t *lb = fbytes + delta;
+    const uint8_t *lb = fbytes + delta;  // LDS
     const bool small = F.m <= (1ull << 30);
     const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
     while (t < b1) {
@@ -1654,7 +1844,7 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
                         const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
                         uint32_t byte;
                         if (q < in_lds) byte = lb[q];
-                        else byte = src[q];  // the tail past the LDS copy, from L2
+                        else byte = gbl(src)[q];  // the tail past the LDS copy, from L2
                         bits &= byte >> (p & 7);
                     }
                 }
@@ -1888,8 +2078,8 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
 
     hipStream_t rs = forked ? ctx->side : s;  // the regions' stream
     if (chunks) {
-        const uint32_t rchunks = (max_file_records + kRegChunkRecs - 1) / kRegChunkRecs;
-        hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rchunks), dim3(256), 0, rs, a);
+        const uint32_t rspans = (max_file_records + kRegSpanRecs - 1) / kRegSpanRecs;
+        hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
         LSM_HIP_CHECK(hipGetLastError());
         if (views) {
             hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, rs, a,

@@ -87,7 +87,7 @@ __device__ __forceinline__ View view(const MergeIn &m, uint32_t i) {
 // and keys and values sit at rec_off + 4 or later).
 __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const gptr_t<const uint32_t> q = gbl_at<const uint32_t>(a & ~(uintptr_t)3);
     return funnel(q[0], q[1], (uint32_t)a);
 }
 
@@ -621,7 +621,8 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
         nc[h] = B[h] > A[h] ? (uint32_t)((B[h] - X[h] + 15) / 16) : 0;
     }
     if (!vals) nc[1] = 0;  // keys only (lsm_build_sst_views reads the values in place)
-    uint8_t *const dsts[2] = {keys, vals};
+    const gptr_t<uint8_t> dsts[2] = {gbl(keys), gbl(vals)};
+    const gptr_t<const uint8_t> src = gbl(m.bytes);
     const uint32_t total = nc[0] + nc[1];
     for (uint32_t P = 0; P < total; P += kMapChunks) {
         const uint32_t np = total - P < kMapChunks ? total - P : kMapChunks;
@@ -642,7 +643,7 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
         for (uint32_t c0 = 0; c0 < np; c0 += kUnroll * kWave) {
             uint32_t q[kUnroll][5];
             uint32_t sh[kUnroll];
-            uint8_t *out[kUnroll];
+            gptr_t<uint8_t> out[kUnroll];
             bool reg[kUnroll];
 #pragma unroll
             for (uint32_t u = 0; u < kUnroll; u++) {
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
                             reg[u] = true;
                             const uintptr_t sa =
                                 reinterpret_cast<uintptr_t>(m.bytes + s_src[w][h][r] + (x - e0));
-                            const uint32_t *qa = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+                            const gptr_t<const uint32_t> qa = gbl_at<const uint32_t>(sa & ~(uintptr_t)3);
                             sh[u] = (uint32_t)sa;
                             out[u] = dsts[h] + x;
 #pragma unroll
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
                     o.y = funnel(q[u][1], q[u][2], sh[u]);
                     o.z = funnel(q[u][2], q[u][3], sh[u]);
                     o.w = funnel(q[u][3], q[u][4], sh[u]);
-                    *reinterpret_cast<u32x4 *>(out[u]) = o;
+                    *(gptr_t<u32x4>)out[u] = o;
                 }
                 const uint32_t c = c0 + u * kWave + lane;
                 const bool irr = c < np && !reg[u];
@@ -700,16 +701,16 @@ __global__ __launch_bounds__(kMergeThreads) void gather_copy_kernel(
             uint32_t r = x >= A[h] ? s_map[w][c] : 0;
             const uint64_t *sd = s_dst[w][h];
             const uint64_t *ss = s_src[w][h];
-            uint8_t *dst = dsts[h];
+            const gptr_t<uint8_t> dst = dsts[h];
             while (r + 1 < cnt && xd >= sd[r + 1]) r++;
             if (xd >= A[h] && xd + 4 <= B[h] && xd >= sd[r] && xd + 4 <= sd[r + 1]) {
-                *reinterpret_cast<uint32_t *>(dst + xd) = ld_u32_any(m.bytes + ss[r] + (xd - sd[r]));
+                *(gptr_t<uint32_t>)(dst + xd) = ld_u32_any(m.bytes + ss[r] + (xd - sd[r]));
             } else {
                 for (uint32_t u = 0; u < 4; u++) {
                     const uint64_t b = xd + u;
                     if (b < A[h] || b >= B[h]) continue;
                     while (b >= sd[r + 1]) r++;
-                    dst[b] = m.bytes[ss[r] + (b - sd[r])];
+                    dst[b] = src[ss[r] + (b - sd[r])];
                 }
             }
         }

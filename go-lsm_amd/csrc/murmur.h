@@ -50,13 +50,13 @@ __device__ __forceinline__ void mmh3_final(uint64_t h1, uint64_t h2, uint64_t k1
 // Requires the 4 bytes past p+3 to be readable (16-byte padded arenas).
 __device__ __forceinline__ uint32_t ldg_u32_unaligned(const uint8_t *p) {
     uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const gptr_t<const uint32_t> w = gbl_at<const uint32_t>(a & ~(uintptr_t)3);
     return funnel(w[0], w[1], (uint32_t)a);
 }
 
 __device__ __forceinline__ uint64_t ldg_u64_unaligned(const uint8_t *p) {
     uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const gptr_t<const uint32_t> w = gbl_at<const uint32_t>(a & ~(uintptr_t)3);
     uint32_t s = (uint32_t)a;
     uint32_t x0 = w[0], x1 = w[1], x2 = w[2];
     return (uint64_t)funnel(x1, x2, s) << 32 | funnel(x0, x1, s);

@@ -8,7 +8,7 @@ i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS" \
            "SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUTD/p$i -o run -- python bench.py ${BENCH_ARGS:---config $CFG} --steps 3 --warmup 1 --no-cpu-baseline > $OUTD/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUTD/p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUTD/p$i -o run -- python ${PYCMD:-bench.py} ${BENCH_ARGS:---config $CFG} --steps 3 --warmup 1 --no-cpu-baseline > $OUTD/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUTD/p$i.log; exit 1; }
 done
 OUTD=$OUTD KF=$KF python - <<'PY'
 import csv, glob, collections, os
