@@ -269,17 +269,30 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
                                                uint32_t cnt) {
     const uint32_t T = cnt * L;  // <= the ring: a run lies inside the landed bytes
     if (T == 0) return;
+    const uint32_t lane = lane_id();
+    // full-rate 24-bit products (v_mul_u32_u24): every operand here is < 2^24
+    auto mul24 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFFFu) * (y & 0xFFFFFFu); };
+    if (((src0 | S | L | (uint32_t)(uintptr_t)out) & 3) == 0) {
+        // dword-aligned run: output dword j is ring dword src0/4 + j + r*(S-L)/4
+        // with r = floor(j / (L/4)) -- one ring read and one store per dword
+        const uint32_t L4 = L >> 2, G4 = (S - L) >> 2, w0 = src0 >> 2, nd = T >> 2;
+        const float inv4 = 1.0f / (float)L4, hinv4 = 0.5f * inv4;
+        uint32_t *a0 = reinterpret_cast<uint32_t *>(out);
+#pragma unroll 1
+        for (uint32_t j = lane; j < nd; j += kWave) {
+            const uint32_t r = (uint32_t)__builtin_fmaf((float)j, inv4, hinv4);
+            a0[j] = rb.word(w0 + j + mul24(r, G4));
+        }
+        return;
+    }
     const uint32_t lead = (uint32_t)((uintptr_t)out & 3);
     uint32_t *a0 = reinterpret_cast<uint32_t *>(out - lead);
     const uint32_t nd = (lead + T + 3) >> 2;
-    // full-rate 24-bit products (v_mul_u32_u24): every operand here is < 2^24
-    auto mul24 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFFFu) * (y & 0xFFFFFFu); };
     const float inv = 1.0f / (float)L, hinv = 0.5f * inv;  // once per run
     auto rec = [&](uint32_t q) -> uint32_t {  // floor(q / L), q < 2^16
         return (uint32_t)__builtin_fmaf((float)q, inv, hinv);
     };
     constexpr uint32_t U = 1;  // dwords per lane per step (2 and 4 measured no faster)
-    const uint32_t lane = lane_id();
 #pragma unroll 1
     for (uint32_t w0 = 0; w0 < nd; w0 += U * kWave) {
         uint32_t W[U], sb[U], kk[U], rr[U];
