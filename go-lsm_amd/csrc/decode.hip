@@ -276,12 +276,23 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
         // dword-aligned run: output dword j is ring dword src0/4 + j + r*(S-L)/4
         // with r = floor(j / (L/4)) -- one ring read and one store per dword
         const uint32_t L4 = L >> 2, G4 = (S - L) >> 2, w0 = src0 >> 2, nd = T >> 2;
-        const float inv4 = 1.0f / (float)L4, hinv4 = 0.5f * inv4;
+        // floor((j + 1/2) * rcp(L4)) is exact for j < 2^16: the quotient is at
+        // least 1/(2 L4) from an integer, the error below 2^-6 / L4
+        const float inv4 = __builtin_amdgcn_rcpf((float)L4), hinv4 = 0.5f * inv4;
         uint32_t *a0 = reinterpret_cast<uint32_t *>(out);
+        constexpr uint32_t V = 4;  // ring reads in flight per lane
 #pragma unroll 1
-        for (uint32_t j = lane; j < nd; j += kWave) {
-            const uint32_t r = (uint32_t)__builtin_fmaf((float)j, inv4, hinv4);
-            a0[j] = rb.word(w0 + j + mul24(r, G4));
+        for (uint32_t j0 = lane; j0 < nd; j0 += V * kWave) {
+            uint32_t v[V];
+#pragma unroll
+            for (uint32_t t = 0; t < V; t++) {  // past nd: harmless ring bytes
+                const uint32_t j = j0 + t * kWave;
+                const uint32_t r = (uint32_t)__builtin_fmaf((float)j, inv4, hinv4);
+                v[t] = rb.word(w0 + j + __umul24(r, G4));
+            }
+#pragma unroll
+            for (uint32_t t = 0; t < V; t++)
+                if (j0 + t * kWave < nd) a0[j0 + t * kWave] = v[t];
         }
         return;
     }
