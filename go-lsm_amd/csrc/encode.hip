@@ -845,6 +845,142 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
     bloom_file_body(g, a, blockIdx.x, lds_bits, n1);
 }
 
+// ---- split bloom build: hash everywhere, then OR per slice (k <= 16) --------
+//
+// bloom_file_kernel pins one 1024-thread workgroup and 100 KiB of LDS per
+// filter to a CU for the whole hash, so beside the region writers it runs on
+// 208 CUs with LDS to spare for only a few region waves.  The split build
+// hashes every key once with no LDS at all (bloom_hash_kernel, any CU, beside
+// the region writers), leaving per key the residues mod m of the four
+// location classes and of the two class steps (location(j) = h[j%2] +
+// j*h[2 + ((j + j%2) % 4)/2], bloom.go:133-136: class c = j%4 is an
+// arithmetic progression) plus the carry bit of each 64-bit step, 24 bytes;
+// bloom_or_kernel then rebuilds the k locations of every key of its filter
+// from them (additions only) and ORs those of its slice into LDS.
+constexpr uint32_t kHashRecDwords = 6;
+constexpr uint32_t kSplitMaxK = 16;  // three carries per class fit the record
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct BloomHashArgs {
+    const uint8_t *keys;
+    const uint64_t *koff;
+    const uint64_t *file_start;  // keys [file_start[0], file_start[nfile])
+    uint32_t nfile;
+    uint32_t m, rl, rh;
+    uint32_t *rec;     // kHashRecDwords per key, key file_start[0] first
+};
+
+__global__ __launch_bounds__(256) void bloom_hash_kernel(BloomHashArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k0 = uni64(a.file_start[0]);
+    if (t >= uni64(a.file_start[a.nfile]) - k0) return;
+    const uint64_t i = k0 + t;
+    const uint64_t ko = a.koff[i], kl = a.koff[i + 1] - ko;
+    uint64_t h[4];
+    sum256_pre(a.keys + ko, kl, ldg_u64_unaligned(a.keys + ko), ldg_u64_unaligned(a.keys + ko + 8), h);
+    uint64_t loc[4] = {h[0], h[1] + h[3], h[0] + (h[3] << 1), h[1] + h[2] + (h[2] << 1)};
+    const uint64_t st2 = h[2] << 2, st3 = h[3] << 2;
+    uint32_t r[6];
+    uint32_t cy = 0;  // bit 3c + n - 1: the step to location 4n + c carries
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {
+        r[c] = mod_small(loc[c], a.m, a.rl, a.rh);
+        const uint64_t st = (c == 0 || c == 3) ? st2 : st3;
+        uint64_t l = loc[c];
+#pragma unroll
+        for (uint32_t n = 0; n < 3; n++) {
+            uint64_t nl;
+            cy |= (uint32_t)__builtin_add_overflow(l, st, &nl) << (3 * c + n);
+            l = nl;
+        }
+    }
+    r[4] = mod_small(st2, a.m, a.rl, a.rh);
+    r[5] = mod_small(st3, a.m, a.rl, a.rh);
+    // residues are < m <= 2^30: two carry bits ride in the top of each dword
+#pragma unroll
+    for (uint32_t d = 0; d < 6; d++) r[d] |= ((cy >> (2 * d)) & 3u) << 30;
+    gptr_t<uint32_t> o = gbl(a.rec + kHashRecDwords * t);
+    *(gptr_t<u32x4>)o = u32x4{r[0], r[1], r[2], r[3]};
+    *(gptr_t<u32x2>)(o + 4) = u32x2{r[4], r[5]};
+}
+
+struct BloomOrArgs {
+    const uint64_t *file_start;  // rec[0] is key file_start[0]
+    const uint32_t *rec;
+    uint32_t m, k, c64;
+    uint32_t split;     // slice 0 = bits [0, split), slice 1 = [split, m)
+    uint64_t nwords;
+    const uint64_t *koff;
+    uint8_t *out;
+    const uint64_t *file_off;
+};
+
+// Filter blockIdx.x, slice blockIdx.y: every key's k locations rebuilt from
+// its record, the slice's bits ORed in LDS, then stored big-endian into the
+// image.  (One workgroup per filter holding 152 KiB and listing the rest was
+// measured slower: the ORs are bound by LDS atomic throughput, about 1.4
+// lanes per clock per CU for scattered words, not by the rebuild.)
+__global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    const uint32_t f = blockIdx.x, sl = blockIdx.y;
+    const uint32_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
+    const uint32_t nw = (hi - lo + 63) / 64 * 2;
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_bits[i] = 0;
+    __syncthreads();
+    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
+    const uint32_t m = a.m, c64 = a.c64;
+    const uint64_t k0 = uni64(a.file_start[0]);
+    // records two rounds ahead in flight (indices past the filter clamped;
+    // a filter without keys loads nothing and stores its zero words)
+    const gptr_t<const uint32_t> rec = gbl(a.rec);
+    auto ld = [&](uint64_t i, u32x4 &x, u32x2 &y) {
+        const uint64_t j = (i < e ? i : e - 1) - k0;
+        x = *(gptr_t<const u32x4>)(rec + kHashRecDwords * j);
+        y = *(gptr_t<const u32x2>)(rec + kHashRecDwords * j + 4);
+    };
+    u32x4 xa, xb;
+    u32x2 ya, yb;
+    if (e > s) {
+        ld(s + threadIdx.x, xa, ya);
+        ld(s + threadIdx.x + blockDim.x, xb, yb);
+    }
+    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const u32x4 x = xa;
+        const u32x2 y = ya;
+        xa = xb;
+        ya = yb;
+        ld(i + 2 * blockDim.x, xb, yb);
+        const uint32_t raw[6] = {x.x, x.y, x.z, x.w, y.x, y.y};
+        uint32_t cy = 0, r[4];
+#pragma unroll
+        for (uint32_t d = 0; d < 6; d++) cy |= (raw[d] >> 30) << (2 * d);
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) r[c] = raw[c] & 0x3FFFFFFFu;
+        const uint32_t d2 = raw[4] & 0x3FFFFFFFu, d3 = raw[5] & 0x3FFFFFFFu;
+        // a step whose 64-bit add wraps loses 2^64: its residue less 2^64 mod m
+        const uint32_t w2 = d2 >= c64 ? d2 - c64 : d2 + m - c64;
+        const uint32_t w3 = d3 >= c64 ? d3 - c64 : d3 + m - c64;
+#pragma unroll
+        for (uint32_t j = 0; j < kSplitMaxK; j++) {
+            const uint32_t c = j & 3, n = j >> 2;  // compile-time: r[] stays in registers
+            if (j >= a.k) continue;                 // wave-uniform
+            const uint32_t p = r[c];
+            if (p >= lo && p < hi) atomicOr(&lds_bits[(p - lo) >> 5], 1u << ((p - lo) & 31));
+            if (n < 3) {
+                const bool a2 = c == 0 || c == 3;
+                const bool carry = (cy >> (3 * c + n)) & 1;
+                const uint32_t t = p + (carry ? (a2 ? w2 : w3) : (a2 ? d2 : d3));
+                r[c] = min(t, t - m);
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t hdr = sst_header_bytes(a.koff, s, e);
+    store_filter_slice(WgGroup{}, lds_bits, lo / 64, sl ? a.nwords : (uint64_t)(hi + 63) / 64,
+                       a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+}
+
 // ---- .sst image writer ------------------------------------------------------
 
 struct SstArgs {
@@ -1982,12 +2118,18 @@ static uint32_t bloom_slices(uint64_t m) {
     return (uint32_t)((m + sb - 1) / sb);
 }
 static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slices(m) <= 2; }
+// two slices and k <= 16: the split build (bloom_hash_kernel + bloom_or_kernel)
+static bool split_bloom(uint64_t m, uint32_t k) {
+    return hash_once_bloom(m) && bloom_slices(m) == 2 && k <= kSplitMaxK;
+}
 
 extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
                                                 uint64_t m, uint32_t k) {
     // the slice-1 position lists of the two-slice hash-once filter
     if (!hash_once_bloom(m) || bloom_slices(m) < 2) return 16;
     const uint64_t kk = k ? k : 1;
+    if (split_bloom(m, (uint32_t)kk))  // a hash record per key
+        return (size_t)(4ull * kHashRecDwords * nfile * (uint64_t)max_file_records + 16);
     return (size_t)(kk * nfile * (uint64_t)max_file_records * 4 + 16);
 }
 
@@ -2025,11 +2167,44 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
 
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
-    bool forked = false;
+    bool forked = false, split = false;
+    BloomOrArgs bo{};
     if (hash_once_bloom(m)) {
         const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
         if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
-        {
+        if (split_bloom(m, kk)) {
+            // the hash beside the regions (no LDS); the per-slice ORs after it
+            // on the caller's stream, launched below behind the regions
+            const uint64_t mr = barrett_recip(m);
+            BloomHashArgs h;
+            h.keys = d_keys;
+            h.koff = d_koff;
+            h.file_start = d_file_start;
+            h.nfile = nfile;
+            h.m = (uint32_t)m;
+            h.rl = (uint32_t)mr;
+            h.rh = (uint32_t)(mr >> 32);
+            h.rec = static_cast<uint32_t *>(d_workspace);
+            const uint64_t nmax = (uint64_t)nfile * max_file_records;
+            LSM_HIP_CHECK(hipEventRecord(ctx->fork, s));
+            LSM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->fork, 0));
+            if (nmax) {
+                hipLaunchKernelGGL(bloom_hash_kernel, dim3((uint32_t)((nmax + 255) / 256)), dim3(256), 0,
+                                   s, h);
+                LSM_HIP_CHECK(hipGetLastError());
+            }
+            bo.file_start = d_file_start;
+            bo.rec = h.rec;
+            bo.m = (uint32_t)m;
+            bo.k = kk;
+            bo.c64 = (uint32_t)((~0ull % m + 1) % m);
+            bo.split = (uint32_t)sb;
+            bo.nwords = nwords;
+            bo.koff = d_koff;
+            bo.out = d_out;
+            bo.file_off = d_file_off;
+            forked = split = true;
+        } else {
             BloomFileArgs b;
             b.keys = d_keys;
             b.koff = d_koff;
@@ -2089,6 +2264,10 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     }
     hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, rs, a);
     LSM_HIP_CHECK(hipGetLastError());
+    if (split) {
+        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo);
+        LSM_HIP_CHECK(hipGetLastError());
+    }
     if (forked) {  // join: the caller's stream waits for the regions
         LSM_HIP_CHECK(hipEventRecord(ctx->join, ctx->side));
         LSM_HIP_CHECK(hipStreamWaitEvent(s, ctx->join, 0));
