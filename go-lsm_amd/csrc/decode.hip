@@ -27,16 +27,6 @@ constexpr uint32_t kRingChunks = 8;  // 8 KiB ring: 4 KiB blocks fit whole, 64 K
 // 80.5 -> 71.7 us for decode4k's memory pattern (tools/block_probe.py).
 constexpr int kBlockLoadAux = 2;
 
-#ifdef LSM_STAMPS
-// Diagnostic build only (liblsm_gpu_stamps.so): per-workgroup s_memrealtime
-// stamps {start, DMA landed, chase done, end} into a buffer of their own.
-__device__ uint64_t *g_stamps;
-__device__ __forceinline__ void stamp(uint32_t k) {
-    if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
-}
-#else
-__device__ __forceinline__ void stamp(uint32_t) {}
-#endif
 
 struct DecodeArgs {
     const uint8_t *in;
@@ -633,7 +623,6 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
             }
         }
         if (++ns == kWave) flush();
-        if (nr == 0) stamp(1);
         nr++;
         pos += S;
 
@@ -817,7 +806,6 @@ __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
     __shared__ uint32_t tab[ARENA ? 129 : 1];
     const uint32_t b = blockIdx.x;
-    stamp(0);
     const uint64_t off = uni64(a.blk_off[b]);
     const uint32_t n = uni(a.blk_len[b]);
     const bool lin = ((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk;
@@ -831,7 +819,6 @@ __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     } else {
         decode_block_v2<G, NCH, false, false>(a, b, ring, tab, off, n);
     }
-    stamp(3);
 }
 
 // ---- planning: exclusive scans over per-block quantities -----------------
@@ -1929,9 +1916,3 @@ extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t
     return 0;
 }
 
-#ifdef LSM_STAMPS
-extern "C" int lsm_debug_set_stamps(void *d_buf) {
-    LSM_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(lsm::g_stamps), &d_buf, sizeof(void *)));
-    return 0;
-}
-#endif
