@@ -234,12 +234,16 @@ def bench_decode(args, world, rank, local):
 
     wal_max = int(blk_len.max()) if args.config == "wal" else 0
     wal_ws = lsmgpu.wal_workspace(ctx, nblk, wal_max) if args.config == "wal" else None
+    # a batch of mixed block sizes goes through lsm_decode_blocks_scheduled
+    # (largest first, the bucketing inside every timed call)
+    sched = lsmgpu.schedule_workspace(ctx, nblk) if args.config == "mixed" else None
 
     def step():
         if args.config == "wal":
             lsmgpu.wal_replay_into(ctx, d_in, d_off, d_len, wal_max, r, wal_ws, stream=stream)
         else:
-            lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream)
+            lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream,
+                               schedule=sched)
 
     for _ in range(args.warmup):
         step()
@@ -310,6 +314,8 @@ def bench_decode(args, world, rank, local):
         "roofline": {
             "bound": "hbm",
             "kernel": ("lsm_wal_replay (seg + stitch + compact launches)" if args.config == "wal"
+                       else "lsm_decode_blocks_scheduled (size-class bucketing + "
+                            "decode_v2_kernel<KV,8>, all launches)" if args.config == "mixed"
                        else "decode_v2_kernel<KV,8,ARENA>" if args.arena
                        else "decode_v2_kernel<KV,8>"),
             "achieved": round(achieved, 1),

@@ -8,7 +8,7 @@ from .codec import (  # noqa: F401
     DEFAULT_BLOOM_K, DEFAULT_BLOOM_M, DESC_DTYPE, GRAMMAR_IDX, GRAMMAR_KV, GRAMMAR_V,
     MAX_SSTABLE_SIZE, STATUS_NAMES, Context, DenseRecords, alloc_decode, alloc_decode_offset,
     alloc_dense, batch_to_device, bloom_probe, build_sst, build_sst_into, compact_into,
-    decode_blocks, decode_into, encode_blocks, pad16, plan, prepare_sst, replan, segment_files,
+    decode_blocks, decode_into, schedule_workspace, encode_blocks, pad16, plan, prepare_sst, replan, segment_files,
     sum256, to_device_bytes, SST_META_DTYPE, SST_STAGE_NAMES, SstDecode, alloc_sst_decode,
     decode_sst, decode_sst_into, wal_replay, wal_replay_into, wal_workspace,
     may_contain, may_contain_into, may_contain_workspace, Merge, alloc_merge, merge_kvs, merge_kvs_into, gather_kvs,

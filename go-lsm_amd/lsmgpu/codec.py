@@ -231,12 +231,26 @@ def _decode_out(r: DecodeResult):
 
 
 def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,
-                blk_len: torch.Tensor, r: DecodeResult, stream=None) -> None:
-    """lsm_decode_blocks into preallocated outputs (asynchronous)."""
+                blk_len: torch.Tensor, r: DecodeResult, stream=None,
+                schedule: Optional[torch.Tensor] = None) -> None:
+    """lsm_decode_blocks into preallocated outputs (asynchronous).  With a
+    `schedule` workspace (schedule_workspace()): lsm_decode_blocks_scheduled,
+    the blocks launched largest first (for batches whose sizes vary)."""
     out = _decode_out(r)
+    if schedule is not None:
+        _lib.check(ctx.lib.lsm_decode_blocks_scheduled(
+            ctx.handle, grammar, _ptr(d_in), _ptr(blk_off), _ptr(blk_len), int(blk_off.numel()),
+            ctypes.byref(out), _ptr(schedule), schedule.numel(), _stream_handle(stream)),
+            "lsm_decode_blocks_scheduled")
+        return
     _lib.check(ctx.lib.lsm_decode_blocks(ctx.handle, grammar, _ptr(d_in), _ptr(blk_off),
                                          _ptr(blk_len), int(blk_off.numel()), ctypes.byref(out),
                                          _stream_handle(stream)), "lsm_decode_blocks")
+
+
+def schedule_workspace(ctx: Context, nblk: int) -> torch.Tensor:
+    n = int(ctx.lib.lsm_decode_schedule_workspace_bytes(nblk))
+    return torch.empty(max(n, 16), dtype=torch.uint8, device=ctx.torch_device)
 
 
 def decode_blocks(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,

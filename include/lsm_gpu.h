@@ -150,6 +150,18 @@ int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in, const uint
                       const uint32_t *d_blk_len, uint32_t nblk, const lsm_decode_out *out,
                       void *stream);
 
+/* lsm_decode_blocks for a batch whose block sizes vary: the blocks are
+ * launched largest first (a device-side bucketing of d_blk_len by power-of-
+ * two size class, part of this call), so the batch does not end on a tail of
+ * large blocks each streamed by a single wave.  Outputs are addressed by
+ * block id exactly as in lsm_decode_blocks (identical results).  Workspace:
+ * lsm_decode_schedule_workspace_bytes(nblk). */
+size_t lsm_decode_schedule_workspace_bytes(uint32_t nblk);
+int lsm_decode_blocks_scheduled(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
+                                const uint64_t *d_blk_off, const uint32_t *d_blk_len,
+                                uint32_t nblk, const lsm_decode_out *out, void *d_workspace,
+                                size_t ws_bytes, void *stream);
+
 /* Compact the records of a finished lsm_decode_blocks into one dense array:
  * d_dense_base[0..nblk] = exclusive scan of nrec (d_dense_base[nblk] = total)
  * and block b's records land at d_dense[d_dense_base[b] ..] (and IDX values

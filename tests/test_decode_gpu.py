@@ -337,11 +337,59 @@ def test_config5_mixed_sample(ctx):
     assert int((r.status != 0).sum()) == 0
     assert np.array_equal(r.nrec.cpu().numpy(), nrec)
     check_against_oracle(lsmgpu.GRAMMAR_KV, buf, blk_off, blk_len, r, arena=True)
-    # DESC output, the bench's kernel and placement
+    # DESC output, offset placement
     r = lsmgpu.decode_blocks(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, placement="offset")
     torch.cuda.synchronize()
     assert int((r.status != 0).sum()) == 0
     check_against_oracle(lsmgpu.GRAMMAR_KV, buf, blk_off, blk_len, r)
+    # the bench's path: lsm_decode_blocks_scheduled (largest first), twice
+    # into the same outputs, then the bench's own post-run check
+    rs = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, blk_off.size, int(d_in.numel()))
+    ws = lsmgpu.schedule_workspace(ctx, blk_off.size)
+    for _ in range(2):
+        lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, rs, schedule=ws)
+    torch.cuda.synchronize()
+    check_against_oracle(lsmgpu.GRAMMAR_KV, buf, blk_off, blk_len, rs)
+    import argparse
+    import bench
+    bench.lsmgpu = lsmgpu
+    args = argparse.Namespace(config="mixed", arena=False, _d_in=d_in)
+    bench.verify_decode(args, rs, d_off, d_len, blk_off.size)
+
+
+@pytest.mark.parametrize("grammar", [0, 1, 2])
+@pytest.mark.parametrize("arena", [False, True])
+def test_scheduled_matches_unscheduled(ctx, grammar, arena):
+    """lsm_decode_blocks_scheduled launches blocks largest first; every
+    output (status, counts, descriptors, arenas) equals lsm_decode_blocks' on
+    fuzzed blocks of 0 B to ~200 KiB, corrupted ones included."""
+    rng = np.random.default_rng(40 + grammar)
+    blocks = []
+    for i in range(700):
+        n = int(rng.choice([0, 1, 3, 20, 60, 300]))
+        b = rand_records(rng, grammar, n, kmax=24, vmax=int(rng.choice([8, 120, 700])))
+        blocks.append(corrupt(rng, b) if i % 3 == 0 else b)
+    buf, d_in, d_off, d_len = dev_batch(ctx, blocks)
+    outs = []
+    for sched in (None, lsmgpu.schedule_workspace(ctx, len(blocks))):
+        r = lsmgpu.alloc_decode_offset(ctx, grammar, len(blocks), int(d_in.numel()), arena=arena)
+        for t in (r.desc, r.idx_value, r.key_arena, r.val_arena):
+            if t is not None:
+                t.fill_(-1)  # slots no block writes compare equal
+        lsmgpu.decode_into(ctx, grammar, d_in, d_off, d_len, r, schedule=sched)
+        torch.cuda.synchronize()
+        outs.append(r)
+    a, b = outs
+    assert torch.equal(a.status, b.status) and torch.equal(a.nrec, b.nrec)
+    assert torch.equal(a.desc, b.desc)
+    if grammar == 2:
+        assert torch.equal(a.idx_value, b.idx_value)
+    if arena:
+        for x, y in ((a.key_arena, b.key_arena), (a.val_arena, b.val_arena)):
+            if x is not None:
+                assert torch.equal(x, y)
+    check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
+                         d_len.cpu().numpy().view(np.uint32), b, arena=arena)
 
 
 def test_decode64k_full_size(ctx):
