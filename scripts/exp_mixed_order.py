@@ -14,7 +14,16 @@ dev = ctx.torch_device
 buf, off, ln, _ = synth.mixed_kv_blocks(1 << 30, seed=synth.SEED)
 d_in = lsmgpu.to_device_bytes(buf, dev)
 s = torch.cuda.current_stream()
-for name, order in (("generated", np.arange(off.size)), ("largest-first", np.argsort(-ln.astype(np.int64), kind="stable"))):
+def qclass(n):
+    n = n.astype(np.int64)
+    l = np.floor(np.log2(np.maximum(n, 1))).astype(np.int64)
+    c = 4 * (l - 1) + ((n >> np.maximum(l - 2, 0)) & 3)
+    return np.where(n < 4, n, c)
+rng = np.random.default_rng(1)
+cls = qclass(ln)
+by_class = np.lexsort((rng.random(ln.size), -cls))  # class desc, random inside a class
+for name, order in (("generated", np.arange(off.size)), ("largest-first", np.argsort(-ln.astype(np.int64), kind="stable")),
+                    ("class-desc", by_class)):
     o, l = off[order], ln[order]
     d_off = torch.tensor(o.view(np.int64), device=dev)
     d_len = torch.tensor(l.view(np.int32), device=dev)
@@ -29,4 +38,15 @@ for name, order in (("generated", np.arange(off.size)), ("largest-first", np.arg
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 50
-    print(f"{os.path.basename(sys.argv[1])} {name}: {ms * 1e3:.1f} us, nblk {o.size}, sizes {np.unique(ln, return_counts=True)}", flush=True)
+    print(f"{os.path.basename(sys.argv[1])} {name}: {ms * 1e3:.1f} us, nblk {o.size}", flush=True)
+    if name == "generated" and hasattr(lsmgpu, "schedule_workspace"):
+        ws = lsmgpu.schedule_workspace(ctx, o.size)
+        for _ in range(5):
+            lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=s, schedule=ws)
+        torch.cuda.synchronize()
+        e0.record(s)
+        for _ in range(50):
+            lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=s, schedule=ws)
+        e1.record(s)
+        torch.cuda.synchronize()
+        print(f"  scheduled entry: {e0.elapsed_time(e1) / 50 * 1e3:.1f} us", flush=True)
