@@ -921,6 +921,7 @@ int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void
 
 template <int G, bool ARENA, uint32_t NCH = kRingChunks>
 int launch_decode(const DecodeArgs &a, hipStream_t s) {
+    static_assert(NCH >= 2, "a record header may straddle two ring chunks");
     hipLaunchKernelGGL((decode_v2_kernel<G, NCH, ARENA>), dim3(a.nblk), dim3(kWave), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
@@ -939,15 +940,17 @@ int launch_decode(const DecodeArgs &a, hipStream_t s) {
 // larger classes and behind the earlier tiles' blocks of the same class.
 // Every output is addressed by block id, so the results do not depend on
 // the order.
-constexpr uint32_t kSchedClasses = 128;
+constexpr uint32_t kSchedSub = 2;  // bits below the leading one that split an octave
+constexpr uint32_t kSchedClasses = (33 - kSchedSub) << kSchedSub;
 constexpr uint32_t kSchedThreads = 1024;
 constexpr uint32_t kSchedPer = 16;  // blocks per thread
 constexpr uint32_t kSchedTile = kSchedThreads * kSchedPer;
+static_assert(kSchedClasses <= kSchedThreads, "one thread per class");
 
 __device__ __forceinline__ uint32_t size_class(uint32_t n) {
-    if (n < 4) return n;
-    const uint32_t l = 31 - __clz(n);                  // 2..31
-    return 4 * (l - 1) + ((n >> (l - 2)) & 3);          // 4..123
+    if (n < (1u << kSchedSub)) return n;
+    const uint32_t l = 31 - __clz(n);  // kSchedSub..31
+    return ((l - kSchedSub + 1) << kSchedSub) | ((n >> (l - kSchedSub)) & ((1u << kSchedSub) - 1));
 }
 
 __global__ __launch_bounds__(kSchedThreads) void sched_hist_kernel(const uint32_t *len, uint32_t nblk,
@@ -1961,10 +1964,11 @@ extern "C" int lsm_decode_blocks_scheduled(lsm_ctx *ctx, int grammar, const uint
     a.key_arena_off = out->key_arena_off;
     a.val_arena_off = out->val_arena_off;
     a.order = order;
-    // mixed sizes: a 4 KiB ring, twice the waves per CU (config 5: 210 us
-    // against 231 us with the 8 KiB ring, which streams uniform 64 KiB blocks
-    // faster)
-    constexpr uint32_t R = kRingChunks / 2;
+    // mixed sizes: a 2 KiB ring, the most waves per CU (config 5: 201 us, 4 KiB
+    // 215 us, 8 KiB 231 us; the 8 KiB ring streams uniform 64 KiB blocks
+    // fastest: 92 against 100 us with 4 KiB).  Quarter-octave classes measured
+    // the same as sixteenth-octave ones.
+    constexpr uint32_t R = kRingChunks / 4;
     switch (grammar) {
     case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true, R>(a, s)
                                      : launch_decode<LSM_GRAMMAR_V, false, R>(a, s);
