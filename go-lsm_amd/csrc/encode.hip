@@ -1072,6 +1072,7 @@ struct RegionPlan {
     uint32_t P, len;  // per lane: chunk-relative record start, payload length
     uint64_t xo;      // per lane: IDX offset
     uint32_t cnt, tot, ph, head, sh, OD, nD, base, sbytes;  // wave-uniform
+    uint32_t ulen;    // wave-uniform: the records' common payload length, or ~0u
     uint64_t Sc;      // wave-uniform: source offset of the first payload byte
     uint8_t *dst;
 };
@@ -1096,6 +1097,10 @@ __device__ __forceinline__ bool region_plan(RegionPlan &R, const ChunkOffs &o, u
     R.sbytes = 0;
     if (tot64 + 64 > 4ull * cap) return false;
     R.len = (uint32_t)len;
+    {
+        const uint32_t l0 = uni((uint32_t)len);
+        R.ulen = __ballot(lane < cnt && (uint32_t)len != l0) ? ~0u : l0;
+    }
     R.P = (uint32_t)P64;
     R.tot = (uint32_t)tot64;
     R.xo = G == LSM_GRAMMAR_IDX ? (uint64_t)(xo_base + (int64_t)(4 * lane) + (int64_t)o.v0) : 0;
@@ -1115,6 +1120,25 @@ __device__ __forceinline__ void region_issue(const RegionPlan &R, uint32_t *buf,
                                              const uint8_t *sbase) {
     constexpr uint32_t pre = G == LSM_GRAMMAR_V ? 4 : 12;
     const uint32_t lane = lane_id();
+    const rsrc_t rs = make_rsrc(sbase + (R.Sc - R.ph), uni((R.sbytes + R.ph + 3) & ~3u));
+    if (R.ulen != ~0u) {
+        // records of one size S: the record of image dword D (first byte
+        // x0 = 4D - ph) is min(cnt - 1, floor(x0 / S)) -- no mask, no scan.
+        // floor((x + 1/2) * rcp(S)) is exact for x < 2^16 (the quotient is at
+        // least 1/(2S) from an integer)
+        const uint32_t S = pre + R.ulen;
+        const float inv = __builtin_amdgcn_rcpf((float)S), hinv = 0.5f * inv;
+        for (uint32_t i = 0; i * kWave < R.nD; i++) {
+            const int32_t x0 = 256 * (int32_t)i + 4 * (int32_t)lane - (int32_t)R.ph;
+            const uint32_t xq = x0 < 0 ? 0u : (uint32_t)x0;
+            const uint32_t r = min((uint32_t)__builtin_fmaf((float)xq, inv, hinv), R.cnt - 1);
+            const uint32_t voff = (uint32_t)(x0 - (int32_t)(pre * r) - 4 + (int32_t)R.ph);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)&buf[R.base + R.OD + i * kWave], 4,
+                voff, 0, 0, 2);
+        }
+        return;
+    }
     mask[lane] = 0;  // kGatherMaskWords == kWave
     __builtin_amdgcn_wave_barrier();
     __asm__ __volatile__("" ::: "memory");
@@ -1127,7 +1151,6 @@ __device__ __forceinline__ void region_issue(const RegionPlan &R, uint32_t *buf,
     const uint32_t mv = mask[lane];
     __builtin_amdgcn_wave_barrier();
     __asm__ __volatile__("" ::: "memory");
-    const rsrc_t rs = make_rsrc(sbase + (R.Sc - R.ph), uni((R.sbytes + R.ph + 3) & ~3u));
     uint32_t rb = 0;
     for (uint32_t i = 0; i * kWave < R.nD; i++) {
         const int32_t x0 = 256 * (int32_t)i + 4 * (int32_t)lane - (int32_t)R.ph;
