@@ -237,13 +237,16 @@ def bench_decode(args, world, rank, local):
     # a batch of mixed block sizes goes through lsm_decode_blocks_scheduled
     # (largest first, the bucketing inside every timed call)
     sched = lsmgpu.schedule_workspace(ctx, nblk) if args.config == "mixed" else None
+    # uniform batches: the block size the workload is built with, as a caller
+    # that configures its block size passes it (lsm_decode_blocks_hinted)
+    hint = UNIFORM[args.config]["slot"] if args.config in UNIFORM else None
 
     def step():
         if args.config == "wal":
             lsmgpu.wal_replay_into(ctx, d_in, d_off, d_len, wal_max, r, wal_ws, stream=stream)
         else:
             lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream,
-                               schedule=sched)
+                               schedule=sched, max_blk_len=hint)
 
     for _ in range(args.warmup):
         step()
@@ -317,6 +320,8 @@ def bench_decode(args, world, rank, local):
                        else "lsm_decode_blocks_scheduled (size-class bucketing + "
                             "decode_v2_kernel<KV,8>, all launches)" if args.config == "mixed"
                        else "decode_v2_kernel<KV,8,ARENA>" if args.arena
+                       else "decode_v2_kernel<KV,16> (lsm_decode_blocks_hinted)"
+                       if args.config == "decode64k"
                        else "decode_v2_kernel<KV,8>"),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

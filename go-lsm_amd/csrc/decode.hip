@@ -1923,6 +1923,50 @@ extern "C" int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
     }
 }
 
+// A caller that knows its blocks are large (max_blk_len > 32 KiB: 64 KiB data
+// blocks, whole index regions) gets a 16 KiB ring: twice the bytes in flight
+// per wave (6,400 x 64 KiB blocks: 89.5 against 92.6 us).  The hint only
+// picks the ring; any block length decodes correctly either way.
+extern "C" int lsm_decode_blocks_hinted(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
+                                        const uint64_t *d_blk_off, const uint32_t *d_blk_len,
+                                        uint32_t nblk, uint32_t max_blk_len,
+                                        const lsm_decode_out *out, void *stream) {
+    if (max_blk_len <= 32 * 1024)
+        return lsm_decode_blocks(ctx, grammar, d_in, d_blk_off, d_blk_len, nblk, out, stream);
+    if (!ctx || !out) return LSM_EINVAL;
+    if (nblk == 0) return 0;
+    if (!d_in || !d_blk_off || !d_blk_len || !out->desc || !out->nrec || !out->status)
+        return LSM_EINVAL;
+    if (grammar < LSM_GRAMMAR_V || grammar > LSM_GRAMMAR_IDX) return LSM_EINVAL;
+    const bool arena = out->key_arena || out->val_arena;
+    DecodeArgs a;
+    a.in = d_in;
+    a.blk_off = d_blk_off;
+    a.blk_len = d_blk_len;
+    a.nblk = nblk;
+    a.desc = reinterpret_cast<u32x4 *>(out->desc);
+    a.rec_base = out->rec_base;
+    a.nrec = out->nrec;
+    a.status = out->status;
+    a.idx_value = out->idx_value;
+    a.key_arena = out->key_arena;
+    a.val_arena = out->val_arena;
+    a.arena_base = out->arena_base;
+    a.key_arena_off = out->key_arena_off;
+    a.val_arena_off = out->val_arena_off;
+    a.order = nullptr;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    constexpr uint32_t R = 2 * kRingChunks;
+    switch (grammar) {
+    case LSM_GRAMMAR_V: return arena ? launch_decode<LSM_GRAMMAR_V, true, R>(a, s)
+                                     : launch_decode<LSM_GRAMMAR_V, false, R>(a, s);
+    case LSM_GRAMMAR_KV: return arena ? launch_decode<LSM_GRAMMAR_KV, true, R>(a, s)
+                                      : launch_decode<LSM_GRAMMAR_KV, false, R>(a, s);
+    default: return arena ? launch_decode<LSM_GRAMMAR_IDX, true, R>(a, s)
+                          : launch_decode<LSM_GRAMMAR_IDX, false, R>(a, s);
+    }
+}
+
 extern "C" size_t lsm_decode_schedule_workspace_bytes(uint32_t nblk) {
     const uint64_t ntile = ((uint64_t)nblk + kSchedTile - 1) / kSchedTile;
     return 4ull * kSchedClasses * ntile + 4ull * nblk + 16;

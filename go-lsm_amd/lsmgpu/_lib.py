@@ -47,6 +47,9 @@ SIGNATURES = {
     "lsm_decode_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u64p, c_u32p,
                                          ctypes.c_uint32, ctypes.POINTER(DecodeOut),
                                          ctypes.c_void_p]),
+    "lsm_decode_blocks_hinted": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u64p, c_u32p,
+                                                ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.POINTER(DecodeOut), ctypes.c_void_p]),
     "lsm_decode_schedule_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32]),
     "lsm_decode_blocks_scheduled": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, c_u8p, c_u64p,
                                                    c_u32p, ctypes.c_uint32,

@@ -232,11 +232,17 @@ def _decode_out(r: DecodeResult):
 
 def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.Tensor,
                 blk_len: torch.Tensor, r: DecodeResult, stream=None,
-                schedule: Optional[torch.Tensor] = None) -> None:
+                schedule: Optional[torch.Tensor] = None, max_blk_len: Optional[int] = None) -> None:
     """lsm_decode_blocks into preallocated outputs (asynchronous).  With a
     `schedule` workspace (schedule_workspace()): lsm_decode_blocks_scheduled,
-    the blocks launched largest first (for batches whose sizes vary)."""
+    the blocks launched largest first (for batches whose sizes vary).  With
+    `max_blk_len`: lsm_decode_blocks_hinted (the ring chosen for that bound)."""
     out = _decode_out(r)
+    if max_blk_len is not None and schedule is None:
+        _lib.check(ctx.lib.lsm_decode_blocks_hinted(
+            ctx.handle, grammar, _ptr(d_in), _ptr(blk_off), _ptr(blk_len), int(blk_off.numel()),
+            int(max_blk_len), ctypes.byref(out), _stream_handle(stream)), "lsm_decode_blocks_hinted")
+        return
     if schedule is not None:
         _lib.check(ctx.lib.lsm_decode_blocks_scheduled(
             ctx.handle, grammar, _ptr(d_in), _ptr(blk_off), _ptr(blk_len), int(blk_off.numel()),

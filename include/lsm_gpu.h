@@ -150,6 +150,14 @@ int lsm_decode_blocks(lsm_ctx *ctx, int grammar, const uint8_t *d_in, const uint
                       const uint32_t *d_blk_len, uint32_t nblk, const lsm_decode_out *out,
                       void *stream);
 
+/* lsm_decode_blocks with the caller's upper bound on the block lengths: above
+ * 32 KiB a larger per-wave LDS ring is used (more bytes in flight per wave).
+ * The hint only selects the ring; results are identical for any input, also
+ * when a block is longer than the hint. */
+int lsm_decode_blocks_hinted(lsm_ctx *ctx, int grammar, const uint8_t *d_in,
+                             const uint64_t *d_blk_off, const uint32_t *d_blk_len, uint32_t nblk,
+                             uint32_t max_blk_len, const lsm_decode_out *out, void *stream);
+
 /* lsm_decode_blocks for a batch whose block sizes vary: the blocks are
  * launched largest first (a device-side bucketing of d_blk_len by power-of-
  * two size class, part of this call), so the batch does not end on a tail of

@@ -410,6 +410,52 @@ def test_decode64k_full_size(ctx):
     want = (np.arange(nblk)[:, None] * 65536 + np.arange(recs)[None, :] * 124).reshape(-1)
     assert np.array_equal(d["rec_off"], want.astype(np.uint64))
     assert (d["key_len"] == 16).all() and (d["val_len"] == 100).all()
+    # the bench's path: lsm_decode_blocks_hinted with the 64 KiB bound (16 KiB
+    # ring), identical outputs, and the bench's own post-run check
+    rh = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()))
+    lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, rh, max_blk_len=65536)
+    torch.cuda.synchronize()
+    assert torch.equal(rh.desc.view(-1, 4)[idx], r.desc.view(-1, 4)[idx])
+    assert torch.equal(rh.nrec[:nblk], r.nrec[:nblk]) and torch.equal(rh.status[:nblk], r.status[:nblk])
+    import argparse
+    import bench
+    bench.lsmgpu = lsmgpu
+    bench.verify_decode(argparse.Namespace(config="decode64k", arena=False, _d_in=d_in), rh, d_off,
+                        d_len, nblk)
+
+
+@pytest.mark.parametrize("grammar", [0, 1, 2])
+@pytest.mark.parametrize("arena", [False, True])
+def test_hinted_matches_plain(ctx, grammar, arena):
+    """lsm_decode_blocks_hinted only picks the ring: with a large-block hint
+    (16 KiB ring) every output equals lsm_decode_blocks', also for blocks
+    longer than the hint and for corrupted ones."""
+    rng = np.random.default_rng(70 + grammar)
+    blocks = []
+    for i in range(300):
+        n = int(rng.choice([0, 2, 40, 300, 900]))
+        b = rand_records(rng, grammar, n, kmax=40, vmax=int(rng.choice([8, 200, 2000])))
+        blocks.append(corrupt(rng, b) if i % 4 == 0 else b)
+    blocks += [rand_records(rng, grammar, 1500, kmax=200, vmax=2000) for _ in range(3)]
+    buf, d_in, d_off, d_len = dev_batch(ctx, blocks, align_pad=7, rng=rng)
+    outs = []
+    for hint in (None, 40000):
+        r = lsmgpu.alloc_decode_offset(ctx, grammar, len(blocks), int(d_in.numel()), arena=arena)
+        for t in (r.desc, r.idx_value, r.key_arena, r.val_arena):
+            if t is not None:
+                t.fill_(-1)
+        lsmgpu.decode_into(ctx, grammar, d_in, d_off, d_len, r, max_blk_len=hint)
+        torch.cuda.synchronize()
+        outs.append(r)
+    a, b = outs
+    assert int(d_len.max()) > 40000  # some blocks exceed the hint
+    assert torch.equal(a.status, b.status) and torch.equal(a.nrec, b.nrec)
+    assert torch.equal(a.desc, b.desc)
+    for x, y in ((a.idx_value, b.idx_value), (a.key_arena, b.key_arena), (a.val_arena, b.val_arena)):
+        if x is not None:
+            assert torch.equal(x, y)
+    check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
+                         d_len.cpu().numpy().view(np.uint32), b, arena=arena)
 
 
 @pytest.mark.parametrize("grammar", [0, 1, 2])
