@@ -845,47 +845,36 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
     bloom_file_body(g, a, blockIdx.x, lds_bits, n1);
 }
 
-// ---- split bloom build: hash everywhere, then OR per slice (k <= 16) --------
+// ---- split bloom build: hash in the region writer, then OR per slice -------
 //
 // bloom_file_kernel pins one 1024-thread workgroup and 100 KiB of LDS per
 // filter to a CU for the whole hash, so beside the region writers it runs on
-// 208 CUs with LDS to spare for only a few region waves.  The split build
-// hashes every key once with no LDS at all (bloom_hash_kernel, any CU, beside
-// the region writers), leaving per key the residues mod m of the four
-// location classes and of the two class steps (location(j) = h[j%2] +
-// j*h[2 + ((j + j%2) % 4)/2], bloom.go:133-136: class c = j%4 is an
-// arithmetic progression) plus the carry bit of each 64-bit step, 24 bytes;
-// bloom_or_kernel then rebuilds the k locations of every key of its filter
-// from them (additions only) and ORs those of its slice into LDS.
+// 208 CUs with LDS to spare for only a few region waves.  For two-slice
+// filters with k <= 16 the build is split: the region writer (which gathers
+// every key into LDS for the index region anyway) hashes each key once and
+// leaves per key the residues mod m of the four location classes and of the
+// two class steps (location(j) = h[j%2] + j*h[2 + ((j + j%2) % 4)/2],
+// bloom.go:133-136: class c = j%4 is an arithmetic progression) plus the carry
+// bit of each 64-bit step, 24 bytes; bloom_or_kernel then rebuilds the k
+// locations of every key of its filter from them (additions only) and ORs
+// those of its slice into LDS.
 constexpr uint32_t kHashRecDwords = 6;
 constexpr uint32_t kSplitMaxK = 16;  // three carries per class fit the record
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-struct BloomHashArgs {
-    const uint8_t *keys;
-    const uint64_t *koff;
-    const uint64_t *file_start;  // keys [file_start[0], file_start[nfile])
-    uint32_t nfile;
-    uint32_t m, rl, rh;
-    uint32_t *rec;     // kHashRecDwords per key, key file_start[0] first
-};
-
-__global__ __launch_bounds__(256) void bloom_hash_kernel(BloomHashArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t k0 = uni64(a.file_start[0]);
-    if (t >= uni64(a.file_start[a.nfile]) - k0) return;
-    const uint64_t i = k0 + t;
-    const uint64_t ko = a.koff[i], kl = a.koff[i + 1] - ko;
-    uint64_t h[4];
-    sum256_pre(a.keys + ko, kl, ldg_u64_unaligned(a.keys + ko), ldg_u64_unaligned(a.keys + ko + 8), h);
+// The 24-byte hash record of a key from its sum256 digest: the residues mod m
+// of the four location classes and of the two class steps, carry bits of the
+// 64-bit steps in the residues' spare top bits (m <= 2^30).
+__device__ __forceinline__ void store_hash_rec(const uint64_t h[4], uint32_t m, uint32_t rl,
+                                               uint32_t rh, uint32_t *rec) {
     uint64_t loc[4] = {h[0], h[1] + h[3], h[0] + (h[3] << 1), h[1] + h[2] + (h[2] << 1)};
     const uint64_t st2 = h[2] << 2, st3 = h[3] << 2;
     uint32_t r[6];
     uint32_t cy = 0;  // bit 3c + n - 1: the step to location 4n + c carries
 #pragma unroll
     for (uint32_t c = 0; c < 4; c++) {
-        r[c] = mod_small(loc[c], a.m, a.rl, a.rh);
+        r[c] = mod_small(loc[c], m, rl, rh);
         const uint64_t st = (c == 0 || c == 3) ? st2 : st3;
         uint64_t l = loc[c];
 #pragma unroll
@@ -895,12 +884,12 @@ __global__ __launch_bounds__(256) void bloom_hash_kernel(BloomHashArgs a) {
             l = nl;
         }
     }
-    r[4] = mod_small(st2, a.m, a.rl, a.rh);
-    r[5] = mod_small(st3, a.m, a.rl, a.rh);
+    r[4] = mod_small(st2, m, rl, rh);
+    r[5] = mod_small(st3, m, rl, rh);
     // residues are < m <= 2^30: two carry bits ride in the top of each dword
 #pragma unroll
     for (uint32_t d = 0; d < 6; d++) r[d] |= ((cy >> (2 * d)) & 3u) << 30;
-    gptr_t<uint32_t> o = gbl(a.rec + kHashRecDwords * t);
+    gptr_t<uint32_t> o = gbl(rec);
     *(gptr_t<u32x4>)o = u32x4{r[0], r[1], r[2], r[3]};
     *(gptr_t<u32x2>)(o + 4) = u32x2{r[4], r[5]};
 }
@@ -995,6 +984,10 @@ struct SstArgs {
     uint64_t m, nwords;
     uint32_t k;
     uint32_t skip_v;  // the V region is written from value views (lsm_build_sst_views)
+    // the filter's key hashes fused into the region writer: a hash record per
+    // key (store_hash_rec, key file_start[0] first), or null
+    uint32_t *hrec;
+    uint32_t hm, hrl, hrh;
 };
 
 struct SstLayout {
@@ -1228,6 +1221,7 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
     uint32_t *mask = buf + kRegBufDwords;
     uint8_t *img = a.out + uni64(a.file_off[f]);
     const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
+    const uint64_t K0 = a.hrec ? uni64(a.file_start[0]) : 0;
     auto count = [&](uint64_t c) { return (uint32_t)(cend - c < (uint64_t)kWave ? cend - c : kWave); };
     ChunkOffs off = load_offs(a, c0, count(c0));
     for (;;) {
@@ -1256,6 +1250,19 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
             __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
             if (!a.skip_v) region_finish<LSM_GRAMMAR_V>(pv, buf);
             region_finish<LSM_GRAMMAR_IDX>(pi, buf);
+            if (a.hrec && lane_id() < cnt) {
+                // Filter.Add's key hash (bloom.go:175-181) from the key
+                // already gathered into the IDX image, while its stores drain
+                const uint32_t A = 4 * (pi.base + pi.OD) + pi.ph + pi.P + 4;
+                const uint32_t q = A >> 2;
+                const uint32_t x0 = buf[q], x1 = buf[q + 1], x2 = buf[q + 2], x3 = buf[q + 3],
+                               x4 = buf[q + 4];
+                const uint64_t f0 = (uint64_t)funnel(x1, x2, A) << 32 | funnel(x0, x1, A);
+                const uint64_t f1 = (uint64_t)funnel(x3, x4, A) << 32 | funnel(x2, x3, A);
+                uint64_t h[4];
+                sum256_pre(a.keys + off.k0, pi.len, f0, f1, h);
+                store_hash_rec(h, a.hm, a.hrl, a.hrh, a.hrec + kHashRecDwords * (c0 + lane_id() - K0));
+            }
             off = nxt;
         } else {
             // a chunk with records too large for one buffer: region by region
@@ -1268,6 +1275,11 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
             ChunkTable *ct = reinterpret_cast<ChunkTable *>(buf);
             if (!a.skip_v) encode_chunk_any<LSM_GRAMMAR_V, kRegMaxImage>(S, c0, cnt, dV, buf, nullptr, ct);
             encode_chunk_any<LSM_GRAMMAR_IDX, kRegMaxImage>(S, c0, cnt, dI, buf, nullptr, ct);
+            if (a.hrec && lane_id() < cnt) {
+                uint64_t h[4];
+                sum256(a.keys + off.k0, off.k1 - off.k0, h);
+                store_hash_rec(h, a.hm, a.hrl, a.hrh, a.hrec + kHashRecDwords * (c0 + lane_id() - K0));
+            }
             if (more) off = load_offs(a, cn, count(cn));
         }
         if (!more) break;
@@ -2141,7 +2153,7 @@ static uint32_t bloom_slices(uint64_t m) {
     return (uint32_t)((m + sb - 1) / sb);
 }
 static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slices(m) <= 2; }
-// two slices and k <= 16: the split build (bloom_hash_kernel + bloom_or_kernel)
+// two slices and k <= 16: the split build (hash in sst_regions_kernel, bloom_or_kernel)
 static bool split_bloom(uint64_t m, uint32_t k) {
     return hash_once_bloom(m) && bloom_slices(m) == 2 && k <= kSplitMaxK;
 }
@@ -2187,51 +2199,26 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     a.nwords = nwords;
     a.k = kk;
     a.skip_v = views != nullptr;
+    a.hrec = nullptr;
+    a.hm = a.hrl = a.hrh = 0;
 
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
-    bool forked = false;
+    bool forked = false, split = false;
     if (hash_once_bloom(m)) {
         const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
         if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
         if (split_bloom(m, kk)) {
-            // the hash first (no LDS, every CU), then the per-slice ORs and,
-            // on the side stream, the regions: the ORs are placed first and
-            // hold their 100 KiB of LDS beside the region writers (the hash
-            // beside the regions with the ORs behind them measured 3% slower:
-            // the ORs then wait for the regions to release LDS)
+            // Filter.Add's key hash runs inside the region writer (the keys
+            // are gathered there anyway, sstable.go:322-326 feeds data, index
+            // and filter in one pass); the per-slice ORs follow on the same
+            // stream and store the filter words into the images.
             const uint64_t mr = barrett_recip(m);
-            BloomHashArgs h;
-            h.keys = d_keys;
-            h.koff = d_koff;
-            h.file_start = d_file_start;
-            h.nfile = nfile;
-            h.m = (uint32_t)m;
-            h.rl = (uint32_t)mr;
-            h.rh = (uint32_t)(mr >> 32);
-            h.rec = static_cast<uint32_t *>(d_workspace);
-            const uint64_t nmax = (uint64_t)nfile * max_file_records;
-            if (nmax) {
-                hipLaunchKernelGGL(bloom_hash_kernel, dim3((uint32_t)((nmax + 255) / 256)), dim3(256), 0,
-                                   s, h);
-                LSM_HIP_CHECK(hipGetLastError());
-            }
-            LSM_HIP_CHECK(hipEventRecord(ctx->fork, s));
-            LSM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->fork, 0));
-            BloomOrArgs bo{};
-            bo.file_start = d_file_start;
-            bo.rec = h.rec;
-            bo.m = (uint32_t)m;
-            bo.k = kk;
-            bo.c64 = (uint32_t)((~0ull % m + 1) % m);
-            bo.split = (uint32_t)sb;
-            bo.nwords = nwords;
-            bo.koff = d_koff;
-            bo.out = d_out;
-            bo.file_off = d_file_off;
-            hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo);
-            LSM_HIP_CHECK(hipGetLastError());
-            forked = true;
+            a.hrec = static_cast<uint32_t *>(d_workspace);
+            a.hm = (uint32_t)m;
+            a.hrl = (uint32_t)mr;
+            a.hrh = (uint32_t)(mr >> 32);
+            split = true;
         } else {
             BloomFileArgs b;
             b.keys = d_keys;
@@ -2292,6 +2279,21 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     }
     hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, rs, a);
     LSM_HIP_CHECK(hipGetLastError());
+    if (split) {
+        BloomOrArgs bo{};
+        bo.file_start = d_file_start;
+        bo.rec = a.hrec;
+        bo.m = (uint32_t)m;
+        bo.k = kk;
+        bo.c64 = (uint32_t)((~0ull % m + 1) % m);
+        bo.split = (uint32_t)sb;
+        bo.nwords = nwords;
+        bo.koff = d_koff;
+        bo.out = d_out;
+        bo.file_off = d_file_off;
+        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo);
+        LSM_HIP_CHECK(hipGetLastError());
+    }
     if (forked) {  // join: the caller's stream waits for the regions
         LSM_HIP_CHECK(hipEventRecord(ctx->join, ctx->side));
         LSM_HIP_CHECK(hipStreamWaitEvent(s, ctx->join, 0));
