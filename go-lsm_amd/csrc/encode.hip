@@ -905,71 +905,6 @@ struct BloomOrArgs {
     const uint64_t *file_off;
 };
 
-// Filter blockIdx.x, slice blockIdx.y: every key's k locations rebuilt from
-// its record, the slice's bits ORed in LDS, then stored big-endian into the
-// image.  (One workgroup per filter holding 152 KiB and listing the rest was
-// measured slower: the ORs are bound by LDS atomic throughput, about 1.4
-// lanes per clock per CU for scattered words, not by the rebuild.)
-__global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
-    const uint32_t f = blockIdx.x, sl = blockIdx.y;
-    const uint32_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
-    const uint32_t nw = (hi - lo + 63) / 64 * 2;
-    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_bits[i] = 0;
-    __syncthreads();
-    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
-    const uint32_t m = a.m, c64 = a.c64;
-    const uint64_t k0 = uni64(a.file_start[0]);
-    // records two rounds ahead in flight (indices past the filter clamped;
-    // a filter without keys loads nothing and stores its zero words)
-    const gptr_t<const uint32_t> rec = gbl(a.rec);
-    auto ld = [&](uint64_t i, u32x4 &x, u32x2 &y) {
-        const uint64_t j = (i < e ? i : e - 1) - k0;
-        x = *(gptr_t<const u32x4>)(rec + kHashRecDwords * j);
-        y = *(gptr_t<const u32x2>)(rec + kHashRecDwords * j + 4);
-    };
-    u32x4 xa, xb;
-    u32x2 ya, yb;
-    if (e > s) {
-        ld(s + threadIdx.x, xa, ya);
-        ld(s + threadIdx.x + blockDim.x, xb, yb);
-    }
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const u32x4 x = xa;
-        const u32x2 y = ya;
-        xa = xb;
-        ya = yb;
-        ld(i + 2 * blockDim.x, xb, yb);
-        const uint32_t raw[6] = {x.x, x.y, x.z, x.w, y.x, y.y};
-        uint32_t cy = 0, r[4];
-#pragma unroll
-        for (uint32_t d = 0; d < 6; d++) cy |= (raw[d] >> 30) << (2 * d);
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++) r[c] = raw[c] & 0x3FFFFFFFu;
-        const uint32_t d2 = raw[4] & 0x3FFFFFFFu, d3 = raw[5] & 0x3FFFFFFFu;
-        // a step whose 64-bit add wraps loses 2^64: its residue less 2^64 mod m
-        const uint32_t w2 = d2 >= c64 ? d2 - c64 : d2 + m - c64;
-        const uint32_t w3 = d3 >= c64 ? d3 - c64 : d3 + m - c64;
-#pragma unroll
-        for (uint32_t j = 0; j < kSplitMaxK; j++) {
-            const uint32_t c = j & 3, n = j >> 2;  // compile-time: r[] stays in registers
-            if (j >= a.k) continue;                 // wave-uniform
-            const uint32_t p = r[c];
-            if (p >= lo && p < hi) atomicOr(&lds_bits[(p - lo) >> 5], 1u << ((p - lo) & 31));
-            if (n < 3) {
-                const bool a2 = c == 0 || c == 3;
-                const bool carry = (cy >> (3 * c + n)) & 1;
-                const uint32_t t = p + (carry ? (a2 ? w2 : w3) : (a2 ? d2 : d3));
-                r[c] = min(t, t - m);
-            }
-        }
-    }
-    __syncthreads();
-    const uint64_t hdr = sst_header_bytes(a.koff, s, e);
-    store_filter_slice(WgGroup{}, lds_bits, lo / 64, sl ? a.nwords : (uint64_t)(hi + 63) / 64,
-                       a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
-}
-
 // ---- .sst image writer ------------------------------------------------------
 
 struct SstArgs {
@@ -1460,6 +1395,74 @@ __device__ void sst_meta_body(const SstArgs &a, uint32_t f) {
 }
 
 __global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body(a, blockIdx.x); }
+
+// Filter blockIdx.x, slice blockIdx.y: every key's k locations rebuilt from
+// its record, the slice's bits ORed in LDS, then stored big-endian into the
+// image; the first slice's workgroup also writes the file's framing.  (One workgroup per filter holding 152 KiB and listing the rest was
+// measured slower: the ORs are bound by LDS atomic throughput, about 1.4
+// lanes per clock per CU for scattered words, not by the rebuild.)
+__global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs sa) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    const uint32_t f = blockIdx.x, sl = blockIdx.y;
+    // the image's header, filter prefix and footer (disjoint from the words)
+    if (sl == 0 && threadIdx.x < kWave) sst_meta_body(sa, f);
+    const uint32_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
+    const uint32_t nw = (hi - lo + 63) / 64 * 2;
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_bits[i] = 0;
+    __syncthreads();
+    const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
+    const uint32_t m = a.m, c64 = a.c64;
+    const uint64_t k0 = uni64(a.file_start[0]);
+    // records two rounds ahead in flight (indices past the filter clamped;
+    // a filter without keys loads nothing and stores its zero words)
+    const gptr_t<const uint32_t> rec = gbl(a.rec);
+    auto ld = [&](uint64_t i, u32x4 &x, u32x2 &y) {
+        const uint64_t j = (i < e ? i : e - 1) - k0;
+        x = *(gptr_t<const u32x4>)(rec + kHashRecDwords * j);
+        y = *(gptr_t<const u32x2>)(rec + kHashRecDwords * j + 4);
+    };
+    u32x4 xa, xb;
+    u32x2 ya, yb;
+    if (e > s) {
+        ld(s + threadIdx.x, xa, ya);
+        ld(s + threadIdx.x + blockDim.x, xb, yb);
+    }
+    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const u32x4 x = xa;
+        const u32x2 y = ya;
+        xa = xb;
+        ya = yb;
+        ld(i + 2 * blockDim.x, xb, yb);
+        const uint32_t raw[6] = {x.x, x.y, x.z, x.w, y.x, y.y};
+        uint32_t cy = 0, r[4];
+#pragma unroll
+        for (uint32_t d = 0; d < 6; d++) cy |= (raw[d] >> 30) << (2 * d);
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) r[c] = raw[c] & 0x3FFFFFFFu;
+        const uint32_t d2 = raw[4] & 0x3FFFFFFFu, d3 = raw[5] & 0x3FFFFFFFu;
+        // a step whose 64-bit add wraps loses 2^64: its residue less 2^64 mod m
+        const uint32_t w2 = d2 >= c64 ? d2 - c64 : d2 + m - c64;
+        const uint32_t w3 = d3 >= c64 ? d3 - c64 : d3 + m - c64;
+#pragma unroll
+        for (uint32_t j = 0; j < kSplitMaxK; j++) {
+            const uint32_t c = j & 3, n = j >> 2;  // compile-time: r[] stays in registers
+            if (j >= a.k) continue;                 // wave-uniform
+            const uint32_t p = r[c];
+            if (p >= lo && p < hi) atomicOr(&lds_bits[(p - lo) >> 5], 1u << ((p - lo) & 31));
+            if (n < 3) {
+                const bool a2 = c == 0 || c == 3;
+                const bool carry = (cy >> (3 * c + n)) & 1;
+                const uint32_t t = p + (carry ? (a2 ? w2 : w3) : (a2 ? d2 : d3));
+                r[c] = min(t, t - m);
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t hdr = sst_header_bytes(a.koff, s, e);
+    store_filter_slice(WgGroup{}, lds_bits, lo / 64, sl ? a.nwords : (uint64_t)(hi + 63) / 64,
+                       a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
+}
+
 
 
 // ---- probe / hash ----------------------------------------------------------
@@ -2277,9 +2280,10 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
             LSM_HIP_CHECK(hipGetLastError());
         }
     }
-    hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, rs, a);
-    LSM_HIP_CHECK(hipGetLastError());
-    if (split) {
+    if (!split) {
+        hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, rs, a);
+        LSM_HIP_CHECK(hipGetLastError());
+    } else {
         BloomOrArgs bo{};
         bo.file_start = d_file_start;
         bo.rec = a.hrec;
@@ -2291,7 +2295,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         bo.koff = d_koff;
         bo.out = d_out;
         bo.file_off = d_file_off;
-        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo);
+        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo, a);
         LSM_HIP_CHECK(hipGetLastError());
     }
     if (forked) {  // join: the caller's stream waits for the regions

@@ -55,6 +55,44 @@ extern "C" int probe_copy(const void *in, void *out, uint64_t nbytes, int grid, 
     return (int)hipGetLastError();
 }
 
+
+// copy variants: U float4s in flight per thread, optional nontemporal stores /
+// loads; and one float4 per thread over a grid covering the buffer
+template <int U, bool NTS, bool NTL>
+__global__ __launch_bounds__(256) void copy_var(const u32x4 *in, u32x4 *out, uint64_t n16) {
+    const uint64_t st = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += U * st) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i + u * st < n16) v[u] = NTL ? __builtin_nontemporal_load(&in[i + u * st]) : in[i + u * st];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i + u * st < n16) {
+                if (NTS) __builtin_nontemporal_store(v[u], &out[i + u * st]);
+                else out[i + u * st] = v[u];
+            }
+    }
+}
+__global__ __launch_bounds__(256) void copy_flat(const u32x4 *in, u32x4 *out, uint64_t n16) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n16) out[i] = in[i];
+}
+extern "C" int probe_copy_var(const void *in, void *out, uint64_t nbytes, int grid, int kind, void *stream) {
+    const u32x4 *a = (const u32x4 *)in;
+    u32x4 *b = (u32x4 *)out;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t n16 = nbytes / 16;
+    switch (kind) {
+    case 0: hipLaunchKernelGGL((copy_var<4, false, false>), dim3(grid), dim3(256), 0, s, a, b, n16); break;
+    case 1: hipLaunchKernelGGL((copy_var<4, true, false>), dim3(grid), dim3(256), 0, s, a, b, n16); break;
+    case 2: hipLaunchKernelGGL((copy_var<4, true, true>), dim3(grid), dim3(256), 0, s, a, b, n16); break;
+    case 3: hipLaunchKernelGGL((copy_var<1, true, false>), dim3(grid), dim3(256), 0, s, a, b, n16); break;
+    default: hipLaunchKernelGGL(copy_flat, dim3((uint32_t)((n16 + 255) / 256)), dim3(256), 0, s, a, b, n16); break;
+    }
+    return (int)hipGetLastError();
+}
+
 // ---- block-shaped probes (decode4k's memory pattern without the parse) ------
 // Each wave stages one 4 KiB block into LDS by four 1 KiB LDS-DMAs, waits,
 // and writes 33 x 16 B descriptors (the DESC output of a 33-record block).
