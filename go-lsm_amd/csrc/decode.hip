@@ -188,6 +188,12 @@ struct RingBytes {
     __device__ __forceinline__ uint32_t word(uint32_t w) const {
         return LIN ? ring[w] : ring[w % (NCH * kChunk / 4)];
     }
+    // the ring dword at dword-aligned stream byte sb
+    __device__ __forceinline__ uint32_t word_at(uint32_t sb) const {
+        constexpr uint32_t kB = NCH * kChunk;
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(ring) +
+                                                   (LIN ? sb : sb & (kB - 1)));
+    }
     __device__ __forceinline__ uint32_t u32(uint32_t sb) const {
         return funnel(word(sb >> 2), word((sb >> 2) + 1), sb);
     }
@@ -254,6 +260,13 @@ __device__ __forceinline__ void set_dword(u32x4 &v, uint32_t j, uint32_t w) {
 // falls inside some lane's dword (k < 4), bytes singly only in the run's
 // first and last dword.  Ring reads are indexed modulo the ring, so lanes
 // past the end read harmless bytes.
+// a*b + c for a, b < 2^24 (full-rate v_mad_u32_u24; b wave-uniform)
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
+
 template <uint32_t NCH, bool LIN>
 __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, uint8_t *out,
                                                uint32_t src0, uint32_t S, uint32_t L,
@@ -264,26 +277,30 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
     // full-rate 24-bit products (v_mul_u32_u24): every operand here is < 2^24
     auto mul24 = [](uint32_t x, uint32_t y) { return (x & 0xFFFFFFu) * (y & 0xFFFFFFu); };
     if (((src0 | S | L | (uint32_t)(uintptr_t)out) & 3) == 0) {
-        // dword-aligned run: output dword j is ring dword src0/4 + j + r*(S-L)/4
-        // with r = floor(j / (L/4)) -- one ring read and one store per dword
-        const uint32_t L4 = L >> 2, G4 = (S - L) >> 2, w0 = src0 >> 2, nd = T >> 2;
+        // dword-aligned run: output dword j is ring byte src0 + 4j + r*(S-L)
+        // with r = floor(j / (L/4)) -- one ring read and one store per dword.
+        // The stores go through a buffer resource spanning exactly the run:
+        // lanes past its end are dropped by the range check (no exec masks),
+        // and their offsets are 4*lane plus scalar parts (no address VALU).
+        const uint32_t L4 = L >> 2, GB = S - L;
         // floor((j + 1/2) * rcp(L4)) is exact for j < 2^16: the quotient is at
         // least 1/(2 L4) from an integer, the error below 2^-6 / L4
         const float inv4 = __builtin_amdgcn_rcpf((float)L4), hinv4 = 0.5f * inv4;
-        uint32_t *a0 = reinterpret_cast<uint32_t *>(out);
+        const rsrc_t os = make_rsrc(out, T);
+        const uint32_t lane4 = 4 * lane;
         constexpr uint32_t V = 4;  // ring reads in flight per lane
 #pragma unroll 1
-        for (uint32_t j0 = lane; j0 < nd; j0 += V * kWave) {
+        for (uint32_t b = 0; b < T; b += 4 * V * kWave) {  // wave-uniform output byte
             uint32_t v[V];
 #pragma unroll
-            for (uint32_t t = 0; t < V; t++) {  // past nd: harmless ring bytes
-                const uint32_t j = j0 + t * kWave;
+            for (uint32_t t = 0; t < V; t++) {  // past the run: harmless ring bytes
+                const uint32_t j = (b >> 2) + t * kWave + lane;
                 const uint32_t r = (uint32_t)__builtin_fmaf((float)j, inv4, hinv4);
-                v[t] = rb.word(w0 + j + __umul24(r, G4));
+                v[t] = rb.word_at(mad_u24(r, GB, src0 + 4 * j));
             }
 #pragma unroll
             for (uint32_t t = 0; t < V; t++)
-                if (j0 + t * kWave < nd) a0[j0 + t * kWave] = v[t];
+                __builtin_amdgcn_raw_buffer_store_b32(v[t], os, lane4, b + 4 * kWave * t, 0);
         }
         return;
     }
@@ -523,7 +540,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                 if (G == LSM_GRAMMAR_IDX && a.idx_value)
                     a.idx_value[base + s_first + lane] = (int64_t)((uint64_t)s_xhi << 32 | s_xlo);
             }
-            if (ARENA) {
+            if (ARENA && ns > pend) {  // (the pending record leaves with its run)
                 lds_u32_t *lring = (lds_u32_t *)ring, *ltab = (lds_u32_t *)tab;
                 // keys, then values: one emitter body serves both arenas
 #pragma unroll 1
