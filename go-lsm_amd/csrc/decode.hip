@@ -280,27 +280,26 @@ __device__ __forceinline__ void arena_emit_run(const RingBytes<NCH, LIN> &rb, ui
         // dword-aligned run: output dword j is ring byte src0 + 4j + r*(S-L)
         // with r = floor(j / (L/4)) -- one ring read and one store per dword.
         // The stores go through a buffer resource spanning exactly the run:
-        // lanes past its end are dropped by the range check (no exec masks),
-        // and their offsets are 4*lane plus scalar parts (no address VALU).
+        // lanes past its end are dropped by the range check (no exec masks,
+        // no 64-bit address arithmetic; the whole offset is in the VGPR).
         const uint32_t L4 = L >> 2, GB = S - L;
         // floor((j + 1/2) * rcp(L4)) is exact for j < 2^16: the quotient is at
         // least 1/(2 L4) from an integer, the error below 2^-6 / L4
         const float inv4 = __builtin_amdgcn_rcpf((float)L4), hinv4 = 0.5f * inv4;
         const rsrc_t os = make_rsrc(out, T);
-        const uint32_t lane4 = 4 * lane;
         constexpr uint32_t V = 4;  // ring reads in flight per lane
 #pragma unroll 1
         for (uint32_t b = 0; b < T; b += 4 * V * kWave) {  // wave-uniform output byte
-            uint32_t v[V];
+            uint32_t v[V], o[V];
 #pragma unroll
             for (uint32_t t = 0; t < V; t++) {  // past the run: harmless ring bytes
                 const uint32_t j = (b >> 2) + t * kWave + lane;
                 const uint32_t r = (uint32_t)__builtin_fmaf((float)j, inv4, hinv4);
-                v[t] = rb.word_at(mad_u24(r, GB, src0 + 4 * j));
+                o[t] = 4 * j;
+                v[t] = rb.word_at(mad_u24(r, GB, src0 + o[t]));
             }
 #pragma unroll
-            for (uint32_t t = 0; t < V; t++)
-                __builtin_amdgcn_raw_buffer_store_b32(v[t], os, lane4, b + 4 * kWave * t, 0);
+            for (uint32_t t = 0; t < V; t++) __builtin_amdgcn_raw_buffer_store_b32(v[t], os, o[t], 0, 0);
         }
         return;
     }

@@ -45,7 +45,7 @@ def dev_batch(ctx, blocks, align_pad=None, rng=None):
             torch.tensor(np.array(lens, np.uint32).view(np.int32), device=dev))
 
 
-def check_against_oracle(grammar, buf, blk_off, blk_len, r, arena=False):
+def check_against_oracle(grammar, buf, blk_off, blk_len, r, arena=False, arena_fill=0):
     nrec = r.nrec.cpu().numpy()
     status = r.status.cpu().numpy()
     rec_base = r.bases(blk_off).astype(np.int64)
@@ -55,6 +55,10 @@ def check_against_oracle(grammar, buf, blk_off, blk_len, r, arena=False):
         ka = r.key_arena.cpu().numpy() if r.key_arena is not None else None
         va = r.val_arena.cpu().numpy() if r.val_arena is not None else None
         ab = r.arena_bases(blk_off).astype(np.int64)
+        # every arena byte outside the blocks' packed ranges keeps its initial
+        # value (arena_fill): no emitter writes past a run or a batch
+        ek = np.full_like(ka, arena_fill) if ka is not None else None
+        ev = np.full_like(va, arena_fill) if va is not None else None
     for b, (o, l) in enumerate(zip(blk_off, blk_len)):
         st, d, oiv = ora.decode_block(grammar, buf, int(o), int(l))
         assert status[b] == st, (b, status[b], st)
@@ -69,6 +73,14 @@ def check_against_oracle(grammar, buf, blk_off, blk_len, r, arena=False):
                 assert ka[ab[b]:ab[b] + ok.size].tobytes() == ok.tobytes(), b
             if va is not None:
                 assert va[ab[b]:ab[b] + ov.size].tobytes() == ov.tobytes(), b
+                ev[ab[b]:ab[b] + ov.size] = ov
+            if ka is not None:
+                ek[ab[b]:ab[b] + ok.size] = ok
+    if arena:
+        for got, exp in ((ka, ek), (va, ev)):
+            if got is not None:
+                bad = np.nonzero(got != exp)[0]
+                assert bad.size == 0, ("arena bytes written outside the packed ranges", bad[:8])
 
 
 def check_compaction(ctx, grammar, blk_off_host, d_off, r):
@@ -389,7 +401,7 @@ def test_scheduled_matches_unscheduled(ctx, grammar, arena):
             if x is not None:
                 assert torch.equal(x, y)
     check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
-                         d_len.cpu().numpy().view(np.uint32), b, arena=arena)
+                         d_len.cpu().numpy().view(np.uint32), b, arena=arena, arena_fill=0xFF)
 
 
 def test_decode64k_full_size(ctx):
@@ -455,7 +467,7 @@ def test_hinted_matches_plain(ctx, grammar, arena):
         if x is not None:
             assert torch.equal(x, y)
     check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
-                         d_len.cpu().numpy().view(np.uint32), b, arena=arena)
+                         d_len.cpu().numpy().view(np.uint32), b, arena=arena, arena_fill=0xFF)
 
 
 @pytest.mark.parametrize("grammar", [0, 1, 2])

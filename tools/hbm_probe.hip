@@ -230,3 +230,15 @@ extern "C" int probe_stream(int nch, const void *in, uint32_t nblk, uint32_t blk
     }
     return (int)hipGetLastError();
 }
+
+// Buffer range-check semantics: 64 lanes store 4 bytes each at voffset 4*lane,
+// soffset `so`, instruction offset 0, through a descriptor of `nrec` bytes;
+// which dwords land tells whether soffset counts in the check.
+__global__ void range_store(uint32_t *out, uint32_t nrec, uint32_t so) {
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, nrec, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(1u + threadIdx.x, r, 4 * threadIdx.x, so, 0);
+}
+extern "C" int probe_range(void *out, uint32_t nrec, uint32_t so, void *stream) {
+    hipLaunchKernelGGL(range_store, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint32_t *)out, nrec, so);
+    return (int)hipGetLastError();
+}
