@@ -83,7 +83,7 @@ def bench_sst(args, world, rank, local):
                    "builder_rule": "lsm_segment_files_host (O(files log n) host search over the "
                                    "CSR offsets), outside the timed region; layout incl. H2D",
                    "parallelism": f"dp{world} (record ranges per rank, no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "lsm_build_sst: bloom_file_kernel || sst_regions_kernel + sst_meta_kernel (forked, joined)",
+        "roofline": {"bound": "hbm", "kernel": "lsm_build_sst: sst_regions_kernel (regions + key hash) -> bloom_or_kernel (filter bits + framing)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": tsrc,

@@ -296,9 +296,10 @@ uint64_t lsm_sst_image_size_host(const uint64_t *koff, const uint64_t *voff, uin
 /* Filter block bytes for m bits: 8 + 24 + 8*ceil(m/64) (bloom.go:472-491). */
 uint64_t lsm_filter_block_size(uint64_t m);
 /* Device workspace lsm_build_sst needs for nfile files of at most
- * max_file_records records each: the bloom's binned bit positions (k u32 per
- * record) when the filter splits into two LDS slices (go-lsm's default m),
- * else a token 16 bytes. */
+ * max_file_records records each: when the filter splits into two LDS slices
+ * (go-lsm's default m), a 24-byte hash record per key (k <= 16: the key hash
+ * runs inside the region writer) or the slice-1 bit positions (k u32 per
+ * record); else a token 16 bytes. */
 size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records, uint64_t m,
                                      uint32_t k);
 
@@ -308,7 +309,9 @@ size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records, 
  * SSTable.Add (sstable.go:322-326), bloom Filter.Add (bloom.go:175-181,
  * murmur.go:245-275) and SSTable.EncodeTo (sstable.go:131-193).  The bloom
  * (m bits, k hashes; go-lsm default 1,600,000 / 16, bloom.go:79-82) is
- * built in LDS slices and its words are stored straight into each image.
+ * built in LDS slices and its words are stored straight into each image;
+ * for the default shape each key is hashed by the kernel that writes its
+ * index entry.
  * d_footer (optional) gets {dataOff, dataSize, idxOff, idxSize} per file.
  * max_file_records must be >= every file_start[f+1]-file_start[f] (it sizes
  * the grid and the workspace).  Requires m >= 1. */
