@@ -194,12 +194,29 @@ def test_sst_config3_full(ctx):
         want, _ = ora.build_sst(keys, koff, vals, voff, int(starts[f]), int(starts[f + 1]))
         o = int(sb.file_off[f])
         assert np.array_equal(out[o:o + want.size], want), f
-    # decode one image back on the GPU: IDX region + V region, positional join
-    f = 3
-    o = int(sb.file_off[f])
-    img = out[o:o + int(sb.file_size[f])]
-    rc, meta, idesc, ival, ddesc = ora.sst_decode(img)
-    assert rc == 0 and meta.ndata == 15888
+    # decode every image back on the GPU (lsm_decode_sst: IDX region + V
+    # region, positional join) straight from the build's device buffer
+    r = lsmgpu.decode_sst(ctx, sb.out, sb.file_off, sb.file_size)
+    torch.cuda.synchronize()
+    meta = r.meta_numpy()
+    assert (meta["stage"] == 0).all() and (meta["status"] == 0).all()
+    assert np.array_equal(meta["ndata"].astype(np.int64), sizes)
+    assert np.array_equal(meta["nidx"].astype(np.int64), sizes)
+    idesc = r.idx_desc.cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+    ival = r.idx_value.cpu().numpy()
+    ddesc = r.data_desc.cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+    bases = r.bases()
+    for f in (0, 3, 207):  # and against the oracle's decode of the same image
+        o = int(sb.file_off[f])
+        rc, om, oi, oiv, od = ora.sst_decode(out[o:o + int(sb.file_size[f])])
+        assert rc == 0 and om.ndata == sizes[f]
+        b = int(bases[f])
+        gi = idesc[b:b + om.nidx].copy()
+        gi["rec_off"] -= np.uint64(o)
+        assert np.array_equal(gi, oi) and np.array_equal(ival[b:b + om.nidx], oiv), f
+        gd = ddesc[b:b + om.ndata].copy()
+        gd["rec_off"] -= np.uint64(o)
+        assert np.array_equal(gd, od), f
 
 
 # ---- hash / probe ----------------------------------------------------------------
