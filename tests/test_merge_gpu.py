@@ -21,7 +21,7 @@ TOMB = lsmgpu.TOMBSTONE
 MiB2 = 2 * 1024 * 1024
 
 
-def lay_out(pairs, kv_layout, rng):
+def lay_out(pairs, kv_layout, rng, align4=False):
     """Pairs as descriptors over one byte buffer, stored in shuffled order.
     kv_layout: KV records [klen][key][vlen][value] (value desc = None);
     else keys and values apart, each after 4 bytes of padding (IDX / V
@@ -35,7 +35,7 @@ def lay_out(pairs, kv_layout, rng):
     vd = np.zeros(n, lsmgpu.DESC_DTYPE)
     for i in place:
         k, v = pairs[i]
-        gap = rng.randint(0, 3)
+        gap = 4 * rng.randint(0, 2) if align4 else rng.randint(0, 3)
         parts.append(bytes(gap))
         pos += gap
         if kv_layout:
@@ -57,9 +57,9 @@ def lay_out(pairs, kv_layout, rng):
     return buf, kd, (None if kv_layout else vd), kpos, vpos
 
 
-def run(ctx, pairs, level, threshold, kv_layout=False, seed=0):
+def run(ctx, pairs, level, threshold, kv_layout=False, seed=0, align4=False):
     rng = random.Random(seed)
-    buf, kd, vd, kpos, vpos = lay_out(pairs, kv_layout, rng)
+    buf, kd, vd, kpos, vpos = lay_out(pairs, kv_layout, rng, align4)
     dev = ctx.torch_device
     d_buf = lsmgpu.to_device_bytes(buf, dev)
     d_kd = torch.from_numpy(kd.view(np.int32).reshape(-1, 4).copy()).to(dev)
@@ -179,6 +179,37 @@ def test_gather_and_build_match_oracle_images(ctx):
             want, _ = ora.build_sst(kn, koff, vn, voff, int(starts[f]), int(starts[f + 1]), m=20_000, k=5)
             o = int(sb2.file_off[f])
             assert np.array_equal(img2[o:o + want.size], want), (kv_layout, f)
+
+
+def test_build_views_dword_aligned_values(ctx):
+    """lsm_build_sst_views when every value is dword-aligned in its source and
+    in the image (16-byte keys, value lengths a multiple of 4, as go-lsm's
+    benchmark records): the per-record copy path, against the oracle's images,
+    including waves that mix aligned and unaligned records."""
+    rng = random.Random(21)
+    pairs = [(b"k%015d" % rng.randint(0, 5000),
+              TOMB if rng.random() < 0.05 else bytes(rng.randint(0, 255) for _ in range(4 * rng.randint(0, 60))))
+             for _ in range(5000)]
+    mixed = pairs[:2500] + [(k, v + b"x") if i % 97 == 0 else (k, v) for i, (k, v) in enumerate(pairs[2500:])]
+    for ps in (pairs, mixed):
+        for kv_layout in (False, True):
+            r, d_buf, d_kd, d_vd, got, starts = run(ctx, ps, 6, 100_000, kv_layout=kv_layout, align4=True)
+            keys = b"".join(ps[i][0] for i in got)
+            vals = b"".join(ps[i][1] for i in got)
+            koff = np.concatenate([[0], np.cumsum([len(ps[i][0]) for i in got])]).astype(np.uint64)
+            voff = np.concatenate([[0], np.cumsum([len(ps[i][1]) for i in got])]).astype(np.uint64)
+            kb = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, r.out, r.nout, len(keys), None)
+            sb = lsmgpu.prepare_sst_device(ctx, kb, r.file_start, r.nfiles, m=20_000, k=5)
+            lsmgpu.build_sst_views_into(ctx, kb, sb, d_buf, d_kd, d_vd, r.out)
+            torch.cuda.synchronize()
+            img = sb.out.cpu().numpy()
+            kn, vn = np.frombuffer(keys, np.uint8), np.frombuffer(vals, np.uint8)
+            for f in range(r.nfiles):
+                want, _ = ora.build_sst(kn, koff, vn, voff, int(starts[f]), int(starts[f + 1]),
+                                        m=20_000, k=5)
+                o = int(sb.file_off[f])
+                assert int(sb.file_size[f]) == want.size
+                assert np.array_equal(img[o:o + want.size], want), (kv_layout, f)
 
 
 def test_sst_pairs_join(ctx):
