@@ -1728,7 +1728,8 @@ constexpr uint32_t kMcMaxFiles = 2048;  // LDS bounds + counters; more files: pe
 struct McWs {
     uint32_t *flag;     // [0] = 1: grouped path
     McFile *files;
-    uint32_t *hist;     // nfile + 1: counts, then exclusive offsets
+    uint32_t *hist;     // nfile + 1: candidate counts per file
+    uint32_t *off;      // nfile + 1: exclusive offsets of the files' probe lists
     uint32_t *cursor;   // nfile
     uint32_t *cand;     // nkeys
     uint64_t *hash;     // 4 * nkeys
@@ -1885,37 +1886,42 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
         if (lh[f]) atomicAdd(&w.hist[f], lh[f]);
 }
 
-__global__ __launch_bounds__(256) void mc_offsets_kernel(uint32_t nfile, McWs w) {
-    if (!w.flag[0]) return;
-    __shared__ uint32_t part[256];
-    uint32_t carry = 0;
-    for (uint32_t f0 = 0; f0 < nfile; f0 += 256) {
-        const uint32_t f = f0 + threadIdx.x;
-        const uint32_t v = f < nfile ? w.hist[f] : 0;
-        part[threadIdx.x] = v;
-        __syncthreads();
-        for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive scan in LDS
-            const uint32_t t = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-            __syncthreads();
-            part[threadIdx.x] += t;
-            __syncthreads();
-        }
-        if (f < nfile) w.hist[f] = carry + part[threadIdx.x] - v;
-        carry += part[255];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) w.hist[nfile] = carry;
-}
-
-// Same probe->workgroup mapping as mc_classify_kernel: ranks inside the
-// workgroup from LDS counters, one global reservation per (workgroup, file).
-// Each candidate's hit byte starts at 1; a filter part that finds a clear bit
-// stores 0 (every writer stores the same value, so no atomics).
 __global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nfile, uint64_t nkeys, McWs w,
                                                                      uint8_t *hit) {
-    __shared__ uint32_t lh[kMcMaxFiles];
+    __shared__ uint32_t lh[kMcMaxFiles], loff[kMcMaxFiles], part[kMcGroupThreads];
     if (!w.flag[0]) return;
-    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads) lh[f] = 0;
+    // The files' list offsets: every workgroup scans the <= 2,048 candidate
+    // counts itself (no separate offsets launch); workgroup 0 publishes them
+    // for mc_test_kernel.
+    constexpr uint32_t kPer = kMcMaxFiles / kMcGroupThreads;
+    const uint32_t t = threadIdx.x;
+    uint32_t cv[kPer], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t f = t * kPer + j;
+        cv[j] = f < nfile ? w.hist[f] : 0u;
+        sum += cv[j];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < kMcGroupThreads; d <<= 1) {  // inclusive scan in LDS
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t ex = part[t] - sum;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t f = t * kPer + j;
+        if (f < nfile) {
+            loff[f] = ex;
+            lh[f] = 0;
+            if (blockIdx.x == 0) w.off[f] = ex;
+        }
+        ex += cv[j];
+    }
+    if (blockIdx.x == 0 && t == kMcGroupThreads - 1) w.off[nfile] = part[t];
     __syncthreads();
     uint32_t c[kMcGroupPer], rk[kMcGroupPer];
 #pragma unroll
@@ -1926,7 +1932,7 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nf
     }
     __syncthreads();
     for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads)
-        if (lh[f]) lh[f] = w.hist[f] + atomicAdd(&w.cursor[f], lh[f]);
+        if (lh[f]) lh[f] = loff[f] + atomicAdd(&w.cursor[f], lh[f]);
     __syncthreads();
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
@@ -1949,7 +1955,7 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
     if (!w.flag[0]) return;
     const uint32_t f = blockIdx.x;
-    const uint32_t b0 = w.hist[f], b1 = w.hist[f + 1];
+    const uint32_t b0 = w.off[f], b1 = w.off[f + 1];
     if (b0 == b1) return;
     const McFile F = w.files[f];
     uint32_t t = b0 + threadIdx.x, i = 0;
@@ -2041,6 +2047,7 @@ McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) 
     w.flag = reinterpret_cast<uint32_t *>(take(16));
     w.files = reinterpret_cast<McFile *>(take(sizeof(McFile) * (size_t)(nfile ? nfile : 1)));
     w.hist = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
+    w.off = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
     w.cursor = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
     w.cand = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
     w.hash = reinterpret_cast<uint64_t *>(take(32 * (nkeys ? nkeys : 1)));
@@ -2377,7 +2384,6 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
         const uint32_t ggrid = (uint32_t)((nkeys + kMcGroupProbes - 1) / kMcGroupProbes);
         hipLaunchKernelGGL(mc_classify_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, d_img,
                            nfile, d_keys, d_koff, nkeys, w, d_hit);
-        hipLaunchKernelGGL(mc_offsets_kernel, dim3(1), dim3(256), 0, s, nfile, w);
         hipLaunchKernelGGL(mc_scatter_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, nfile, nkeys, w,
                            d_hit);
         hipLaunchKernelGGL(mc_test_kernel, dim3(nfile), dim3(kMcTestThreads), kMcLdsBytes, s,
