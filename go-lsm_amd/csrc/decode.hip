@@ -992,25 +992,39 @@ __global__ __launch_bounds__(kSchedThreads) void sched_scatter_kernel(const uint
                                                                      uint32_t nblk, uint32_t ntile,
                                                                      const uint32_t *hist,
                                                                      uint32_t *order) {
-    __shared__ uint32_t tot[kSchedClasses], base[kSchedClasses], h[kSchedClasses];
-    if (threadIdx.x < kSchedClasses) {
-        const uint32_t c = threadIdx.x;
+    constexpr uint32_t kScan = 128;  // classes padded to a power of two
+    static_assert(kSchedClasses <= kScan && kScan <= kSchedThreads, "one thread per class");
+    __shared__ uint32_t tot[kScan], base[kScan], h[kScan], suf[2][kScan];
+    const uint32_t t = threadIdx.x;
+    if (t < kScan) {
         uint32_t all = 0, before = 0;
-        for (uint32_t w = 0; w < ntile; w++) {
-            const uint32_t x = hist[w * kSchedClasses + c];
-            all += x;
-            before += w < blockIdx.x ? x : 0;
+        if (t < kSchedClasses) {
+            for (uint32_t w0 = 0; w0 < ntile; w0 += 4) {  // four tiles' counts in flight
+                uint32_t x[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) x[k] = w0 + k < ntile ? hist[(w0 + k) * kSchedClasses + t] : 0u;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    all += x[k];
+                    before += w0 + k < blockIdx.x ? x[k] : 0u;
+                }
+            }
         }
-        tot[c] = all;
-        base[c] = before;
-        h[c] = 0;
+        tot[t] = all;
+        base[t] = before;
+        h[t] = 0;
+        suf[0][t] = all;
     }
     __syncthreads();
-    if (threadIdx.x < kSchedClasses) {
-        uint32_t larger = 0;  // every block of a larger class comes first
-        for (uint32_t c = threadIdx.x + 1; c < kSchedClasses; c++) larger += tot[c];
-        base[threadIdx.x] += larger;
+    // every block of a larger class comes first: suffix sums over the classes
+    // (a log-step scan; a serial sum per class was 124 dependent LDS reads)
+    uint32_t sp = 0;
+    for (uint32_t d = 1; d < kScan; d <<= 1) {
+        if (t < kScan) suf[sp ^ 1][t] = suf[sp][t] + (t + d < kScan ? suf[sp][t + d] : 0u);
+        sp ^= 1;
+        __syncthreads();
     }
+    if (t < kScan) base[t] += suf[sp][t] - tot[t];
     __syncthreads();
     const uint32_t t0 = blockIdx.x * kSchedTile + threadIdx.x;
     uint32_t n[kSchedPer];
