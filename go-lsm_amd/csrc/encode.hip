@@ -1509,6 +1509,7 @@ __global__ __launch_bounds__(256) void bloom_probe_kernel(const uint64_t *words,
 // hit matrix coalesced (dwords when nfile is a multiple of 4).
 constexpr uint32_t kMcTile = 64;
 constexpr uint32_t kMcThreads = 256;
+constexpr uint32_t kMcProbeGrid = 1024;  // per-probe path: workgroups (grid-stride)
 constexpr uint32_t kMcRow = kMcTile / 4 + 1;  // dwords per out-tile row (+1: LDS banks)
 
 // Filter.Test tests hashNum locations and stops at the first clear bit; a
@@ -1585,127 +1586,132 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
     __shared__ McFile tile[kMcTile];
     if (*grouped) return;  // the files are sorted and disjoint: mc_* kernels answer
     __shared__ uint32_t sout[kMcThreads * kMcRow];
-    const uint64_t i0 = (uint64_t)blockIdx.x * kMcThreads;
-    const uint64_t i = i0 + threadIdx.x;
-    const bool act = i < nkeys;
-    const uint32_t rows = nkeys - i0 < kMcThreads ? (uint32_t)(nkeys - i0) : kMcThreads;
-    uint64_t k0 = 0, kl = 0;
-    uint64_t h[4] = {0, 0, 0, 0};
-    uint32_t kw[4] = {0, 0, 0, 0};
-    if (act) {
-        k0 = koff[i];
-        kl = koff[i + 1] - k0;
-        sum256(keys + k0, kl, h);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) kw[j] = be_word_at(keys + k0, kl, j);
-    }
-    const uint8_t *kp = keys + k0;
-    for (uint32_t f0 = 0; f0 < nfile; f0 += kMcTile) {
-        const uint32_t nt = nfile - f0 < kMcTile ? nfile - f0 : kMcTile;
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < nt; t += kMcThreads) {
-            const lsm_sst_meta &M = meta[f0 + t];
-            const uint64_t fo = file_off[f0 + t];
-            const uint8_t *base = img + fo;
-            McFile F;
-            F.ok = M.stage != 1 && M.stage != 2;
-            F.lo_len = (uint32_t)M.min_key_len;
-            F.hi_len = (uint32_t)M.max_key_len;
-            for (uint32_t j = 0; j < 4; j++) {
-                F.lo[j] = F.ok ? be_word_at(base + M.min_key_off, M.min_key_len, j) : 0;
-                F.hi[j] = F.ok ? be_word_at(base + M.max_key_off, M.max_key_len, j) : 0;
-            }
-            F.lo_at = fo + M.min_key_off;
-            F.hi_at = fo + M.max_key_off;
-            F.words_at = fo + M.filter_words_off;
-            // k from the file (no max(1, k) on a decoded filter); Test's
-            // early exit ends a probe at its first clear bit, a corrupted k
-            // beyond kMcMaxK is capped (deviations)
-            F.k = M.filter_k < kMcMaxK ? (uint32_t)M.filter_k : kMcMaxK;
-            F.m = M.filter_m;
-            F.mr = M.filter_m ? ~0ull / M.filter_m : 0;
-            F.nbits = M.filter_nbits;
-            tile[t] = F;
+    // a capped grid strides over the probes (when the grouped path answers,
+    // fewer workgroups have to start only to see the flag)
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kMcThreads; i0 < nkeys;
+         i0 += (uint64_t)gridDim.x * kMcThreads) {
+        __syncthreads();  // sout and tile of the previous rows are consumed
+        const uint64_t i = i0 + threadIdx.x;
+        const bool act = i < nkeys;
+        const uint32_t rows = nkeys - i0 < kMcThreads ? (uint32_t)(nkeys - i0) : kMcThreads;
+        uint64_t k0 = 0, kl = 0;
+        uint64_t h[4] = {0, 0, 0, 0};
+        uint32_t kw[4] = {0, 0, 0, 0};
+        if (act) {
+            k0 = koff[i];
+            kl = koff[i + 1] - k0;
+            sum256(keys + k0, kl, h);
+    #pragma unroll
+            for (uint32_t j = 0; j < 4; j++) kw[j] = be_word_at(keys + k0, kl, j);
         }
-        // a tile of decoded files in key order with disjoint ranges (level >= 1
-        // files) holds a key in at most one file: the last whose MinKey <= key
-        bool sorted = true;
-        if (threadIdx.x < nt) {
-            const McFile &A = tile[threadIdx.x];
-            // MinKey <= MaxKey too: a corrupted header with min > max breaks
-            // the order the binary search relies on
-            sorted = A.ok != 0 &&
-                     bound_cmp_fast(A.lo, A.lo_len, img + A.lo_at, A.hi, A.hi_len, img + A.hi_at) <= 0;
-            if (sorted && threadIdx.x + 1 < nt) {
-                const McFile &B = tile[threadIdx.x + 1];
-                sorted = B.ok && bound_cmp_fast(A.hi, A.hi_len, img + A.hi_at, B.lo, B.lo_len,
-                                                img + B.lo_at) < 0;
+        const uint8_t *kp = keys + k0;
+        for (uint32_t f0 = 0; f0 < nfile; f0 += kMcTile) {
+            const uint32_t nt = nfile - f0 < kMcTile ? nfile - f0 : kMcTile;
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < nt; t += kMcThreads) {
+                const lsm_sst_meta &M = meta[f0 + t];
+                const uint64_t fo = file_off[f0 + t];
+                const uint8_t *base = img + fo;
+                McFile F;
+                F.ok = M.stage != 1 && M.stage != 2;
+                F.lo_len = (uint32_t)M.min_key_len;
+                F.hi_len = (uint32_t)M.max_key_len;
+                for (uint32_t j = 0; j < 4; j++) {
+                    F.lo[j] = F.ok ? be_word_at(base + M.min_key_off, M.min_key_len, j) : 0;
+                    F.hi[j] = F.ok ? be_word_at(base + M.max_key_off, M.max_key_len, j) : 0;
+                }
+                F.lo_at = fo + M.min_key_off;
+                F.hi_at = fo + M.max_key_off;
+                F.words_at = fo + M.filter_words_off;
+                // k from the file (no max(1, k) on a decoded filter); Test's
+                // early exit ends a probe at its first clear bit, a corrupted k
+                // beyond kMcMaxK is capped (deviations)
+                F.k = M.filter_k < kMcMaxK ? (uint32_t)M.filter_k : kMcMaxK;
+                F.m = M.filter_m;
+                F.mr = M.filter_m ? ~0ull / M.filter_m : 0;
+                F.nbits = M.filter_nbits;
+                tile[t] = F;
             }
-        }
-        sorted = __syncthreads_and(sorted);
-        uint32_t cand_lo = 0, cand_hi = nt;  // files to test: [cand_lo, cand_hi)
-        if (sorted && act) {
-            uint32_t lo = 0, hi = nt;  // first t with MinKey > key
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) / 2;
-                const McFile &F = tile[mid];
-                if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0) lo = mid + 1;
-                else hi = mid;
-            }
-            cand_lo = lo ? lo - 1 : 0;
-            cand_hi = lo;
-        }
-        uint32_t pack = 0;
-        for (uint32_t t = 0; t < nt; t++) {
-            uint32_t r = 0;
-            if (act && t >= cand_lo && t < cand_hi && tile[t].ok) {
-                const McFile &F = tile[t];
-                // sstable.go:301: MinKey > key || MaxKey < key -> false
-                if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0 &&
-                    bound_cmp_fast(F.hi, F.hi_len, img + F.hi_at, kw, kl, kp) >= 0) {
-                    const uint64_t m = F.m;
-                    // hashNum 0: Test is true (bloom.go:373 loop never runs);
-                    // m == 0 with k > 0: Go's location() divides by zero and
-                    // panics, answered false here
-                    r = F.k == 0 || m != 0;
-                    // Test's answer is the AND of all k bits (its early exit
-                    // changes nothing): sixteen loads in flight at a time
-                    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
-                        uint32_t bits = 1;
-#pragma unroll
-                        for (uint32_t u = 0; u < 16; u++) {
-                            const uint32_t j = j0 + u;
-                            if (j < F.k && r) {
-                                const uint64_t x = location(h[0], h[1], h[2], h[3], j);
-                                const uint64_t p = m < (1ull << 63) ? mod_barrett(x, m, F.mr) : x % m;
-                                bits &= p < F.nbits
-                                            ? (uint32_t)(img[F.words_at + 8 * (p >> 6) + 7 - ((p & 63) >> 3)] >> (p & 7)) & 1
-                                            : 0u;
-                            }
-                        }
-                        r &= bits;
-                    }
+            // a tile of decoded files in key order with disjoint ranges (level >= 1
+            // files) holds a key in at most one file: the last whose MinKey <= key
+            bool sorted = true;
+            if (threadIdx.x < nt) {
+                const McFile &A = tile[threadIdx.x];
+                // MinKey <= MaxKey too: a corrupted header with min > max breaks
+                // the order the binary search relies on
+                sorted = A.ok != 0 &&
+                         bound_cmp_fast(A.lo, A.lo_len, img + A.lo_at, A.hi, A.hi_len, img + A.hi_at) <= 0;
+                if (sorted && threadIdx.x + 1 < nt) {
+                    const McFile &B = tile[threadIdx.x + 1];
+                    sorted = B.ok && bound_cmp_fast(A.hi, A.hi_len, img + A.hi_at, B.lo, B.lo_len,
+                                                    img + B.lo_at) < 0;
                 }
             }
-            pack |= r << (8 * (t & 3));
-            if ((t & 3) == 3 || t + 1 == nt) {
-                sout[threadIdx.x * kMcRow + t / 4] = pack;
-                pack = 0;
+            sorted = __syncthreads_and(sorted);
+            uint32_t cand_lo = 0, cand_hi = nt;  // files to test: [cand_lo, cand_hi)
+            if (sorted && act) {
+                uint32_t lo = 0, hi = nt;  // first t with MinKey > key
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) / 2;
+                    const McFile &F = tile[mid];
+                    if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0) lo = mid + 1;
+                    else hi = mid;
+                }
+                cand_lo = lo ? lo - 1 : 0;
+                cand_hi = lo;
             }
-        }
-        __syncthreads();
-        // the rows x nt sub-block of hit, coalesced
-        if ((nfile & 3) == 0) {  // every row segment starts 4-aligned (nt is a multiple of 4)
-            const uint32_t nd = nt / 4;
-            for (uint32_t x = threadIdx.x; x < rows * nd; x += kMcThreads) {
-                const uint32_t rr = x / nd, c = x % nd;
-                *reinterpret_cast<uint32_t *>(hit + (i0 + rr) * nfile + f0 + 4 * c) =
-                    sout[rr * kMcRow + c];
+            uint32_t pack = 0;
+            for (uint32_t t = 0; t < nt; t++) {
+                uint32_t r = 0;
+                if (act && t >= cand_lo && t < cand_hi && tile[t].ok) {
+                    const McFile &F = tile[t];
+                    // sstable.go:301: MinKey > key || MaxKey < key -> false
+                    if (bound_cmp_fast(F.lo, F.lo_len, img + F.lo_at, kw, kl, kp) <= 0 &&
+                        bound_cmp_fast(F.hi, F.hi_len, img + F.hi_at, kw, kl, kp) >= 0) {
+                        const uint64_t m = F.m;
+                        // hashNum 0: Test is true (bloom.go:373 loop never runs);
+                        // m == 0 with k > 0: Go's location() divides by zero and
+                        // panics, answered false here
+                        r = F.k == 0 || m != 0;
+                        // Test's answer is the AND of all k bits (its early exit
+                        // changes nothing): sixteen loads in flight at a time
+                        for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
+                            uint32_t bits = 1;
+    #pragma unroll
+                            for (uint32_t u = 0; u < 16; u++) {
+                                const uint32_t j = j0 + u;
+                                if (j < F.k && r) {
+                                    const uint64_t x = location(h[0], h[1], h[2], h[3], j);
+                                    const uint64_t p = m < (1ull << 63) ? mod_barrett(x, m, F.mr) : x % m;
+                                    bits &= p < F.nbits
+                                                ? (uint32_t)(img[F.words_at + 8 * (p >> 6) + 7 - ((p & 63) >> 3)] >> (p & 7)) & 1
+                                                : 0u;
+                                }
+                            }
+                            r &= bits;
+                        }
+                    }
+                }
+                pack |= r << (8 * (t & 3));
+                if ((t & 3) == 3 || t + 1 == nt) {
+                    sout[threadIdx.x * kMcRow + t / 4] = pack;
+                    pack = 0;
+                }
             }
-        } else {
-            for (uint32_t x = threadIdx.x; x < rows * nt; x += kMcThreads) {
-                const uint32_t rr = x / nt, c = x % nt;
-                hit[(i0 + rr) * nfile + f0 + c] = (uint8_t)(sout[rr * kMcRow + c / 4] >> (8 * (c & 3)));
+            __syncthreads();
+            // the rows x nt sub-block of hit, coalesced
+            if ((nfile & 3) == 0) {  // every row segment starts 4-aligned (nt is a multiple of 4)
+                const uint32_t nd = nt / 4;
+                for (uint32_t x = threadIdx.x; x < rows * nd; x += kMcThreads) {
+                    const uint32_t rr = x / nd, c = x % nd;
+                    *reinterpret_cast<uint32_t *>(hit + (i0 + rr) * nfile + f0 + 4 * c) =
+                        sout[rr * kMcRow + c];
+                }
+            } else {
+                for (uint32_t x = threadIdx.x; x < rows * nt; x += kMcThreads) {
+                    const uint32_t rr = x / nt, c = x % nt;
+                    hit[(i0 + rr) * nfile + f0 + c] = (uint8_t)(sout[rr * kMcRow + c / 4] >> (8 * (c & 3)));
+                }
             }
         }
     }
@@ -2389,7 +2395,8 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
         hipLaunchKernelGGL(mc_test_kernel, dim3(nfile), dim3(kMcTestThreads), kMcLdsBytes, s,
                            d_img, nfile, w, d_hit);
     }
-    hipLaunchKernelGGL(may_contain_kernel, dim3((uint32_t)grid), dim3(kMcThreads), 0, s, d_img,
+    const uint32_t pgrid = grid < kMcProbeGrid ? (uint32_t)grid : kMcProbeGrid;
+    hipLaunchKernelGGL(may_contain_kernel, dim3(pgrid), dim3(kMcThreads), 0, s, d_img,
                        d_file_off, d_meta, nfile, d_keys, d_koff, nkeys, d_hit,
                        (const uint32_t *)w.flag);
     LSM_HIP_CHECK(hipGetLastError());

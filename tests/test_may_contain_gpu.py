@@ -252,3 +252,31 @@ def test_may_contain_truncated_bitset_and_k_zero(ctx):
     at = 8 + 2 * mnl + 8
     m0[at:at + 8] = np.frombuffer(struct.pack(">Q", 0), np.uint8)  # m = 0, k = 2
     check(ctx, rng, [m0] + sorted_imgs[1:], probes, held_check=False)
+
+
+def test_may_contain_per_probe_path_many_probes(ctx):
+    """Overlapping files (the per-probe path) with more probes than one pass
+    of its capped grid covers (1,024 workgroups x 256 probes): every row of
+    the hit matrix against the oracle's batched MayContain, nfile % 4 == 0
+    (dword write-out) and != 0 (byte write-out)."""
+    rng = np.random.default_rng(77)
+    images = []
+    for f in range(5):
+        lo = int(rng.integers(0, 40_000))
+        keys = sorted({b"p%07d" % int(x) for x in rng.integers(lo, lo + 60_000, 3000)})
+        images.append(build(keys, m=20_000, k=4))
+    n = 300_000
+    probes = [b"p%07d" % int(x) for x in rng.integers(0, 110_000, n)]
+    kb, ko = csr(probes)
+    for imgs in (images[:4], images):
+        offs = np.cumsum([0] + [im.size for im in imgs[:-1]]).astype(np.uint64)
+        buf = np.concatenate(imgs)
+        d_img = lsmgpu.to_device_bytes(buf, ctx.torch_device)
+        r = lsmgpu.decode_sst(ctx, d_img, offs, np.array([im.size for im in imgs], np.uint64))
+        batch = lsmgpu.batch_to_device(ctx, kb, ko, np.zeros(1, np.uint8), np.zeros(n + 1, np.uint64))
+        hit = lsmgpu.may_contain(ctx, d_img, r, batch).cpu().numpy()
+        torch.cuda.synchronize()
+        metas = [ora.sst_decode(im)[1] for im in imgs]
+        want = ora.may_contain_batch(buf, offs, metas, kb, ko, 0, n)
+        assert np.array_equal(hit, want), np.argwhere(hit != want)[:8]
+        assert hit.any(axis=1).sum() > n // 20
