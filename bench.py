@@ -255,21 +255,11 @@ def bench_decode(args, world, rank, local):
     assert int((r.status[:nblk] != 0).sum()) == 0, "decode reported errors"
     nrec_total = int(r.nrec[:nblk].sum().item())
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record(stream)
-        step()
-        ends[i].record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(world, t1 - t0)
-
-    times = np.array([s.elapsed_time(e) for s, e in zip(starts, ends)])
+    elapsed = timed_region(world, step, args.steps)
+    # kernel time from HIP events, in passes of their own: an event pair
+    # around every launch puts a ~10 us marker gap between launches
+    # (profiles/r03_ktrace_events.txt), so the wall-timed loop has none
+    times, kern_ms = kernel_times(step, stream, args.steps)
     # the timed output is checked after the timed region: the line fails on a
     # single wrong descriptor (kv/kv.go:77-115 record chain, closed form)
     verify_decode(args, r, d_off, d_len, nblk)
@@ -286,7 +276,6 @@ def bench_decode(args, world, rank, local):
     alg = parsed + 12.0 * nblk + 16.0 * nrec_total + 8.0 * nblk
     if args.arena:
         alg += float(nrec_total) * (16 + 100) if args.config != "mixed" else parsed
-    kern_ms = float(times.mean())
     achieved = alg / (kern_ms * 1e-3) / 1e9
     wkey = f"{args.config}:{nblk}:{'arena' if args.arena else 'desc'}"
     traffic, tsrc = traffic_from_profile(wkey)
@@ -316,13 +305,7 @@ def bench_decode(args, world, rank, local):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("lsm_wal_replay (seg + stitch + compact launches)" if args.config == "wal"
-                       else "lsm_decode_blocks_scheduled (size-class bucketing + "
-                            "decode_v2_kernel<KV,8>, all launches)" if args.config == "mixed"
-                       else "decode_v2_kernel<KV,8,ARENA>" if args.arena
-                       else "decode_v2_kernel<KV,16> (lsm_decode_blocks_hinted)"
-                       if args.config == "decode64k"
-                       else "decode_v2_kernel<KV,8>"),
+            "kernel": decode_kernel_label(args),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -331,11 +314,69 @@ def bench_decode(args, world, rank, local):
             "traffic_source": tsrc,
             "alg_bytes_per_launch": int(alg),
             "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_source": KERNEL_MS_SOURCE,
             "kernel_ms_median": round(float(np.median(times)), 5),
             "kernel_ms_min": round(float(times.min()), 5),
         },
     }
     return out, (buf, blk_off, blk_len)
+
+
+def decode_kernel_label(args):
+    """The kernel (instantiation) a decode line times, from config and output
+    mode together."""
+    if args.config == "wal":
+        return "lsm_wal_replay (seg + stitch + compact launches)"
+    arena = ",ARENA" if args.arena else ""
+    if args.config == "mixed":
+        return ("lsm_decode_blocks_scheduled (size-class bucketing + "
+                f"decode_v2_kernel<KV,2{arena}>, all launches)")
+    if args.config == "decode64k":
+        return f"decode_v2_kernel<KV,16{arena}> (lsm_decode_blocks_hinted)"
+    return f"decode_v2_kernel<KV,8{arena}>"
+
+
+KERNEL_MS_SOURCE = ("HIP events around K back-to-back launches on the launch stream "
+                    "(a pass of its own); median / min from per-launch event pairs")
+
+
+def timed_region(world, step, steps):
+    """The driver contract's timed region: barrier + synchronize, exactly
+    `steps` steps, synchronize; t1 is read before the trailing barrier (rank
+    skew would otherwise be charged to every rank), the max over ranks is the
+    elapsed time.  Nothing else is enqueued inside it."""
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    return max_over_ranks(world, t1 - t0)
+
+
+def kernel_times(step, stream, steps):
+    """Average launch duration from one event pair around `steps` back-to-back
+    launches (no marker between them, as in the timed region), and per-launch
+    event pairs in a second pass for the median and minimum.
+    -> (per-launch ms array, mean ms)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    mean = e0.elapsed_time(e1) / steps
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    for i in range(steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    return np.array([s.elapsed_time(e) for s, e in zip(starts, ends)]), mean
 
 
 def verify_decode(args, r, d_off, d_len, nblk):
@@ -473,8 +514,9 @@ def bench_e2e(args, world, rank, local):
     for _ in range(steps):
         run_once()
     torch.cuda.synchronize()
+    t1 = time.perf_counter()
     barrier(world)
-    elapsed = max_over_ranks(world, time.perf_counter() - t0)
+    elapsed = max_over_ranks(world, t1 - t0)
     parsed = float(blk_len.astype(np.float64).sum())
     value = sum_over_ranks(world, parsed) * steps / elapsed / GIB
     h2d_bytes, d2h_bytes = per * slot_bytes, nrec * 16 + per * 8

@@ -64,7 +64,7 @@ def build_images(ctx, runs):
 
 
 def bench_compact(args, world, rank, local):
-    from bench import barrier, max_over_ranks, sum_over_ranks
+    from bench import barrier, max_over_ranks, sum_over_ranks, timed_region
     ctx = lsmgpu.Context(local)
     n1 = (args.blocks or 100_000) * 33
     first = rank * n1
@@ -108,15 +108,13 @@ def bench_compact(args, world, rank, local):
         step()
     torch.cuda.synchronize()
     steps = max(1, min(args.steps, 20))
+    elapsed = timed_region(world, step, steps)
+    # stage times from events in a pass of their own (markers between the
+    # stages would add their gaps to the wall-timed region)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
     for s in range(steps):
         sb, batch = step(evs[s])
     torch.cuda.synchronize()
-    barrier(world)
-    elapsed = max_over_ranks(world, time.perf_counter() - t0)
     stage_ms = {nm: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in evs]))
                 for i, nm in enumerate(ev_names)}
     in_bytes = float(file_size.astype(np.float64).sum())

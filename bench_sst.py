@@ -22,7 +22,7 @@ GIB = float(1 << 30)
 
 
 def bench_sst(args, world, rank, local):
-    from bench import barrier, max_over_ranks, sum_over_ranks, HBM_PEAK_GBS
+    from bench import barrier, max_over_ranks, sum_over_ranks, timed_region, kernel_times, HBM_PEAK_GBS
     ctx = lsmgpu.Context(local)
     n = (args.blocks or 100_000) * 33
     keys, koff, vals, voff = synth.kv_stream(n, first=rank * n)
@@ -40,20 +40,12 @@ def bench_sst(args, world, rank, local):
     for _ in range(args.warmup):
         lsmgpu.build_sst_into(ctx, batch, sb, stream=stream)
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+
+    def step():
         lsmgpu.build_sst_into(ctx, batch, sb, stream=stream)
-        e.record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    elapsed = max_over_ranks(world, time.perf_counter() - t0)
-    times = np.array([s.elapsed_time(e) for s, e in ev])
-    kern_ms = float(times.mean())
+
+    elapsed = timed_region(world, step, args.steps)
+    times, kern_ms = kernel_times(step, stream, args.steps)
     img = float(sb.file_size.astype(np.float64).sum())
     img_all = sum_over_ranks(world, img)
     nf = len(starts) - 1

@@ -22,7 +22,7 @@ GIB = float(1 << 30)
 
 
 def bench_sst_decode(args, world, rank, local):
-    from bench import barrier, max_over_ranks, sum_over_ranks, HBM_PEAK_GBS
+    from bench import barrier, max_over_ranks, sum_over_ranks, timed_region, kernel_times, HBM_PEAK_GBS
     ctx = lsmgpu.Context(local)
     one = args.config == "sstdec1"
     n = 15_888 if one else (args.blocks or 100_000) * 33
@@ -40,19 +40,12 @@ def bench_sst_decode(args, world, rank, local):
     torch.cuda.synchronize()
     meta = r.meta_numpy()
     assert (meta["stage"] == 0).all() and int(meta["nidx"].sum()) == n, "decode failed"
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+
+    def step():
         lsmgpu.decode_sst_into(ctx, sb.out, r, stream=stream)
-        e.record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    elapsed = max_over_ranks(world, time.perf_counter() - t0)
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    elapsed = timed_region(world, step, args.steps)
+    times, kern_ms = kernel_times(step, stream, args.steps)
     parsed = float(meta["data_size"].astype(np.float64).sum() +
                    meta["idx_size"].astype(np.float64).sum())
     parsed_all = sum_over_ranks(world, parsed)
@@ -114,16 +107,48 @@ def cpu_baseline_sst_decode(args, data):
     v1 = float(sum(parsed[f % nf] for f in range(done))) / t1 / GIB
     passes, tn = timed_threads(one, list(range(nf)), cpu["threads"], args.cpu_seconds)
     vn = float(parsed.sum()) * passes / tn / GIB
-    return {"value": round(vn, 4), "unit": "GiB/s", "cores": cpu["threads"], "kind": "port",
-            "sample": f"all {nf} images x {passes} passes on {cpu['threads']} threads in "
-                      f"{tn:.1f} s; 1 thread: {done} image decodes in {t1:.1f} s",
-            "value_1t": round(v1, 4), "host": cpu}
+    out = {"value": round(vn, 4), "unit": "GiB/s", "cores": cpu["threads"], "kind": "port",
+           "sample": f"all {nf} images x {passes} passes on {cpu['threads']} threads in "
+                     f"{tn:.1f} s; 1 thread: {done} image decodes in {t1:.1f} s",
+           "value_1t": round(v1, 4), "host": cpu}
+    if args.config == "sstdec1":
+        out["file_backed"] = file_backed_baseline(args, img, file_off, file_size, parsed)
+    return out
+
+
+def file_backed_baseline(args, img, file_off, file_size, parsed):
+    """config 1 from a real file the way the reference
+    reads it -- SSTable.DecodeFrom(path) + GetDataBlockFromFile(path) over an
+    unbuffered *os.File, one read(2) per length field, key and value
+    (sstable.go:87-127,214-268; ora_sst_decode_file).  The file sits in the
+    page cache (written just before), as a freshly flushed table does.
+    1 thread: the reference decodes one file per goroutine."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as ora
+    o, n = int(file_off[0]), int(file_size[0])
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "000001.sst")
+        with open(path, "wb") as f:
+            f.write(img[o:o + n].tobytes())
+        want = ora.sst_decode(img[o:o + n])[1].nidx
+        t, reps = 0.0, 0
+        while t < args.cpu_seconds / 3 or reps == 0:
+            t0 = time.perf_counter()
+            got = ora.sst_decode_file(path)
+            t += time.perf_counter() - t0
+            reps += 1
+            assert got == want, (got, want)
+    return {"value": round(float(parsed[0]) * reps / t / GIB, 5), "unit": "GiB/s", "cores": 1,
+            "kind": "port", "ms_per_file": round(t * 1e3 / reps, 3),
+            "sample": f"one {n}-byte .sst file, {want} pairs, {reps} decodes in {t:.1f} s "
+                      "(one read(2) per field, page cache)"}
 
 
 def bench_may_contain(args, world, rank, local):
     """batched SSTable.MayContain -- 1M probe keys (half
     held by the files, half not) against the 208 config-3 images."""
-    from bench import barrier, max_over_ranks, sum_over_ranks
+    from bench import barrier, max_over_ranks, sum_over_ranks, timed_region, kernel_times
     ctx = lsmgpu.Context(local)
     n = (args.blocks or 100_000) * 33
     keys, koff, vals, voff = synth.kv_stream(n, first=rank * n)
@@ -149,19 +174,12 @@ def bench_may_contain(args, world, rank, local):
     for _ in range(args.warmup):
         lsmgpu.may_contain_into(ctx, sb.out, r, probes, hit, ws=ws, stream=stream)
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+
+    def step():
         lsmgpu.may_contain_into(ctx, sb.out, r, probes, hit, ws=ws, stream=stream)
-        e.record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    elapsed = max_over_ranks(world, time.perf_counter() - t0)
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    elapsed = timed_region(world, step, args.steps)
+    times, kern_ms = kernel_times(step, stream, args.steps)
     # checked after the timed region: host work between warmup and timing
     # left the GPU idle long enough to add ~20 ms of wake-up to the first step
     rows = hit.sum(dim=1).cpu().numpy()

@@ -5,6 +5,7 @@
 #include "common.h"
 
 extern "C" int lsm_abi_version(void) { return LSM_ABI_VERSION; }
+extern "C" int lsm_input_slack(void) { return LSM_INPUT_SLACK; }
 
 extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
     if (!out) return LSM_EINVAL;

@@ -58,6 +58,18 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return (uint64_t)hi << 32 | lo;
 }
 
+// XCD-contiguous unit order.  Workgroups are dealt round-robin over the 8
+// XCDs (observed placement, MI355X_MICROARCH.md "Workgroup dispatch"): WG i
+// runs on the XCD of i % 8.  Mapping WG i to unit xcd_linear(i, n) gives each
+// XCD one contiguous eighth of the units, so the per-unit metadata lines and
+// the partial output lines of neighbouring units meet in one XCD's L2
+// instead of being fetched (and written back) by all eight.  A bijection on
+// [0, n) for any n; correctness never depends on the placement.
+__device__ __forceinline__ uint32_t xcd_linear(uint32_t i, uint32_t n) {
+    const uint32_t q = n >> 3, r = n & 7, x = i & 7, k = i >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
 // Raw buffer over [base, base+bytes): loads past `bytes` return 0 and touch no memory.
 __device__ __forceinline__ rsrc_t make_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes,

@@ -822,7 +822,13 @@ template <int G, uint32_t NCH, bool ARENA>
 __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
     __shared__ uint32_t tab[ARENA ? 129 : 1];
-    const uint32_t b = a.order ? uni(a.order[blockIdx.x]) : blockIdx.x;
+    // a caller's launch order (largest first) is kept as given.  Large blocks
+    // (the 16 KiB ring) go XCD-contiguous: 64 KiB blocks 87.9 -> 86.2 us.
+    // Small blocks keep the dispatch order: XCD-contiguous 4 KiB blocks
+    // measured 76.7 -> 80.0 us (eight separate address streams; the chip
+    // streams one interleaved window faster).
+    const uint32_t b = a.order ? uni(a.order[blockIdx.x])
+                               : NCH >= 16 ? xcd_linear(blockIdx.x, a.nblk) : blockIdx.x;
     const uint64_t off = uni64(a.blk_off[b]);
     const uint32_t n = uni(a.blk_len[b]);
     const bool lin = ((off & 15) + (uint64_t)n + 15) / 16 * 16 <= NCH * kChunk;
@@ -1128,7 +1134,8 @@ __device__ void sst_parse(const ImgReader &R, uint64_t n, SstWork &w) {
     const uint64_t L = R.u64(pos);
     if (L > n - pos - 8 || L < 24) { m.stage = LSM_SST_FILTER; return; }
     const uint64_t fm = R.u64be(pos + 8), fk = R.u64be(pos + 16), nb = R.u64be(pos + 24);
-    if ((nb + 63) / 64 > (L - 24) / 8) { m.stage = LSM_SST_FILTER; return; }
+    // words needed for nb bits, without the (nb + 63) overflow (nb near 2^64)
+    if (nb / 64 + ((nb & 63) != 0) > (L - 24) / 8) { m.stage = LSM_SST_FILTER; return; }
     m.filter_m = fm;
     m.filter_k = fk;
     m.filter_nbits = nb;

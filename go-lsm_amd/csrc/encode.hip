@@ -1976,7 +1976,7 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     // holding at least one filter byte (no fault).  Lanes past the end load
     // the last chunk again into LDS the filter does not use.
     const uint8_t *src = img + F.words_at;
-    const uint64_t nb = 8 * ((F.nbits + 63) / 64);
+    const uint64_t nb = 8 * (F.nbits / 64 + ((F.nbits & 63) != 0));
     const uint32_t delta = (uint32_t)((uintptr_t)src & 15);
     const uint64_t in_lds = nb < kMcLdsBytes - 16 ? nb : kMcLdsBytes - 16;  // bytes [0, in_lds)
     const uint4 *src16 = reinterpret_cast<const uint4 *>(src - delta);
@@ -2283,20 +2283,29 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
 
 
     hipStream_t rs = forked ? ctx->side : s;  // the regions' stream
+    // Past the fork every error still joins: kernels already queued on the
+    // side stream must be ordered before the caller's stream (which may free
+    // the outputs once the call returns an error).
+    int rc = 0;
+#define LSM_TRY(expr)                                   \
+    do {                                                \
+        const hipError_t _e = (expr);                   \
+        if (_e != hipSuccess && rc == 0) rc = -(1000 + (int)_e); \
+    } while (0)
     if (chunks) {
         const uint32_t rspans = (max_file_records + kRegSpanRecs - 1) / kRegSpanRecs;
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
-        LSM_HIP_CHECK(hipGetLastError());
-        if (views) {
+        LSM_TRY(hipGetLastError());
+        if (views && rc == 0) {
             hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, rs, a,
                                *views);
-            LSM_HIP_CHECK(hipGetLastError());
+            LSM_TRY(hipGetLastError());
         }
     }
-    if (!split) {
+    if (rc == 0 && !split) {
         hipLaunchKernelGGL(sst_meta_kernel, dim3(nfile), dim3(kWave), 0, rs, a);
-        LSM_HIP_CHECK(hipGetLastError());
-    } else {
+        LSM_TRY(hipGetLastError());
+    } else if (rc == 0) {
         BloomOrArgs bo{};
         bo.file_start = d_file_start;
         bo.rec = a.hrec;
@@ -2309,13 +2318,14 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         bo.out = d_out;
         bo.file_off = d_file_off;
         hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo, a);
-        LSM_HIP_CHECK(hipGetLastError());
+        LSM_TRY(hipGetLastError());
     }
-    if (forked) {  // join: the caller's stream waits for the regions
-        LSM_HIP_CHECK(hipEventRecord(ctx->join, ctx->side));
-        LSM_HIP_CHECK(hipStreamWaitEvent(s, ctx->join, 0));
+    if (forked) {  // join (also after an error): the caller's stream waits for the regions
+        LSM_TRY(hipEventRecord(ctx->join, ctx->side));
+        LSM_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     }
-    return 0;
+#undef LSM_TRY
+    return rc;
 }
 
 extern "C" int lsm_build_sst(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,

@@ -11,8 +11,11 @@
 // whatever the heap's array history makes it (about one duplicate group in
 // seven differs from input order on compaction-shaped inputs).
 // merge.go:41 states the contract -- the newest pair, first in the input,
-// wins -- and merge_test.go:25,53 checks it; this path implements that
-// contract: equal keys leave in input order.
+// wins -- and merge_test.go:25,53 checks it; LSM_TIE_INPUT implements that
+// contract: equal keys leave in input order.  LSM_TIE_GOHEAP reproduces the
+// heap exactly: the sort below gives dense key ranks, one host thread replays
+// heap.Push / heap.Pop over them (a single dependent chain), and the pop
+// order replaces the sorted order before steps 3-5.
 //
 // GPU shape:
 //   1. key statistics in one pass (max / min key length; per 8-byte chunk the
@@ -277,6 +280,15 @@ __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, c
     if (!gs) gs = !keys_equal(m.bytes, v, view(m, perm[j - 1]));
     const bool wr = level < 6 || !is_tombstone(m.bytes, v);
     flags[j] = (uint8_t)((gs ? 1 : 0) | (wr ? 2 : 0));
+}
+
+// eq[j] = 1 when sorted position j holds the same key as j - 1 (plain key
+// equality: for container/heap "" equals "", merge.go:21-23's Less is key <)
+__global__ __launch_bounds__(kMergeThreads) void merge_eq_kernel(MergeIn m, const uint32_t *perm,
+                                                                 uint8_t *eq) {
+    const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
+    if (j >= m.n) return;
+    eq[j] = j > 0 && keys_equal(m.bytes, view(m, perm[j]), view(m, perm[j - 1]));
 }
 
 // candidate = the first pair of its group that may be written; the backward
@@ -825,9 +837,54 @@ MergeWs merge_ws_layout(uint8_t *base, uint32_t n) {
 uint32_t grid_for(uint64_t n) { return (uint32_t)((n + kMergeThreads - 1) / kMergeThreads); }
 
 }  // namespace
+
+// container/heap's pop order (Go heap.go) over dense key ranks: heap.Push of
+// pairs 0 .. n-1 (append + up), then heap.Pop until empty (swap(0, n-1),
+// down(0, n-1), take the last), with Less(i, j) = rank[i] < rank[j] -- the
+// order merge.go:47-66 pops in, equal keys included.  Entries carry
+// rank << 32 | index, so one load serves the compare and the move.  One host
+// thread: the heap's history is one dependent chain.
+void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order) {
+    std::vector<uint64_t> h(n ? n : 1);
+    for (uint32_t i = 0; i < n; i++) {  // Push: append, up(h, i)
+        const uint64_t x = (uint64_t)rank[i] << 32 | i;
+        uint32_t j = i;
+        while (j > 0) {
+            const uint32_t p = (j - 1) / 2;
+            if (!((x >> 32) < (h[p] >> 32))) break;
+            h[j] = h[p];
+            j = p;
+        }
+        h[j] = x;
+    }
+    for (uint32_t r = n; r > 0; r--) {  // Pop: swap(0, r-1), down(0, r-1)
+        const uint64_t top = h[0], x = h[r - 1];
+        const uint32_t m = r - 1;
+        uint32_t i = 0;
+        for (;;) {
+            const uint32_t j1 = 2 * i + 1;
+            if (j1 >= m) break;
+            uint32_t j = j1;
+            if (j1 + 1 < m && (h[j1 + 1] >> 32) < (h[j1] >> 32)) j = j1 + 1;
+            if (!((h[j] >> 32) < (x >> 32))) break;
+            h[i] = h[j];
+            i = j;
+        }
+        if (m) h[i] = x;
+        h[m] = top;
+        order[n - r] = (uint32_t)top;
+    }
+}
+
 }  // namespace lsm
 
 using namespace lsm;
+
+extern "C" int lsm_goheap_pop_order_host(const uint32_t *rank, uint64_t n, uint32_t *order) {
+    if (n >= 0xFFFFFFFFull || (n && (!rank || !order))) return LSM_EINVAL;
+    goheap_pop_order(rank, (uint32_t)n, order);
+    return 0;
+}
 
 static_assert(sizeof(MergeFile) == 16, "MergeFile layout");
 static_assert(sizeof(SumPair) == 16, "SumPair layout");
@@ -837,11 +894,13 @@ extern "C" size_t lsm_merge_kvs_workspace_bytes(uint64_t n) {
     return merge_ws_layout(nullptr, (uint32_t)n).total;
 }
 
-extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
-                             const lsm_rec_desc *d_val_desc, uint64_t n, int level,
-                             uint64_t threshold, uint32_t *d_out, uint64_t *d_file_start,
-                             uint64_t *h_counts, void *d_ws, size_t ws_bytes, void *stream) {
+extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
+                                 const lsm_rec_desc *d_key_desc, const lsm_rec_desc *d_val_desc,
+                                 uint64_t n, int level, uint64_t threshold, int tie,
+                                 uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts,
+                                 void *d_ws, size_t ws_bytes, void *stream) {
     if (!ctx || !h_counts || threshold == 0 || n >= 0xFFFFFFFFull) return LSM_EINVAL;
+    if (tie != LSM_TIE_INPUT && tie != LSM_TIE_GOHEAP) return LSM_EINVAL;
     if (n && (!d_bytes || !d_key_desc || !d_out || !d_ws)) return LSM_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     h_counts[0] = h_counts[1] = 0;
@@ -934,6 +993,30 @@ extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec
                            w.perm[cur], N);
     const uint32_t *perm = w.perm[cur];
 
+    if (tie == LSM_TIE_GOHEAP) {
+        // container/heap's own tie order: dense key ranks from the sorted
+        // order (equal-to-predecessor flags on the device), the heap's
+        // push / pop history replayed over the ranks on this thread, and
+        // its pop order -- sorted by key, equal keys as the heap pops them
+        // -- becomes the sorted order the steps below walk
+        hipLaunchKernelGGL(merge_eq_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m, perm,
+                           w.flags);
+        LSM_HIP_CHECK(hipGetLastError());
+        std::vector<uint32_t> hperm(N), rank(N), order(N);
+        std::vector<uint8_t> eq(N);
+        LSM_HIP_CHECK(hipMemcpyAsync(hperm.data(), perm, 4ull * N, hipMemcpyDeviceToHost, s));
+        LSM_HIP_CHECK(hipMemcpyAsync(eq.data(), w.flags, N, hipMemcpyDeviceToHost, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));
+        uint32_t g = 0;
+        for (uint32_t j = 0; j < N; j++) {
+            g += (j > 0 && !eq[j]) ? 1u : 0u;
+            rank[hperm[j]] = g;
+        }
+        goheap_pop_order(rank.data(), N, order.data());
+        LSM_HIP_CHECK(hipMemcpyAsync(w.perm[cur], order.data(), 4ull * N, hipMemcpyHostToDevice, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));  // `order` is freed on return
+    }
+
     // 3. groups and candidates; 4. sums and the file walk; 5. emit
     hipLaunchKernelGGL(merge_flags_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m, perm,
                        level, w.flags);
@@ -957,6 +1040,14 @@ extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec
     h_counts[0] = c4[0];
     h_counts[1] = c4[1];
     return 0;
+}
+
+extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                             const lsm_rec_desc *d_val_desc, uint64_t n, int level,
+                             uint64_t threshold, uint32_t *d_out, uint64_t *d_file_start,
+                             uint64_t *h_counts, void *d_ws, size_t ws_bytes, void *stream) {
+    return lsm_merge_kvs_tie(ctx, d_bytes, d_key_desc, d_val_desc, n, level, threshold,
+                             LSM_TIE_INPUT, d_out, d_file_start, h_counts, d_ws, ws_bytes, stream);
 }
 
 extern "C" size_t lsm_gather_kvs_workspace_bytes(uint64_t nout) {

@@ -481,7 +481,7 @@ Error Filter::DecodeFrom(Reader &r) {
     r.Skip(L);
     if (L < 24) return Error("unexpected EOF");
     const uint64_t m = ld64be(p), k = ld64be(p + 8), nbits = ld64be(p + 16);
-    const uint64_t nw = (nbits + 63) / 64;
+    const uint64_t nw = nbits / 64 + ((nbits & 63) != 0);  // no (nbits + 63) overflow
     if (nw > (L - 24) / 8) return Error("unexpected EOF");
     m_ = m;
     k_ = k;

@@ -34,6 +34,7 @@ class DecodeOut(ctypes.Structure):
 # name -> (restype, argtypes)
 SIGNATURES = {
     "lsm_abi_version": (ctypes.c_int, []),
+    "lsm_input_slack": (ctypes.c_int, []),
     "lsm_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "lsm_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "lsm_ctx_num_cus": (ctypes.c_int, [ctypes.c_void_p]),
@@ -105,6 +106,11 @@ SIGNATURES = {
                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
                                      c_u64p, c_u64p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_void_p]),
+    "lsm_merge_kvs_tie": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.c_int, ctypes.c_void_p, c_u64p, c_u64p,
+                                         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_goheap_pop_order_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "lsm_gather_kvs_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint64]),
     "lsm_gather_kvs": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_uint64, c_u8p, c_u64p, c_u8p,
@@ -132,6 +138,9 @@ SIGNATURES = {
     "lsm_stream_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
+ABI_VERSION = 3   # LSM_ABI_VERSION this binding is written against
+INPUT_SLACK = 32  # LSM_INPUT_SLACK: device inputs are padded by this much
+
 _lib = None
 
 
@@ -149,6 +158,10 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.lsm_abi_version() != ABI_VERSION or lib.lsm_input_slack() != INPUT_SLACK:
+        raise RuntimeError(
+            f"{LIB_PATH}: ABI {lib.lsm_abi_version()} / input slack {lib.lsm_input_slack()}, "
+            f"this binding expects ABI {ABI_VERSION} / slack {INPUT_SLACK}: rebuild")
     _lib = lib
     return lib
 

@@ -45,7 +45,7 @@ def _stream_handle(stream: Optional[torch.cuda.Stream]):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-INPUT_SLACK = 32  # LSM_INPUT_SLACK, include/lsm_gpu.h
+INPUT_SLACK = _lib.INPUT_SLACK  # LSM_INPUT_SLACK, include/lsm_gpu.h (checked at load)
 
 
 def pad16(n: int) -> int:
@@ -236,9 +236,12 @@ def decode_into(ctx: Context, grammar: int, d_in: torch.Tensor, blk_off: torch.T
     """lsm_decode_blocks into preallocated outputs (asynchronous).  With a
     `schedule` workspace (schedule_workspace()): lsm_decode_blocks_scheduled,
     the blocks launched largest first (for batches whose sizes vary).  With
-    `max_blk_len`: lsm_decode_blocks_hinted (the ring chosen for that bound)."""
+    `max_blk_len`: lsm_decode_blocks_hinted (the ring chosen for that bound).
+    The two are exclusive: the scheduled path picks its own (2 KiB) ring."""
+    if max_blk_len is not None and schedule is not None:
+        raise ValueError("decode_into: pass either schedule or max_blk_len, not both")
     out = _decode_out(r)
-    if max_blk_len is not None and schedule is None:
+    if max_blk_len is not None:
         _lib.check(ctx.lib.lsm_decode_blocks_hinted(
             ctx.handle, grammar, _ptr(d_in), _ptr(blk_off), _ptr(blk_len), int(blk_off.numel()),
             int(max_blk_len), ctypes.byref(out), _stream_handle(stream)), "lsm_decode_blocks_hinted")
@@ -609,25 +612,39 @@ def alloc_merge(ctx: Context, n: int) -> Merge:
                  workspace=torch.empty(ws, dtype=torch.uint8, device=dev), n=n)
 
 
+TIE_INPUT, TIE_GOHEAP = 0, 1  # enum lsm_tie
+
+
 def merge_kvs_into(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
                    val_desc: Optional[torch.Tensor], r: Merge, level: int = 1,
-                   threshold: int = MAX_SSTABLE_SIZE, stream=None) -> Merge:
+                   threshold: int = MAX_SSTABLE_SIZE, stream=None, tie: int = TIE_INPUT) -> Merge:
     """CompactAndMergeKVs (merge.go:42-94) over pairs given as descriptors
-    (key: IDX/KV descriptor, value: V descriptor or None for KV records)."""
+    (key: IDX/KV descriptor, value: V descriptor or None for KV records).
+    tie=TIE_GOHEAP: equal keys in container/heap's pop order (exact)."""
     counts = np.zeros(2, np.uint64)
-    _lib.check(ctx.lib.lsm_merge_kvs(
-        ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), r.n, level, threshold,
+    _lib.check(ctx.lib.lsm_merge_kvs_tie(
+        ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), r.n, level, threshold, tie,
         _ptr(r.out), _ptr(r.file_start), counts.ctypes.data, _ptr(r.workspace),
-        r.workspace.numel(), _stream_handle(stream)), "lsm_merge_kvs")
+        r.workspace.numel(), _stream_handle(stream)), "lsm_merge_kvs_tie")
     r.nout, r.nfiles = int(counts[0]), int(counts[1])
     return r
 
 
 def merge_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
               val_desc: Optional[torch.Tensor], level: int = 1,
-              threshold: int = MAX_SSTABLE_SIZE, stream=None) -> Merge:
+              threshold: int = MAX_SSTABLE_SIZE, stream=None, tie: int = TIE_INPUT) -> Merge:
     r = alloc_merge(ctx, int(key_desc.shape[0]))
-    return merge_kvs_into(ctx, d_bytes, key_desc, val_desc, r, level, threshold, stream)
+    return merge_kvs_into(ctx, d_bytes, key_desc, val_desc, r, level, threshold, stream, tie)
+
+
+def goheap_pop_order(ctx_or_lib, rank: np.ndarray) -> np.ndarray:
+    """lsm_goheap_pop_order_host: container/heap's pop order over key ranks."""
+    lib = ctx_or_lib.lib if isinstance(ctx_or_lib, Context) else ctx_or_lib
+    rank = np.ascontiguousarray(rank, dtype=np.uint32)
+    order = np.zeros(max(rank.size, 1), np.uint32)
+    _lib.check(lib.lsm_goheap_pop_order_host(rank.ctypes.data, rank.size, order.ctypes.data),
+               "lsm_goheap_pop_order_host")
+    return order[:rank.size]
 
 
 def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,

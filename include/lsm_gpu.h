@@ -5,8 +5,10 @@
  * the Go methods it replaces are cited per entry point.  Plain pointers and
  * sizes only; `stream` is an opaque hipStream_t (NULL = default stream).
  * Every launch entry point is asynchronous on `stream`, performs no device
- * allocation and no host synchronisation (hipGraph-capturable); the caller
- * owns every buffer and the library keeps no pointer after the call returns.
+ * allocation and no host synchronisation (hipGraph-capturable) -- except
+ * lsm_merge_kvs, which synchronizes `stream` (its radix passes are chosen
+ * from key statistics read back to the host); the caller owns every buffer
+ * and the library keeps no pointer after the call returns.
  *
  * Device input buffers (blocks, images, logs, key and value arenas) must be
  * readable up to LSM_INPUT_SLACK bytes past the next multiple of 16 bytes
@@ -28,7 +30,9 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 2
+/* v3: the input slack grew from 16 to 32 bytes (a binding built for v2 pads
+ * too little); lsm_input_slack() reports it at run time. */
+#define LSM_ABI_VERSION 3
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
 /* Record grammars (all fixed-width little-endian). */
@@ -100,6 +104,8 @@ typedef struct lsm_ctx lsm_ctx;
 /* ---- context ------------------------------------------------------------ */
 
 int lsm_abi_version(void);
+/* LSM_INPUT_SLACK of the loaded library: a binding checks it at load time. */
+int lsm_input_slack(void);
 /* One context per goroutine / OS thread (callers are concurrent goroutines,
  * sstable_test.go:379-400); no hidden global mutable state. */
 int lsm_ctx_create(int device, lsm_ctx **out);
@@ -364,7 +370,9 @@ int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint
  *
  * Pairs leave in key order (Go string order, bytewise); equal keys leave in
  * input order -- merge.go:41's contract, "the newest pair comes first and
- * wins" (container/heap's own tie order is unspecified).  Per
+ * wins".  lsm_merge_kvs_tie with LSM_TIE_GOHEAP reproduces container/heap's
+ * own tie order instead (the reference's exact output; a host replay of the
+ * heap over device-computed key ranks).  Per
  * pair, as merge.go:57-85: a key equal to the last written non-empty key is
  * skipped; a tombstone (kv.DeletedValue) is dropped when level >= 6
  * (maxSSTableLevel); otherwise it is written; a file is flushed when the
@@ -377,6 +385,19 @@ int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint
  * n + 1 entries), d_file_start[nfiles] = nout; h_counts (host) = {nout, nfiles}.
  * Synchronizes the stream (the radix passes are chosen from key statistics). */
 size_t lsm_merge_kvs_workspace_bytes(uint64_t n);
+enum lsm_tie {
+    LSM_TIE_INPUT = 0,   /* equal keys in input order (merge.go:41's contract)              */
+    LSM_TIE_GOHEAP = 1,  /* equal keys in container/heap's pop order (merge.go:47-66, exact) */
+};
+/* lsm_merge_kvs = lsm_merge_kvs_tie(..., LSM_TIE_INPUT, ...).  Same workspace. */
+int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                      const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
+                      int tie, uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts,
+                      void *d_ws, size_t ws_bytes, void *stream);
+/* container/heap's pop order over dense key ranks (host, no device): Push of
+ * 0 .. n-1, then Pop until empty, Less = rank <; order[j] = the j-th popped
+ * index.  What LSM_TIE_GOHEAP replays. */
+int lsm_goheap_pop_order_host(const uint32_t *rank, uint64_t n, uint32_t *order);
 int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
                   const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
                   uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts, void *d_ws,

@@ -294,7 +294,8 @@ int ora_filter_decode(const uint8_t *in, uint64_t n, uint64_t *m, uint64_t *k, u
     *m = ld_u64be(p);
     *k = ld_u64be(p + 8);
     *nbits = ld_u64be(p + 16);
-    uint64_t nw = (*nbits + 63) / 64;
+    /* words stored for nbits bits, without the (nbits + 63) overflow */
+    uint64_t nw = *nbits / 64 + ((*nbits & 63) != 0);
     if (nw > (L - 24) / 8) return -4;           /* bitset.ReadFrom words short   */
     if (words) {
         if (nw > words_cap) return -5;
@@ -656,4 +657,147 @@ void ora_may_contain_batch(const uint8_t *img, const uint64_t *file_off, const o
             hit[(i - k0) * nfile + f] = r;
         }
     }
+}
+
+/* ---- config 1 from a file, the reference's syscall pattern --------------- */
+/* SSTable.DecodeFrom(path) (sstable.go:87-127) then GetDataBlockFromFile(path)
+ * (sstable.go:227-268) over an unbuffered *os.File: every binary.Read and
+ * io.ReadFull is one read(2) of exactly the field (Header keys header.go:40-52
+ * via Key.DecodeFrom kv.go:124-139; the filter length and block bloom.go:
+ * 453-469; the footer's two 16-byte handles footer.go:58-86 after a Stat and
+ * a Seek; per index entry 4 + key + 8 bytes index.go:70-98; per value 4 +
+ * value bytes data.go:58-76 under io.LimitReader), a fresh heap buffer per key
+ * and value, append-grown entry slices and the positional join into an
+ * append-grown pair slice.  Test infrastructure: the file-backed CPU
+ * baseline of config 1.  -> pairs, or < 0. */
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+static int rd_full(int fd, void *p, uint64_t n) {  /* io.ReadFull: one read(2) */
+    uint8_t *q = (uint8_t *)p;
+    while (n) {
+        const ssize_t r = read(fd, q, n);
+        if (r <= 0) return -1;
+        q += r;
+        n -= (uint64_t)r;
+    }
+    return 0;
+}
+
+typedef struct { uint8_t *p; uint32_t n; } ora_buf;
+typedef struct { ora_buf *a; uint64_t len, cap; } ora_bufvec;
+
+static void bv_push(ora_bufvec *v, ora_buf b) {     /* Go append growth */
+    if (v->len == v->cap) {
+        v->cap = v->cap ? (v->cap < 256 ? 2 * v->cap : v->cap + v->cap / 4) : 1;
+        v->a = (ora_buf *)realloc(v->a, v->cap * sizeof(ora_buf));
+    }
+    v->a[v->len++] = b;
+}
+
+static void bv_free(ora_bufvec *v) {
+    for (uint64_t i = 0; i < v->len; i++) free(v->a[i].p);
+    free(v->a);
+}
+
+static int rd_key(int fd, ora_buf *k) {             /* Key.DecodeFrom kv.go:124-139 */
+    uint32_t kl;
+    if (rd_full(fd, &kl, 4)) return -1;
+    k->p = (uint8_t *)malloc(kl ? kl : 1);
+    k->n = kl;
+    return rd_full(fd, k->p, kl);
+}
+
+int64_t ora_sst_decode_file(const char *path) {
+    /* SSTable.DecodeFrom: header, filter, footer, index */
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return -1;
+    ora_buf mn = {0}, mx = {0};
+    int64_t rc = -2;
+    ora_bufvec ikeys = {0};
+    uint64_t *ioffs = NULL, nio = 0, cio = 0;
+    int64_t fo[4];
+    if (rd_key(fd, &mn) || rd_key(fd, &mx)) goto out;
+    uint64_t L;
+    if (rd_full(fd, &L, 8)) goto out;
+    uint8_t *fb = (uint8_t *)malloc(L ? L : 1);
+    if (rd_full(fd, fb, L) || L < 24) { free(fb); goto out; }
+    {   /* UnmarshalBinary: m, k, then the bitset words into a fresh slice */
+        const uint64_t nb = ld_u64be(fb + 16), nw = nb / 64 + ((nb & 63) != 0);
+        if (nw > (L - 24) / 8) { free(fb); goto out; }
+        uint64_t *words = (uint64_t *)malloc((nw ? nw : 1) * 8);
+        for (uint64_t i = 0; i < nw; i++) words[i] = ld_u64be(fb + 24 + 8 * i);
+        free(words);
+        free(fb);
+    }
+    struct stat st;
+    if (fstat(fd, &st) || st.st_size < 32 || lseek(fd, st.st_size - 32, SEEK_SET) < 0) goto out;
+    if (rd_full(fd, fo, 16) || rd_full(fd, fo + 2, 16)) goto out;  /* two Handles */
+    if (fo[2] < 0 || fo[3] < 0 || lseek(fd, fo[2], SEEK_SET) < 0) goto out;
+    for (int64_t tot = 0; tot < fo[3];) {               /* IndexBlock.DecodeFrom */
+        ora_buf k;
+        if (rd_key(fd, &k)) goto out;
+        bv_push(&ikeys, k);
+        int64_t o;
+        if (rd_full(fd, &o, 8)) goto out;
+        if (nio == cio) {
+            cio = cio ? (cio < 256 ? 2 * cio : cio + cio / 4) : 1;
+            ioffs = (uint64_t *)realloc(ioffs, cio * 8);
+        }
+        ioffs[nio++] = (uint64_t)o;
+        tot += 4 + (int64_t)k.n + 8;
+        if (tot > fo[3]) goto out;
+    }
+    close(fd);
+    /* GetDataBlockFromFile: open, DecodeDataBlock, GetKeyValuePairs */
+    fd = open(path, O_RDONLY);
+    if (fd < 0) { fd = -1; goto out; }
+    ora_bufvec vals = {0};
+    if (fo[0] < 0 || lseek(fd, fo[0], SEEK_SET) < 0) goto out;
+    {
+        uint64_t left = fo[1] > 0 ? (uint64_t)fo[1] : ~0ull;  /* io.LimitReader */
+        for (;;) {                                      /* DataBlock.DecodeFrom */
+            uint32_t vl;
+            uint64_t got = 0;
+            while (got < 4 && left) {                   /* binary.Read: ReadFull of 4 */
+                const uint64_t want = 4 - got < left ? 4 - got : left;
+                const ssize_t r = read(fd, (uint8_t *)&vl + got, want);
+                if (r <= 0) break;
+                got += (uint64_t)r;
+                left -= (uint64_t)r;
+            }
+            if (got == 0) break;                        /* io.EOF: a clean stop */
+            if (got < 4 || left < vl) { bv_free(&vals); goto out; }
+            ora_buf v = {(uint8_t *)malloc(vl ? vl : 1), vl};
+            if (rd_full(fd, v.p, vl)) { free(v.p); bv_free(&vals); goto out; }
+            left -= vl;
+            bv_push(&vals, v);
+        }
+    }
+    if (vals.len == 0 || ikeys.len == 0) rc = 0;
+    else if (vals.len != ikeys.len) rc = -3;            /* mismatched entries */
+    else {
+        typedef struct { ora_buf k, v; } pair;          /* pairs := make(.., 0); append */
+        pair *pairs = NULL;
+        uint64_t np = 0, cp = 0;
+        for (uint64_t i = 0; i < vals.len; i++) {
+            if (np == cp) {
+                cp = cp ? (cp < 256 ? 2 * cp : cp + cp / 4) : 1;
+                pairs = (pair *)realloc(pairs, cp * sizeof(pair));
+            }
+            pairs[np].k = ikeys.a[i];
+            pairs[np++].v = vals.a[i];
+        }
+        free(pairs);
+        rc = (int64_t)np;
+    }
+    bv_free(&vals);
+out:
+    if (fd >= 0) close(fd);
+    free(mn.p);
+    free(mx.p);
+    bv_free(&ikeys);
+    free(ioffs);
+    return rc;
 }

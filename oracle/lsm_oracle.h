@@ -188,6 +188,8 @@ uint64_t ora_merge_kvs(const uint8_t *bytes, const uint64_t *koff, const uint32_
 /* Decode blocks the way the Go path does: a fresh heap buffer per key and
  * per value, append-grown record slices; `threads` pthreads over a static
  * block partition.  Returns total records decoded. */
+/* config 1 from a file with the reference's read(2)-per-field pattern -> pairs, < 0 on error */
+int64_t ora_sst_decode_file(const char *path);
 uint64_t ora_bench_decode_golike(int grammar, const uint8_t *base, const uint64_t *blk_off,
                                  const uint32_t *blk_len, uint64_t nblk, int threads);
 

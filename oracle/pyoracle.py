@@ -63,6 +63,7 @@ def lib():
         "ora_sst_decode": (ctypes.c_int, [vp, u64, ctypes.POINTER(SstMeta), vp, vp, u64, vp,
                                           u64]),
         "ora_bench_decode_golike": (u64, [ctypes.c_int, vp, vp, vp, u64, ctypes.c_int]),
+        "ora_sst_decode_file": (ctypes.c_int64, [ctypes.c_char_p]),
         "ora_merge_kvs": (u64, [vp, vp, vp, vp, vp, u64, ctypes.c_int, u64, ctypes.c_int, vp, vp,
                                 vp]),
     }
@@ -292,6 +293,12 @@ def bench_decode_golike(grammar, buf, blk_off, blk_len, threads=1):
     blk_len = np.ascontiguousarray(blk_len, dtype=np.uint32)
     return lib().ora_bench_decode_golike(grammar, _p(buf), _p(blk_off), _p(blk_len),
                                          blk_off.size, threads)
+
+
+def sst_decode_file(path):
+    """SSTable.DecodeFrom + GetDataBlockFromFile from a file with one read(2)
+    per field (the reference's *os.File pattern) -> pairs, or < 0."""
+    return int(lib().ora_sst_decode_file(os.fsencode(path)))
 
 
 def may_contain_batch(img, file_off, metas, keys, koff, k0, k1):

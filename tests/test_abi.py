@@ -31,7 +31,8 @@ def test_header_functions_exported():
 
 
 def test_abi_version():
-    assert _lib.load().lsm_abi_version() == 2
+    assert _lib.load().lsm_abi_version() == 3
+    assert _lib.load().lsm_input_slack() == 32
 
 
 def test_ctx_create_without_gpu_fails_cleanly():

@@ -254,6 +254,29 @@ def test_may_contain_truncated_bitset_and_k_zero(ctx):
     check(ctx, rng, [m0] + sorted_imgs[1:], probes, held_check=False)
 
 
+def test_may_contain_nbits_overflow_rejected(ctx):
+    """a stored bit count near 2^64 with no stored words must fail
+    the filter decode (bitset.ReadFrom cannot read that many words) instead
+    of passing a wrapped (nbits + 63) / 64 check and letting MayContain read
+    bit positions far past the image.  GPU and oracle: stage LSM_SST_FILTER,
+    no hit, on both the grouped and the per-probe path."""
+    rng = np.random.default_rng(8)
+    sorted_imgs = [build([b"w%02d_%04d" % (i, j) for j in range(50)], m=4096, k=3) for i in range(4)]
+    probes = [b"w%02d_%04d" % (i, j) for i in range(5) for j in range(0, 60, 3)]
+    for nb in ((1 << 64) - 1, (1 << 64) - 63, (1 << 64) - 64, 1 << 63):
+        bad = _patch_nbits(sorted_imgs[1], nb)
+        rc, meta, *_ = ora.sst_decode(bad)
+        assert meta.stage == 2, (nb, meta.stage)   # LSM_SST_FILTER
+        imgs = [sorted_imgs[0], bad] + sorted_imgs[2:]
+        d_img = lsmgpu.to_device_bytes(np.concatenate(imgs), ctx.torch_device)
+        offs = np.cumsum([0] + [im.size for im in imgs[:-1]]).astype(np.uint64)
+        r = lsmgpu.decode_sst(ctx, d_img, offs, np.array([im.size for im in imgs], np.uint64))
+        assert int(r.meta_numpy()[1]["stage"]) == 2
+        check(ctx, rng, imgs, probes, held_check=False)                 # grouped path
+        check(ctx, rng, imgs + [build([b"w00_0000", b"w04_9999"], m=64, k=1)], probes,
+              held_check=False)                                         # per-probe path
+
+
 def test_may_contain_per_probe_path_many_probes(ctx):
     """Overlapping files (the per-probe path) with more probes than one pass
     of its capped grid covers (1,024 workgroups x 256 probes): every row of

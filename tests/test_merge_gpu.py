@@ -57,20 +57,21 @@ def lay_out(pairs, kv_layout, rng, align4=False):
     return buf, kd, (None if kv_layout else vd), kpos, vpos
 
 
-def run(ctx, pairs, level, threshold, kv_layout=False, seed=0, align4=False):
+def run(ctx, pairs, level, threshold, kv_layout=False, seed=0, align4=False, tie=0):
     rng = random.Random(seed)
     buf, kd, vd, kpos, vpos = lay_out(pairs, kv_layout, rng, align4)
     dev = ctx.torch_device
     d_buf = lsmgpu.to_device_bytes(buf, dev)
     d_kd = torch.from_numpy(kd.view(np.int32).reshape(-1, 4).copy()).to(dev)
     d_vd = None if vd is None else torch.from_numpy(vd.view(np.int32).reshape(-1, 4).copy()).to(dev)
-    r = lsmgpu.merge_kvs(ctx, d_buf, d_kd, d_vd, level=level, threshold=threshold)
+    r = lsmgpu.merge_kvs(ctx, d_buf, d_kd, d_vd, level=level, threshold=threshold, tie=tie)
     torch.cuda.synchronize()
     got = r.out[:r.nout].cpu().numpy().view(np.uint32)
     starts = r.file_start[:r.nfiles + 1].cpu().numpy().view(np.uint64)
     klen = np.array([len(k) for k, _ in pairs], np.uint32)
     vlen = np.array([len(v) for _, v in pairs], np.uint32)
-    want, wstarts = ora.merge_kvs(buf, kpos, klen, vpos, vlen, level, threshold, ora.TIE_INPUT)
+    want, wstarts = ora.merge_kvs(buf, kpos, klen, vpos, vlen, level, threshold,
+                                  ora.TIE_GOHEAP if tie else ora.TIE_INPUT)
     assert np.array_equal(got, want), (level, threshold, got[:20], want[:20])
     assert np.array_equal(starts, wstarts), (level, threshold, starts, wstarts)
     return r, d_buf, d_kd, d_vd, got, starts
@@ -85,32 +86,40 @@ def random_pairs(rng, n, alphabet, maxlen, tomb=0.2, maxval=40):
     return out
 
 
-def test_reference_vector(ctx):
+TIES = [lsmgpu.TIE_INPUT, lsmgpu.TIE_GOHEAP]
+
+
+@pytest.mark.parametrize("tie", TIES)
+def test_reference_vector(ctx, tie):
     pairs = [(b"alpha", b"A"), (b"beta", b"B"), (b"beta", b"B2"), (b"carrot", b"C"), (b"delta", b"D")]
     for kv in (False, True):
-        _, _, _, _, got, starts = run(ctx, pairs, 1, MiB2, kv_layout=kv)
+        _, _, _, _, got, starts = run(ctx, pairs, 1, MiB2, kv_layout=kv, tie=tie)
         assert list(got) == [0, 1, 3, 4] and list(starts) == [0, 4]
 
 
-def test_edge_sizes(ctx):
-    run(ctx, [(b"a", b"b")], 1, MiB2)
-    run(ctx, [(b"", TOMB)], 6, MiB2)                      # nothing written: no file
-    run(ctx, [(b"", b""), (b"", b"x"), (b"", TOMB)], 6, 1)
+@pytest.mark.parametrize("tie", TIES)
+def test_edge_sizes(ctx, tie):
+    run(ctx, [(b"a", b"b")], 1, MiB2, tie=tie)
+    run(ctx, [(b"", TOMB)], 6, MiB2, tie=tie)                      # nothing written: no file
+    run(ctx, [(b"", b""), (b"", b"x"), (b"", TOMB)], 6, 1, tie=tie)
+    run(ctx, [(b"", b"%d" % i) for i in range(40)] + [(b"q", b"1"), (b"", TOMB)], 1, 30, tie=tie)
     r = lsmgpu.merge_kvs(ctx, torch.zeros(16, dtype=torch.uint8, device=ctx.torch_device),
-                         torch.zeros((0, 4), dtype=torch.int32, device=ctx.torch_device), None)
+                         torch.zeros((0, 4), dtype=torch.int32, device=ctx.torch_device), None,
+                         tie=tie)
     assert r.nout == 0 and r.nfiles == 0
 
 
+@pytest.mark.parametrize("tie", TIES)
 @pytest.mark.parametrize("level", [1, 6])
 @pytest.mark.parametrize("threshold", [1, 60, 700, MiB2])
-def test_random_duplicates_tombstones_flushes(ctx, level, threshold):
+def test_random_duplicates_tombstones_flushes(ctx, level, threshold, tie):
     """Short keys over a 4-letter alphabet with zero bytes (prefix, padding
     and "a" < "a\\0" order), many duplicates, tombstones, and thresholds
     that flush inside duplicate groups."""
     rng = random.Random(level * 1000 + threshold % 997)
     pairs = random_pairs(rng, 3000, b"ab\x00\xff", 11)
     for kv in (False, True):
-        run(ctx, pairs, level, threshold, kv_layout=kv, seed=level)
+        run(ctx, pairs, level, threshold, kv_layout=kv, seed=level, tie=tie)
 
 
 def test_long_keys_shared_prefixes(ctx):
@@ -125,9 +134,12 @@ def test_long_keys_shared_prefixes(ctx):
         run(ctx, pairs, level, threshold)
 
 
-def test_compaction_shaped_runs(ctx):
+@pytest.mark.parametrize("tie", TIES)
+def test_compaction_shaped_runs(ctx, tie):
     """loadLevelData's shape (compaction.go:173-193): newest files first,
-    each sorted and unique, overlapping key ranges; 2 MiB and 64 KiB files."""
+    each sorted and unique, overlapping key ranges; 2 MiB and 64 KiB files.
+    Both tie orders against the oracle; they must differ somewhere (the
+    heap keeps another pair of some duplicate groups)."""
     rng = np.random.default_rng(6)
     pairs = []
     for r in range(6):
@@ -135,8 +147,12 @@ def test_compaction_shaped_runs(ctx):
         for i in ids:
             v = TOMB if (i * 7 + r) % 23 == 0 else b"r%d_" % r + b"x" * int(i % 90)
             pairs.append((b"key%012d" % i, v))
+    outs = []
     for level, threshold in ((1, MiB2), (6, MiB2), (2, 64 * 1024)):
-        run(ctx, pairs, level, threshold, kv_layout=(level == 2))
+        outs.append(run(ctx, pairs, level, threshold, kv_layout=(level == 2), tie=tie)[4])
+    if tie == lsmgpu.TIE_GOHEAP:
+        inp = run(ctx, pairs, 1, MiB2)[4]
+        assert outs[0].size == inp.size and not np.array_equal(outs[0], inp)
 
 
 def test_gather_and_build_match_oracle_images(ctx):
@@ -278,3 +294,38 @@ def test_full_size_compaction_merge(ctx):
                                       v["rec_off"] + 4, v["val_len"], level, MiB2, ora.TIE_INPUT)
         assert np.array_equal(got, want) and np.array_equal(starts, wstarts), level
         assert m.nfiles >= 200
+
+
+def test_full_size_compaction_merge_goheap(ctx):
+    """LSM_TIE_GOHEAP at the compact bench's full size (3.43M pairs): the
+    reference's exact output (container/heap's own tie order) against
+    ora_merge_kvs(ORA_TIE_GOHEAP); prints the call's cost beside the
+    input-order path."""
+    import os
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench_compact import build_images, level0_runs
+    from lsmgpu import synth
+    n1 = 100_000 * 33
+    img, file_off, file_size = build_images(ctx, level0_runs(n1, 0, 0) + [synth.kv_stream(n1)])
+    r = lsmgpu.alloc_sst_decode(ctx, file_off, file_size, int(img.numel()))
+    lsmgpu.decode_sst_into(ctx, img, r)
+    kd, vd, prefix = lsmgpu.sst_pairs(ctx, r)
+    m = lsmgpu.alloc_merge(ctx, int(kd.shape[0]))
+    t = {}
+    for tie in (lsmgpu.TIE_INPUT, lsmgpu.TIE_GOHEAP):
+        lsmgpu.merge_kvs_into(ctx, img, kd, vd, m, level=1, tie=tie)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lsmgpu.merge_kvs_into(ctx, img, kd, vd, m, level=1, tie=tie)
+        torch.cuda.synchronize()
+        t[tie] = time.perf_counter() - t0
+    got = m.out[:m.nout].cpu().numpy().view(np.uint32)
+    starts = m.file_start[:m.nfiles + 1].cpu().numpy().view(np.uint64)
+    k = kd.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+    v = vd.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+    want, wstarts = ora.merge_kvs(img.cpu().numpy(), k["rec_off"] + 4, k["key_len"],
+                                  v["rec_off"] + 4, v["val_len"], 1, MiB2, ora.TIE_GOHEAP)
+    assert np.array_equal(got, want) and np.array_equal(starts, wstarts)
+    print(f"merge of {k.size} pairs: TIE_INPUT {t[0] * 1e3:.2f} ms, TIE_GOHEAP {t[1] * 1e3:.2f} ms")

@@ -190,3 +190,32 @@ def test_goheap_winner_depends_on_larger_keys_pushed_later():
     assert kept(pre + group + ext, T[1]) == [b"A"]
     # the input-order contract keeps the first pair either way
     assert kept(pre + group, T[0]) == kept(pre + group + ext, T[0]) == [b"A"]
+
+
+def test_library_goheap_pop_order_matches_restatement():
+    """lsm_goheap_pop_order_host (the host replay behind LSM_TIE_GOHEAP) is
+    container/heap's pop order: against the Python restatement above, over
+    dense key ranks, on random keys with many ties and on concatenated
+    sorted runs (compaction-shaped)."""
+    from lsmgpu import _lib, goheap_pop_order
+    lib = _lib.load()
+    rng = random.Random(12)
+    cases = []
+    for _ in range(150):
+        cases.append([bytes(rng.choice(b"abc") for _ in range(rng.randint(0, 4)))
+                      for _ in range(rng.randint(0, 200))])
+    for _ in range(30):
+        keys = []
+        for r in range(rng.randint(2, 6)):
+            keys += [b"key%04d" % k for k in sorted(rng.sample(range(400), rng.randint(5, 90)))]
+        cases.append(keys)
+    for keys in cases:
+        uniq = {k: i for i, k in enumerate(sorted(set(keys)))}
+        rank = np.array([uniq[k] for k in keys], np.uint32)
+        got = goheap_pop_order(lib, rank)
+        assert list(got) == goheap_order(keys)
+    # the winner-depends-on-later-keys case, through ranks
+    keys = [b"k24", b"k14", b"k30", b"k15", b"k15", b"k24", b"k19", b"k21", b"k19"]
+    uniq = {k: i for i, k in enumerate(sorted(set(keys)))}
+    assert list(goheap_pop_order(lib, np.array([uniq[k] for k in keys], np.uint32))) == \
+        goheap_order(keys)

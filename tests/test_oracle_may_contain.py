@@ -54,3 +54,24 @@ def test_batch_matches_per_file_restatement():
     for i, p in enumerate(probes):
         for f, im in enumerate(imgs):
             assert hit[i, f] == _expected(im, p), (p, f)
+
+
+def test_filter_nbits_near_2_64_fails_decode():
+    """nbits near 2^64 with no stored words is a failed filter
+    decode (stage LSM_SST_FILTER = 2; bitset.ReadFrom cannot read that many
+    words), not a wrapped (nbits + 63) / 64 that passes the length check.
+    Also through ora_filter_decode directly and the batched MayContain."""
+    img = _img([b"n%03d" % i for i in range(20)], m=1024, k=3)
+    mnl = int(np.frombuffer(img[:4].tobytes(), "<u4")[0])
+    at = 8 + 2 * mnl + 8 + 16
+    for nb in ((1 << 64) - 1, (1 << 64) - 63, 1 << 63):
+        bad = img.copy()
+        bad[at:at + 8] = np.frombuffer(struct.pack(">Q", nb), np.uint8)
+        rc, meta, *_ = ora.sst_decode(bad)
+        assert meta.stage == 2, (nb, meta.stage)
+        kb = np.frombuffer(b"n005", np.uint8)
+        hit = ora.may_contain_batch(bad, np.zeros(1, np.uint64), [meta], kb,
+                                    np.array([0, 4], np.uint64), 0, 1)
+        assert hit[0, 0] == 0
+    good = ora.sst_decode(img)[1]
+    assert good.stage == 0
