@@ -25,8 +25,6 @@ extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
-    for (int i = 0; i < kCtxBatchEvents && e == hipSuccess; i++)
-        e = hipEventCreateWithFlags(&c->batch[i], hipEventDisableTiming);
     if (e != hipSuccess) {
         lsm_ctx_destroy(c);
         return -(1000 + (int)e);
@@ -38,8 +36,6 @@ extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
 extern "C" int lsm_ctx_destroy(lsm_ctx *ctx) {
     if (!ctx) return 0;
     if (hipSetDevice(ctx->device) == hipSuccess) {
-        for (int i = 0; i < kCtxBatchEvents; i++)
-            if (ctx->batch[i]) (void)hipEventDestroy(ctx->batch[i]);
         if (ctx->join) (void)hipEventDestroy(ctx->join);
         if (ctx->fork) (void)hipEventDestroy(ctx->fork);
         if (ctx->side) (void)hipStreamDestroy(ctx->side);

@@ -16,13 +16,11 @@
 // its CU count, and a side stream with fork / join events for a call that
 // runs two independent kernels at once (lsm_build_sst: the VALU-bound filters
 // beside the HBM-bound regions, co-resident on the CUs).
-constexpr int kCtxBatchEvents = 8;  // lsm_build_sst's per-batch hand-offs
 struct lsm_ctx {
     int device;
     int num_cus;
     hipStream_t side;
     hipEvent_t fork, join;
-    hipEvent_t batch[kCtxBatchEvents];
 };
 
 namespace lsm {

@@ -859,8 +859,6 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
 // locations of every key of its filter from them (additions only) and ORs
 // those of its slice into LDS.
 constexpr uint32_t kHashRecDwords = 6;
-// lsm_build_sst: file batches whose ORs overlap the next batches' regions
-constexpr uint32_t kOrBatches = 1;
 constexpr uint32_t kSplitMaxK = 16;  // three carries per class fit the record
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -905,7 +903,6 @@ struct BloomOrArgs {
     const uint64_t *koff;
     uint8_t *out;
     const uint64_t *file_off;
-    uint32_t f0;  // first file of this launch (file = f0 + blockIdx.x)
 };
 
 // ---- .sst image writer ------------------------------------------------------
@@ -926,7 +923,6 @@ struct SstArgs {
     // key (store_hash_rec, key file_start[0] first), or null
     uint32_t *hrec;
     uint32_t hm, hrl, hrh;
-    uint32_t f0;  // first file of this launch (file = f0 + blockIdx.x)
 };
 
 struct SstLayout {
@@ -1150,7 +1146,7 @@ __device__ __forceinline__ void region_finish(const RegionPlan &R, uint32_t *buf
 
 __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kRegWaves][kRegBufDwords + kGatherMaskWords];
-    const uint32_t f = a.f0 + blockIdx.x;
+    const uint32_t f = blockIdx.x;
     const SstLayout L = sst_layout(a, f);
     const uint32_t wave = uni(threadIdx.x / kWave);
     uint64_t c0 = L.s + (uint64_t)blockIdx.y * kRegSpanRecs + (uint64_t)wave * kRegWaveChunks * kWave;
@@ -1261,7 +1257,7 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
     __shared__ uint32_t s_vl[W][kWave];
     __shared__ uint8_t s_map[W][kVvMap];
     __shared__ uint16_t s_q[W][kVvMap];
-    const uint32_t f = a.f0 + blockIdx.x, w = threadIdx.x / kWave, lane = lane_id();
+    const uint32_t f = blockIdx.x, w = threadIdx.x / kWave, lane = lane_id();
     const SstLayout L = sst_layout(a, f);
     const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kSstChunkRecs + (uint64_t)w * kWave;
     if (c0 >= L.e) return;
@@ -1398,7 +1394,7 @@ __device__ void sst_meta_body(const SstArgs &a, uint32_t f) {
     }
 }
 
-__global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body(a, a.f0 + blockIdx.x); }
+__global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body(a, blockIdx.x); }
 
 // Filter blockIdx.x, slice blockIdx.y: every key's k locations rebuilt from
 // its record, the slice's bits ORed in LDS, then stored big-endian into the
@@ -1407,7 +1403,7 @@ __global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body
 // lanes per clock per CU for scattered words, not by the rebuild.)
 __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs sa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
-    const uint32_t f = a.f0 + blockIdx.x, sl = blockIdx.y;
+    const uint32_t f = blockIdx.x, sl = blockIdx.y;
     // the image's header, filter prefix and footer (disjoint from the words)
     if (sl == 0 && threadIdx.x < kWave) sst_meta_body(sa, f);
     const uint32_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
@@ -2221,7 +2217,6 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     a.skip_v = views != nullptr;
     a.hrec = nullptr;
     a.hm = a.hrl = a.hrh = 0;
-    a.f0 = 0;
 
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
@@ -2297,47 +2292,8 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         const hipError_t _e = (expr);                   \
         if (_e != hipSuccess && rc == 0) rc = -(1000 + (int)_e); \
     } while (0)
-    const uint32_t rspans = (max_file_records + kRegSpanRecs - 1) / kRegSpanRecs;
-    static_assert(kOrBatches <= (uint32_t)kCtxBatchEvents, "one event per batch");
-    if (kOrBatches > 1 && split && chunks && !views && nfile >= 2 * kOrBatches) {
-        // The ORs of a file batch (LDS-atomic bound) run on the side stream
-        // under the regions of the next batches (HBM / issue bound): batch b's
-        // ORs wait only for batch b's hash records.
-        BloomOrArgs bo{};
-        bo.file_start = d_file_start;
-        bo.rec = a.hrec;
-        bo.m = (uint32_t)m;
-        bo.k = kk;
-        bo.c64 = (uint32_t)((~0ull % m + 1) % m);
-        bo.split = (uint32_t)sb;
-        bo.nwords = nwords;
-        bo.koff = d_koff;
-        bo.out = d_out;
-        bo.file_off = d_file_off;
-        LSM_TRY(hipEventRecord(ctx->fork, s));
-        LSM_TRY(hipStreamWaitEvent(ctx->side, ctx->fork, 0));
-        const uint32_t per = (nfile + kOrBatches - 1) / kOrBatches;
-        for (uint32_t b = 0; b < kOrBatches && rc == 0; b++) {
-            const uint32_t f0 = b * per, f1 = f0 + per < nfile ? f0 + per : nfile;
-            if (f0 >= f1) break;
-            a.f0 = f0;
-            hipLaunchKernelGGL(sst_regions_kernel, dim3(f1 - f0, rspans), dim3(kRegWaves * kWave), 0,
-                               s, a);
-            LSM_TRY(hipGetLastError());
-            LSM_TRY(hipEventRecord(ctx->batch[b], s));
-            LSM_TRY(hipStreamWaitEvent(ctx->side, ctx->batch[b], 0));
-            bo.f0 = f0;
-            a.f0 = f0;
-            if (rc == 0)
-                hipLaunchKernelGGL(bloom_or_kernel, dim3(f1 - f0, 2), dim3(1024), (size_t)(sb / 8),
-                                   ctx->side, bo, a);
-            LSM_TRY(hipGetLastError());
-        }
-        LSM_TRY(hipEventRecord(ctx->join, ctx->side));
-        LSM_TRY(hipStreamWaitEvent(s, ctx->join, 0));
-        return rc;
-    }
     if (chunks) {
+        const uint32_t rspans = (max_file_records + kRegSpanRecs - 1) / kRegSpanRecs;
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
         LSM_TRY(hipGetLastError());
         if (views && rc == 0) {
