@@ -1458,6 +1458,34 @@ struct WalLog {
         }
         exitp = p;
     }
+    // The first plausible start in [ss, se), every position of which lies in
+    // the LDS copy (a lane's share of its segment).  A plausible start holds a
+    // key length <= 1024, so its u32 has two zero high bytes: positions are
+    // screened 16 at a time from five LDS dwords read together, and only the
+    // (few) that pass -- in KV logs the length fields -- are tested in full.
+    // (Testing every position in full was a serial chain of ~40 dependent
+    // LDS round trips per lane.)
+    __device__ __forceinline__ uint32_t first_plausible(uint32_t ss, uint32_t se) const {
+        const uint32_t ob = h - s0;  // LDS byte offset of log position 0 (mod 2^32)
+        for (uint32_t w = (ob + ss) >> 2; 4 * w < ob + se; w += 4) {
+            uint32_t d[5];
+#pragma unroll
+            for (uint32_t t = 0; t < 5; t++) d[t] = lds[w + t];
+            uint32_t m = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++) {
+                const uint32_t x = funnel(d[j >> 2], d[(j >> 2) + 1], j);
+                const uint32_t p = 4 * w + j - ob;
+                m |= (uint32_t)(x <= 1024u && p >= ss && p < se) << j;
+            }
+            while (m) {
+                const uint32_t p = 4 * w + (uint32_t)__builtin_ctz(m) - ob;
+                if (plausible(p)) return p;
+                m &= m - 1;
+            }
+        }
+        return 0xFFFFFFFFu;
+    }
     // plausible record start (as the segment guess: two records or the log's end)
     __device__ __forceinline__ bool plausible(uint32_t q) const {
         uint32_t seen = 0;
@@ -1534,8 +1562,7 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     uint32_t e0 = 0xFFFFFFFFu, e1 = 0xFFFFFFFFu, c0 = 0, c1 = 0, x0 = 0, x1 = 0;
     int32_t st0 = LSM_OK, st1 = LSM_OK;
     if (lane > 0 && ss < se) {
-        for (uint32_t p = ss; p < se; p++)
-            if (L.plausible(p)) { e0 = p; break; }
+        e0 = L.first_plausible(ss, se);
         if (e0 != 0xFFFFFFFFu && (uint64_t)e0 + 4 <= len) {
             const uint32_t v = L.rd32(e0);
             if ((uint64_t)e0 + 4 + v <= len) e1 = e0 + 4 + v;
