@@ -58,6 +58,9 @@ def parse(argv=None):
     ap.add_argument("--arena", action="store_true", help="materialize keys/values too")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--placement", default="offset", choices=["offset", "plan"],
+                    help="decode output placement: offset-addressed (no plan) or dense "
+                         "(lsm_plan_* inside every step)")
     ap.add_argument("--no-cold", action="store_true",
                     help="skip the cold-input pass (input rotated over copies the MALL cannot hold)")
     ap.add_argument("--no-verify", action="store_true",
@@ -229,8 +232,15 @@ def bench_decode(args, world, rank, local):
     d_in = lsmgpu.to_device_bytes(buf, dev)
     d_off = torch.tensor(blk_off.view(np.int64), device=dev)
     d_len = torch.tensor(blk_len.view(np.int32), device=dev)
-    r = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()),
-                                   arena=args.arena)
+    if args.placement == "plan":
+        # dense outputs: the plan (exclusive scans of blk_len) is part of
+        # every step, as for a batch whose layout is new each time
+        plan = lsmgpu.plan(ctx, lsmgpu.GRAMMAR_KV, d_len, arena=args.arena)
+        r = lsmgpu.alloc_decode(ctx, lsmgpu.GRAMMAR_KV, nblk, plan, arena=args.arena)
+    else:
+        plan = None
+        r = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()),
+                                       arena=args.arena)
     args._d_in = d_in
     stream = torch.cuda.current_stream()
 
@@ -247,6 +257,8 @@ def bench_decode(args, world, rank, local):
         if args.config == "wal":
             lsmgpu.wal_replay_into(ctx, d_in, d_off, d_len, wal_max, r, wal_ws, stream=stream)
         else:
+            if plan is not None:
+                lsmgpu.replan(ctx, lsmgpu.GRAMMAR_KV, d_len, plan, stream=stream)
             lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r, stream=stream,
                                schedule=sched, max_blk_len=hint)
 
@@ -264,11 +276,12 @@ def bench_decode(args, world, rank, local):
     times, kern_ms = kernel_times(step, stream, args.steps)
     # the timed output is checked after the timed region: the line fails on a
     # single wrong descriptor (kv/kv.go:77-115 record chain, closed form)
-    verify_decode(args, r, d_off, d_len, nblk)
+    if args.placement == "offset":
+        verify_decode(args, r, d_off, d_len, nblk)
 
     parsed = float(blk_len.astype(np.float64).sum())
     cold = (cold_input_pass(args, ctx, buf, d_off, d_len, nblk, hint, stream, parsed)
-            if args.config in UNIFORM and not args.no_cold else None)
+            if args.config in UNIFORM and not args.no_cold and args.placement == "offset" else None)
     parsed_all = sum_over_ranks(world, parsed)
     value = parsed_all * args.steps / elapsed / GIB
     scaling = block_ids_for(args, world, rank)[1] if args.config in UNIFORM else "weak"

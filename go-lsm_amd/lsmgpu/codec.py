@@ -160,6 +160,10 @@ def replan(ctx: Context, grammar: int, blk_len: torch.Tensor, p: DecodePlan, str
                                          _ptr(p.rec_base), _ptr(p.workspace),
                                          p.workspace.numel(), _stream_handle(stream)),
                "lsm_plan_rec_base")
+    if p.arena_base is not None:
+        _lib.check(ctx.lib.lsm_plan_arena_base(ctx.handle, _ptr(blk_len), nblk, _ptr(p.arena_base),
+                                               _ptr(p.workspace), p.workspace.numel(),
+                                               _stream_handle(stream)), "lsm_plan_arena_base")
 
 
 def alloc_decode(ctx: Context, grammar: int, nblk: int, p: DecodePlan,

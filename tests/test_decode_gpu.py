@@ -493,3 +493,44 @@ def test_arena_uniform_runs(ctx, grammar):
         blocks.append(rec * 40 + rand_records(rng, grammar, 3, kmax=9, vmax=30) + rec * 90)
     run(ctx, grammar, blocks, arena=True, align_pad=11, seed=5)
     run(ctx, grammar, blocks, arena=True, align_pad=11, seed=6, placement="offset")
+
+
+@pytest.mark.parametrize("grammar", [0, 1, 2])
+def test_hinted_arena_linear_ring(ctx, grammar):
+    """ARENA with a bound that fits the 8 KiB ring (lsm_decode_blocks_hinted's
+    linear-ring kernel): outputs equal lsm_decode_blocks' and the oracle's --
+    for a batch within the bound, and for one where some blocks break it (the
+    marked blocks go through the streamed fallback launch), corrupted blocks,
+    odd alignments and equal-shape runs included."""
+    rng = np.random.default_rng(90 + grammar)
+    blocks = []
+    for i in range(400):
+        n = int(rng.choice([0, 1, 3, 20, 60]))
+        b = rand_records(rng, grammar, n, kmax=24, vmax=int(rng.choice([8, 40])))
+        blocks.append(corrupt(rng, b) if i % 5 == 0 else b)
+    kb, vb = bytes(range(7, 23)), bytes((i * 37) & 255 for i in range(100))
+    rec = {0: struct.pack("<I", 100) + vb, 1: struct.pack("<I", 16) + kb + struct.pack("<I", 100) + vb,
+           2: struct.pack("<I", 16) + kb + struct.pack("<q", 12345)}[grammar]
+    blocks += [rec * r for r in (1, 33, 60)]
+    fit = [b for b in blocks if len(b) <= 4000]
+    big = fit + [rand_records(rng, grammar, 400, kmax=30, vmax=200) for _ in range(5)] + [rec * 200]
+    for batch, hint in ((fit, 4000), (big, 4000)):
+        buf, d_in, d_off, d_len = dev_batch(ctx, batch, align_pad=7, rng=rng)
+        outs = []
+        for h in (None, hint):
+            r = lsmgpu.alloc_decode_offset(ctx, grammar, len(batch), int(d_in.numel()), arena=True)
+            for t in (r.desc, r.idx_value, r.key_arena, r.val_arena):
+                if t is not None:
+                    t.fill_(-1)
+            lsmgpu.decode_into(ctx, grammar, d_in, d_off, d_len, r, max_blk_len=h)
+            torch.cuda.synchronize()
+            outs.append(r)
+        a, b = outs
+        assert torch.equal(a.status, b.status) and torch.equal(a.nrec, b.nrec)
+        assert torch.equal(a.desc, b.desc)
+        for x, y in ((a.idx_value, b.idx_value), (a.key_arena, b.key_arena), (a.val_arena, b.val_arena)):
+            if x is not None:
+                assert torch.equal(x, y)
+        check_against_oracle(grammar, buf, d_off.cpu().numpy().view(np.uint64),
+                             d_len.cpu().numpy().view(np.uint32), b, arena=True, arena_fill=0xFF)
+    assert max(len(x) for x in big) > 8192  # the fallback ran
