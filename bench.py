@@ -296,6 +296,10 @@ def bench_decode(args, world, rank, local):
     achieved = alg / (kern_ms * 1e-3) / 1e9
     wkey = f"{args.config}:{nblk}:{'arena' if args.arena else 'desc'}"
     traffic, tsrc = traffic_from_profile(wkey)
+    if args.config == "mixed":
+        # the FETCH_SIZE x 2 correction is not calibrated for this access
+        # pattern (it read below the algorithmic bytes): no figure
+        traffic, tsrc = None, "not calibrated for the scheduled mixed-size pattern (DESIGN.md §7)"
     if cold is not None:
         cold["frac"] = round(alg / (cold["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     out = {

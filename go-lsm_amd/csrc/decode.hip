@@ -1444,6 +1444,79 @@ struct WalLog {
         if (rem2 - 4 < vl) return LSM_ST_TRUNC_VAL;
         return LSM_OK;
     }
+    // bytes [x, x+4) and [y, y+4): both from LDS in one round trip when both
+    // lie in the copy (the common case), else one at a time
+    __device__ __forceinline__ void rd32x2(uint32_t x, uint32_t y, uint32_t &u, uint32_t &v) const {
+        const uint32_t ox = h + x - s0, oy = h + y - s0;  // wraps above sz when below s0
+        if (ox <= sz - 8 && oy <= sz - 8) {
+            const uint32_t a0 = lds[ox >> 2], a1 = lds[(ox >> 2) + 1];
+            const uint32_t b0 = lds[oy >> 2], b1 = lds[(oy >> 2) + 1];
+            u = funnel(a0, a1, ox);
+            v = funnel(b0, b1, oy);
+        } else {
+            u = rd32(x);
+            v = rd32(y);
+        }
+    }
+    // chase() of two chains at once (a lane's two guesses): each step reads
+    // both chains' key lengths in one LDS round trip, then both value lengths
+    // (the chains are independent; chased one after the other they were two
+    // serial chains of dependent reads).  `park` is a position inside the copy
+    // for a chain that has stopped.  Same results as two chase() calls.
+    __device__ __forceinline__ void chase2(uint32_t pa, uint32_t pb, uint32_t end, uint32_t park,
+                                           uint32_t &ca, uint32_t &xa, int32_t &sa, uint32_t &cb,
+                                           uint32_t &xb, int32_t &sb) const {
+        ca = cb = 0;
+        sa = sb = LSM_OK;
+        bool ra = pa < end && pa < len, rb = pb < end && pb < len;
+        while (ra || rb) {
+            // kv.go:77-115 order, as record(): length prefix, key, value length, value
+            const uint32_t rma = len - pa, rmb = len - pb;
+            const bool ka_ok = ra && rma >= 4, kb_ok = rb && rmb >= 4;
+            uint32_t ka, kb;
+            rd32x2(ka_ok ? pa : park, kb_ok ? pb : park, ka, kb);
+            const bool ka2 = ka_ok && ka <= kKeyCap && rma - 4 >= ka && rma - 4 - ka >= 4;
+            const bool kb2 = kb_ok && kb <= kKeyCap && rmb - 4 >= kb && rmb - 4 - kb >= 4;
+            uint32_t va, vb;
+            rd32x2(ka2 ? pa + 4 + ka : park, kb2 ? pb + 4 + kb : park, va, vb);
+            if (ra) {
+                int32_t st = LSM_OK;
+                if (!ka_ok) st = LSM_ST_TRUNC_LEN_PREFIX;
+                else if (ka > kKeyCap) st = LSM_ST_KEY_TOO_LONG;
+                else if (rma - 4 < ka) st = LSM_ST_TRUNC_KEY;
+                else if (rma - 4 - ka < 4) st = LSM_ST_TRUNC_VLEN;
+                else if (va > kValCap) st = LSM_ST_VAL_TOO_LONG;
+                else if (rma - 8 - ka < va) st = LSM_ST_TRUNC_VAL;
+                if (st != LSM_OK) {
+                    sa = st;
+                    ra = false;
+                } else {
+                    ca++;
+                    pa += 8 + ka + va;
+                    ra = pa < end && pa < len;
+                }
+            }
+            if (rb) {
+                int32_t st = LSM_OK;
+                if (!kb_ok) st = LSM_ST_TRUNC_LEN_PREFIX;
+                else if (kb > kKeyCap) st = LSM_ST_KEY_TOO_LONG;
+                else if (rmb - 4 < kb) st = LSM_ST_TRUNC_KEY;
+                else if (rmb - 4 - kb < 4) st = LSM_ST_TRUNC_VLEN;
+                else if (vb > kValCap) st = LSM_ST_VAL_TOO_LONG;
+                else if (rmb - 8 - kb < vb) st = LSM_ST_TRUNC_VAL;
+                if (st != LSM_OK) {
+                    sb = st;
+                    rb = false;
+                } else {
+                    cb++;
+                    pb += 8 + kb + vb;
+                    rb = pb < end && pb < len;
+                }
+            }
+        }
+        xa = pa;
+        xb = pb;
+    }
     // chase from p while records start before `end`: count, stop position, status
     __device__ __forceinline__ void chase(uint32_t p, uint32_t end, uint32_t &cnt, uint32_t &exitp,
                                           int32_t &st) const {
@@ -1572,8 +1645,16 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     // passes its position through (exit = the guess); chase() returns exactly
     // that.  Leaving its exit unset once made a share holding only a value
     // field report exit 0 when the previous chain ended on that guess.
-    if (e0 != 0xFFFFFFFFu) L.chase(e0, se, c0, x0, st0);
-    if (e1 != 0xFFFFFFFFu) L.chase(e1, se, c1, x1, st1);
+    {
+        // both guesses' chains at once; a missing guess is a stopped chain
+        // (its count, exit and status keep their initial values)
+        uint32_t ca, xa, cb, xb;
+        int32_t sa, sb;
+        L.chase2(e0 != 0xFFFFFFFFu ? e0 : se, e1 != 0xFFFFFFFFu ? e1 : se, se, start, ca, xa, sa, cb,
+                 xb, sb);
+        if (e0 != 0xFFFFFFFFu) { c0 = ca; x0 = xa; st0 = sa; }
+        if (e1 != 0xFFFFFFFFu) { c1 = cb; x1 = xb; st1 = sb; }
+    }
     // 2. + 3. per phase: stitch from the entry, then write the accepted chains
     for (uint32_t ph = 0; ph < 2; ph++) {
         const uint64_t q = q0 + ph;

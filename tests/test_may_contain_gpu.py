@@ -302,4 +302,8 @@ def test_may_contain_per_probe_path_many_probes(ctx):
         metas = [ora.sst_decode(im)[1] for im in imgs]
         want = ora.may_contain_batch(buf, offs, metas, kb, ko, 0, n)
         assert np.array_equal(hit, want), np.argwhere(hit != want)[:8]
-        assert hit.any(axis=1).sum() > n // 20
+        # not vacuous: a probe lies in a file's 60k-key range with p ~ 0.55 and
+        # then hits with p ~ 0.05 (held) + 0.04 (false positive, m = 20,000,
+        # k = 4, 3,000 keys), so ~ 0.2 of the probes hit some file; the exact
+        # matrix is checked against the oracle above
+        assert hit.any(axis=1).sum() > n // 10
