@@ -347,7 +347,7 @@ def bench_decode(args, world, rank, local):
     return out, (buf, blk_off, blk_len)
 
 
-def cold_input_pass(args, ctx, buf, d_off, d_len, nblk, hint, stream, parsed, copies=8):
+def cold_input_pass(args, ctx, buf, d_off, d_len, nblk, hint, stream, parsed, copies=None):
     """The same decode with input the Infinity Cache (MALL, 256 MB) cannot
     hold: K launches rotating over `copies` distinct copies of the batch, each
     with its own outputs (8 x 409.6 MB for config 2), so every launch reads
@@ -357,6 +357,9 @@ def cold_input_pass(args, ctx, buf, d_off, d_len, nblk, hint, stream, parsed, co
     10 rotating copies).  Event-timed over the whole pass; every copy's
     output is checked."""
     dev = ctx.torch_device
+    if copies is None:  # >= 3.2 GB of input in rotation (2 copies of a GB-scale batch)
+        batch = nblk * UNIFORM[args.config]["slot"]
+        copies = int(min(8, max(2, -(-3_200_000_000 // batch))))
     ins = [args._d_in] + [lsmgpu.to_device_bytes(buf, dev) for _ in range(copies - 1)]
     outs = [lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(ins[0].numel()),
                                        arena=args.arena) for _ in range(copies)]

@@ -7,7 +7,7 @@
 # failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out; TAG=${TAG:-r02}
+OUT=gpurun_out; TAG=${TAG:-r03}
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)" >&2; timeout -k 10 $lim "$@"; }
@@ -29,7 +29,7 @@ DA[d64]="--config decode64k"; DK[d64]=decode64k:6400:desc
 for t in ${PMC1:-desc arena d64}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_${t}_$c 180 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${TAG}_${t}_$c -o run \
-      -- python bench.py ${DA[$t]} --steps 5 --warmup 2 --no-cpu-baseline > $OUT/pmc_${TAG}_${t}_$c.log 2>&1 || exit 1
+      -- python bench.py ${DA[$t]} --steps 5 --warmup 2 --no-cpu-baseline --no-cold > $OUT/pmc_${TAG}_${t}_$c.log 2>&1 || exit 1
   done
   python scripts/pmc_summary.py $OUT/pmc_${TAG}_${t}_FETCH_SIZE $OUT/pmc_${TAG}_${t}_WRITE_SIZE decode_v2_kernel \
     ${DK[$t]} $OUT/${TAG}_pmc_$t.json > /dev/null && cp $OUT/${TAG}_pmc_$t.json profiles/ || exit 1
@@ -41,10 +41,10 @@ K[mixed]=sched_hist_kernel,sched_scatter_kernel,decode_v2_kernel; A[mixed]=decod
 K[sstdec]=sst_index_kernel,sst_index_fixup_kernel,sst_data_verify_kernel,sst_data_fixup_kernel; A[sstdec]=sst_index_fixup_kernel; W[sstdec]=sstdec:208
 K[probe]=mc_prep_kernel,mc_classify_kernel,mc_scatter_kernel,mc_test_kernel,may_contain_kernel; A[probe]=mc_prep_kernel; W[probe]=probe:208:1048576
 K[wal]=wal_seg_lanes_kernel,wal_stitch_kernel,wal_compact_kernel; A[wal]=wal_stitch_kernel; W[wal]=wal:64:desc
-for cfg in ${PMCM:-sst mixed sstdec probe wal}; do
+for cfg in ${PMCM:-sst sstdec probe wal}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmcm_${cfg}_$c 180 rocprofv3 --pmc $c --output-format csv -d $OUT/pmcm_${TAG}_${cfg}_$c -o run \
-      -- python bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline > $OUT/pmcm_${TAG}_${cfg}_$c.log 2>&1 || exit 1
+      -- python bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-cold > $OUT/pmcm_${TAG}_${cfg}_$c.log 2>&1 || exit 1
   done
   python scripts/pmc_multi.py $OUT/pmcm_${TAG}_${cfg}_FETCH_SIZE $OUT/pmcm_${TAG}_${cfg}_WRITE_SIZE "${K[$cfg]}" "${A[$cfg]}" "${W[$cfg]}" \
     profiles/${TAG}_pmc_$cfg.json $OUT/${TAG}_pmc_$cfg.json > /dev/null || exit 1
@@ -62,10 +62,10 @@ for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal 
     || { tail -20 $OUT/bench_${TAG}_$line.err; exit 1; }
   cut -c1-200 $OUT/bench_${TAG}_$line.json
 done
-for p in ${PROF:-decode4k arena sst}; do
+for p in ${PROF:-decode4k arena decode64k mixed sst sstdec probe wal compact}; do
   case $p in arena) args="--arena" ;; *) args="--config $p" ;; esac
   step prof_$p 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_$p -o run \
-    -- python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_${TAG}_$p.log 2>&1 || exit 1
+    -- python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline --no-cold > $OUT/prof_${TAG}_$p.log 2>&1 || exit 1
 done
 fi
 echo "== done $(date +%T)"
