@@ -859,6 +859,7 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
 // locations of every key of its filter from them (additions only) and ORs
 // those of its slice into LDS.
 constexpr uint32_t kHashRecDwords = 6;
+constexpr uint32_t kOrSlices = 2;  // bloom_or_kernel workgroups per filter
 constexpr uint32_t kSplitMaxK = 16;  // three carries per class fit the record
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -1406,7 +1407,7 @@ __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs s
     const uint32_t f = blockIdx.x, sl = blockIdx.y;
     // the image's header, filter prefix and footer (disjoint from the words)
     if (sl == 0 && threadIdx.x < kWave) sst_meta_body(sa, f);
-    const uint32_t lo = sl ? a.split : 0, hi = sl ? a.m : a.split;
+    const uint32_t lo = sl * a.split, hi = lo + a.split < a.m ? lo + a.split : a.m;
     const uint32_t nw = (hi - lo + 63) / 64 * 2;
     for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_bits[i] = 0;
     __syncthreads();
@@ -1459,7 +1460,7 @@ __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs s
     }
     __syncthreads();
     const uint64_t hdr = sst_header_bytes(a.koff, s, e);
-    store_filter_slice(WgGroup{}, lds_bits, lo / 64, sl ? a.nwords : (uint64_t)(hi + 63) / 64,
+    store_filter_slice(WgGroup{}, lds_bits, lo / 64, hi == a.m ? a.nwords : (uint64_t)(hi + 63) / 64,
                        a.out + uni64(a.file_off[f]) + hdr + 32, nullptr);
 }
 
@@ -2312,12 +2313,15 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         bo.m = (uint32_t)m;
         bo.k = kk;
         bo.c64 = (uint32_t)((~0ull % m + 1) % m);
-        bo.split = (uint32_t)sb;
+        // kOrSlices word-aligned slices per filter, one workgroup each
+        const uint64_t osb = ((m + kOrSlices - 1) / kOrSlices + 63) / 64 * 64;
+        bo.split = (uint32_t)osb;
         bo.nwords = nwords;
         bo.koff = d_koff;
         bo.out = d_out;
         bo.file_off = d_file_off;
-        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, 2), dim3(1024), (size_t)(sb / 8), s, bo, a);
+        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, (uint32_t)((m + osb - 1) / osb)), dim3(1024),
+                           (size_t)(osb / 8), s, bo, a);
         LSM_TRY(hipGetLastError());
     }
     if (forked) {  // join (also after an error): the caller's stream waits for the regions
