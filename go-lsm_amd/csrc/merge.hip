@@ -864,6 +864,7 @@ void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order) {
         for (;;) {
             const uint32_t j1 = 2 * i + 1;
             if (j1 >= m) break;
+            __builtin_prefetch(&h[4 * (uint64_t)i + 3]);  // the grandchildren's line
             uint32_t j = j1;
             if (j1 + 1 < m && (h[j1 + 1] >> 32) < (h[j1] >> 32)) j = j1 + 1;
             if (!((h[j] >> 32) < (x >> 32))) break;
