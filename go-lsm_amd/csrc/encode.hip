@@ -1226,18 +1226,21 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
 // Data region (V grammar, sstable.go:159-175) of file blockIdx.x straight
 // from value views: record j of the batch is [u32 vlen][value], its value at
 // bytes + view(idx[j]) (a V descriptor, or the value of a KV descriptor).
-// One wave per 64 records: their records form one contiguous output range,
-// cut into 16-byte chunks (aligned in the output); an LDS map gives each
-// chunk its record; a chunk inside one value is five aligned source dwords
-// funnel-shifted into one 16-byte store, any other chunk (a length prefix,
-// a record boundary, an end of the range) is queued and written a dword or
-// a byte at a time.  Chunks are handled kVvMap at a time (any value size).
+// One wave per 64 records: their records form one contiguous output range
+// [A, B), written a dword per lane per step (256 coalesced bytes per store
+// instruction).  An LDS map gives each output dword the record holding its
+// first byte; the dword is assembled from that record's prefix and value
+// bytes and, where the record ends inside it, the next record's prefix (a
+// record is at least its 4-byte prefix, so no dword spans three records).
+// Only the two dwords cut by A and B are written a byte at a time (the
+// neighbouring waves own their other bytes).  kVvMap dwords per pass.
 struct VViewArgs {
     const uint8_t *bytes;
     const u32x4 *kd, *vd;  // vd == null: KV descriptors (value after the key)
     const uint32_t *idx;
 };
-constexpr uint32_t kVvMap = 1024;
+constexpr uint32_t kVvMap = 2048;
+constexpr uint32_t kVvUnroll = 8;
 
 __device__ __forceinline__ uint32_t ld_any32(const uint8_t *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -1257,7 +1260,6 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
     __shared__ uint64_t s_src[W][kWave];      // source offset of its value bytes
     __shared__ uint32_t s_vl[W][kWave];
     __shared__ uint8_t s_map[W][kVvMap];
-    __shared__ uint16_t s_q[W][kVvMap];
     const uint32_t f = blockIdx.x, w = threadIdx.x / kWave, lane = lane_id();
     const SstLayout L = sst_layout(a, f);
     const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kSstChunkRecs + (uint64_t)w * kWave;
@@ -1289,65 +1291,60 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
     }
     if (lane == 0) s_dst[w][cnt] = rbase + 4 * (c0 + cnt) + a.voff[c0 + cnt];
     vv_sync();
-    const uint64_t A = s_dst[w][0], B = s_dst[w][cnt], X = A & ~(uint64_t)15;
-    const uint64_t nch = (B - X + 15) / 16;
+    const uint64_t A = s_dst[w][0], B = s_dst[w][cnt], X = A & ~(uint64_t)3;
+    const uint64_t ndw = (B - X + 3) / 4;
     const gptr_t<uint8_t> out = gbl(a.out);
     const gptr_t<const uint8_t> vb = gbl(v.bytes);
-    for (uint64_t P = 0; P < nch; P += kVvMap) {
-        const uint32_t np = (uint32_t)(nch - P < kVvMap ? nch - P : kVvMap);
-        // 1. chunks whose first byte lies in my record
+    for (uint64_t P = 0; P < ndw; P += kVvMap) {
+        const uint32_t np = (uint32_t)(ndw - P < kVvMap ? ndw - P : kVvMap);
+        // 1. dwords whose first byte lies in my record
         if (lane < cnt) {
-            const uint64_t lo = d0 > X ? (d0 - X + 15) / 16 : 0;
-            const uint64_t hi = (d1 - 1 - X) / 16;
+            const uint64_t lo = (d0 - X + 3) / 4, hi = (d1 - 1 - X) / 4;
             const uint64_t c_lo = lo > P ? lo : P;
             const uint64_t c_hi = hi < P + np - 1 ? hi : P + np - 1;
             for (uint64_t c = c_lo; c <= c_hi; c++) s_map[w][c - P] = (uint8_t)lane;
         }
         vv_sync();
-        // 2. chunks inside one value; queue the rest
-        uint32_t qn = 0;
-        for (uint32_t cc0 = 0; cc0 < np; cc0 += kWave) {
-            const uint32_t c = cc0 + lane;
-            const uint64_t x = X + 16 * (P + c);
-            bool regular = false;
-            if (c < np && x >= A && x + 16 <= B) {
-                const uint32_t r = s_map[w][c];
-                const uint64_t e0 = s_dst[w][r] + 4, e1 = s_dst[w][r + 1];
-                if (x >= e0 && x + 16 <= e1) {
-                    regular = true;
-                    const uintptr_t sa = reinterpret_cast<uintptr_t>(v.bytes + s_src[w][r] + (x - e0));
-                    const gptr_t<const uint32_t> q = gbl_at<const uint32_t>(sa & ~(uintptr_t)3);
-                    const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
-                    const uint32_t sh = (uint32_t)sa;
-                    u32x4 o;
-                    o.x = funnel(q0, q1, sh);
-                    o.y = funnel(q1, q2, sh);
-                    o.z = funnel(q2, q3, sh);
-                    o.w = funnel(q3, q4, sh);
-                    *(gptr_t<u32x4>)(out + x) = o;
-                }
+        // 2. kVvUnroll dwords per lane per step, every load issued before
+        //    the first is used (the step is one load latency, not kVvUnroll)
+        for (uint32_t cb = 0; cb < np; cb += kWave * kVvUnroll) {
+            uint32_t q0[kVvUnroll], q1[kVvUnroll], o_[kVvUnroll], r_[kVvUnroll];
+            bool ok[kVvUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kVvUnroll; u++) {
+                const uint32_t c = cb + u * kWave + lane;
+                const uint64_t x = X + 4 * (P + c);
+                ok[u] = c < np && x >= A && x + 4 <= B;
+                const uint32_t r = ok[u] ? s_map[w][c] : 0;
+                const uint32_t o = ok[u] ? (uint32_t)(x - s_dst[w][r]) : 4;  // byte o of record r
+                const uintptr_t sa = reinterpret_cast<uintptr_t>(v.bytes + s_src[w][r] + (o >= 4 ? o - 4 : 0));
+                const gptr_t<const uint32_t> q = gbl_at<const uint32_t>(sa & ~(uintptr_t)3);
+                q0[u] = q[0];
+                q1[u] = q[1];
+                o_[u] = o;
+                r_[u] = r;
             }
-            const bool irr = c < np && !regular;
-            const uint64_t im = __ballot(irr);
-            if (irr) s_q[w][qn + mbcnt(im)] = (uint16_t)c;
-            qn += (uint32_t)__builtin_popcountll(im);
+#pragma unroll
+            for (uint32_t u = 0; u < kVvUnroll; u++) {
+                if (!ok[u]) continue;
+                const uint32_t c = cb + u * kWave + lane, r = r_[u], o = o_[u];
+                const uint64_t x = X + 4 * (P + c);
+                const uintptr_t sa = reinterpret_cast<uintptr_t>(v.bytes + s_src[w][r] + (o >= 4 ? o - 4 : 0));
+                uint32_t val = funnel(q0[u], q1[u], (uint32_t)sa);
+                if (o < 4) val = (s_vl[w][r] >> (8 * o)) | (o ? val << (32 - 8 * o) : 0);
+                const uint32_t k = (uint32_t)(s_dst[w][r + 1] - x);  // bytes left in record r
+                if (k < 4) val = (val & ((1u << (8 * k)) - 1)) | (s_vl[w][r + 1] << (8 * k));
+                *(gptr_t<uint32_t>)(out + x) = val;
+            }
         }
-        vv_sync();
-        // 3. queued chunks: four lanes per chunk, a dword (or its bytes) each
-        for (uint32_t i0 = 0; i0 < qn; i0 += kWave / 4) {
-            const uint32_t i = i0 + lane / 4;
-            if (i >= qn) continue;
-            const uint32_t c = s_q[w][i];
-            const uint64_t x = X + 16 * (P + c), xd = x + 4 * (lane & 3);
-            if (xd >= B) continue;
-            uint32_t r = x >= A ? s_map[w][c] : 0;
-            while (r + 1 < cnt && xd >= s_dst[w][r + 1]) r++;
-            const uint64_t e0 = s_dst[w][r] + 4;
-            if (xd >= A && xd + 4 <= B && xd >= e0 && xd + 4 <= s_dst[w][r + 1]) {
-                *(gptr_t<uint32_t>)(out + xd) = ld_any32(v.bytes + s_src[w][r] + (xd - e0));
-            } else {
+        // 3. the dwords cut by A and B, a byte at a time
+        if (lane < 2) {
+            const uint64_t c = lane == 0 ? 0 : ndw - 1;
+            const uint64_t x = X + 4 * c;
+            if (c >= P && c < P + np && (x < A || x + 4 > B)) {
+                uint32_t r = x >= A ? cnt - 1 : 0;
                 for (uint32_t u = 0; u < 4; u++) {
-                    const uint64_t b = xd + u;
+                    const uint64_t b = x + u;
                     if (b < A || b >= B) continue;
                     while (b >= s_dst[w][r + 1]) r++;
                     const uint64_t t = b - s_dst[w][r];  // byte t of record r

@@ -29,7 +29,8 @@
 //      candidate of each group: its first pair that may be written;
 //   4. one scan of the candidates' (size, count) into interleaved sums, then
 //      one wave walks the file boundaries -- one probe round per file when it
-//      starts a group; a flush inside a group makes the next writable pair of
+//      starts a group, and the windows around the next files' predicted ends
+//      ride in the same round trip (up to kWalkAhead files per round); a flush inside a group makes the next writable pair of
 //      that group a write of its own (the "extra" of the next file);
 //   5. emit: each candidate's output slot from its file's start.
 // Steps 3-5 are exact for any input; only the tie order is specified above.
@@ -445,6 +446,13 @@ __device__ uint32_t wave_lower_bound(const SumPair *sc, uint32_t lo, uint32_t hi
 // file spans about as many positions as the last one -- takes one round of
 // loads: lane 0 reads flags[p] and sc[p] while lanes 1..63 probe sc around
 // the predicted end.
+constexpr uint32_t kWalkAhead = 8;  // windows (files) per round trip of the walk
+
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
 __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
     const uint32_t n = a.m.n, lane = lane_id();
     const SumPair tail = a.sc[n];
@@ -462,6 +470,23 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
             const uint32_t k = w0 + lane + kWave * i;
             q[i] = a.sc[k <= n ? k : n];
         }
+        // ... and, in the same round trip, the windows around the next
+        // kWalkAhead - 1 predicted ends and the flags of every window: files
+        // that start a group chain through them without another round
+        const bool ahead = span > 128;
+        const uint32_t span0 = span;
+        SumPair qx[kWalkAhead - 1][4];
+        uint8_t fx[kWalkAhead][4];
+#pragma unroll
+        for (uint32_t j = 0; j < kWalkAhead; j++) {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint64_t k = (uint64_t)w0 + (uint64_t)j * span0 + lane + kWave * i;
+                const uint32_t kc = k <= n ? (uint32_t)k : n;
+                if (j) qx[j - 1][i] = a.sc[kc];  // unconditional: no branch per load
+                fx[j][i] = a.flags[kc < n ? kc : n - 1];
+            }
+        }
         const SumPair q0 = a.sc[p];
         const uint8_t fl0 = lane == 0 ? a.flags[p] : 0;
         const bool starts = p == 0 || (__builtin_amdgcn_readfirstlane(fl0) & 1);
@@ -469,7 +494,8 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
         uint32_t g = p, w = kNone, e = kNone;
         uint64_t wsize = 0, Cg = C0;
         bool done = false, have_ce = false;
-        uint64_t Ce = 0;
+        uint64_t Ce = 0, Sk = 0;  // at the end found in window 0
+        uint32_t fk = 0;
         if (starts) {
             const uint64_t t = S0 + a.threshold;
             if (tail.s < t) {
@@ -484,8 +510,9 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
                     if (k > w0 || k == p + 1) {  // the position before k is below t
                         e = k - 1;
                         done = true;
-                        Ce = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(q[i].c >> 32), f) << 32 |
-                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)q[i].c, f);
+                        Ce = lane_u64(q[i].c, f);
+                        Sk = lane_u64(q[i].s, f);
+                        fk = (uint32_t)__builtin_amdgcn_readlane((uint32_t)fx[0][i], f);
                         have_ce = true;
                     }
                     break;
@@ -533,6 +560,44 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
         nf++;
         span = end - g;
         p = end;
+        if (!(starts && have_ce && ahead)) continue;
+        // chain: file j starts at p (found in window j - 1, with its S, C and
+        // flags); its end is exact when it lies inside window j
+        uint64_t Sj = Sk, Cj = Ce;
+        uint32_t fj = fk;
+#pragma unroll
+        for (uint32_t j = 1; j < kWalkAhead; j++) {
+            if (p >= n || !(fj & 1)) break;  // done, or a group continues: general round
+            const uint64_t t = Sj + a.threshold;
+            if (tail.s < t) break;  // the last file: general round
+            const uint64_t wj = (uint64_t)w0 + (uint64_t)j * span0;
+            bool hit = false;
+            uint32_t k = 0, fn = 0;
+            uint64_t Cn = 0, Sn = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint64_t ge = __ballot(qx[j - 1][i].s >= t);
+                if (!ge) continue;
+                const uint32_t f = (uint32_t)__builtin_ctzll(ge);
+                const uint64_t kk = wj + kWave * i + f;
+                hit = kk > wj || kk == (uint64_t)p + 1;  // the position before is below t
+                k = (uint32_t)kk;
+                Cn = lane_u64(qx[j - 1][i].c, f);
+                Sn = lane_u64(qx[j - 1][i].s, f);
+                fn = (uint32_t)__builtin_amdgcn_readlane((uint32_t)fx[j][i], f);
+                break;
+            }
+            if (!hit || Cn == Cj) break;
+            if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
+            o += Cn - Cj;
+            nf++;
+            fast++;
+            span = k - p;
+            p = k;
+            Cj = Cn;
+            Sj = Sn;
+            fj = fn;
+        }
     }
     if (lane == 0) {
         a.files[nf] = MergeFile{n, kNone, o};
