@@ -99,7 +99,8 @@ def bench_compact(args, world, rank, local):
         batch = lsmgpu.gather_kvs(ctx, img, kd, vd, mg.out, mg.nout, key_bytes, None,
                                   stream=stream)
         mark(4)
-        sb = lsmgpu.prepare_sst_device(ctx, batch, mg.file_start, mg.nfiles)
+        sb = lsmgpu.prepare_sst_device(ctx, batch, mg.file_start, mg.nfiles, mg.max_recs,
+                                       val_bytes=val_bytes, stream=stream)
         lsmgpu.build_sst_views_into(ctx, batch, sb, img, kd, vd, mg.out, stream=stream)
         mark(5)
         return sb, batch
@@ -119,7 +120,7 @@ def bench_compact(args, world, rank, local):
                 for i, nm in enumerate(ev_names)}
     in_bytes = float(file_size.astype(np.float64).sum())
     total = sum_over_ranks(world, in_bytes)
-    # the build stage (image layout + lsm_build_sst_views) moves the most
+    # the build stage (lsm_sst_layout + lsm_build_sst_views) moves the most
     # bytes: per written pair the packed key and its koff / voff (16 B), the
     # index (4 B) and value descriptor (16 B), the value bytes read, and every
     # image byte written
@@ -142,7 +143,7 @@ def bench_compact(args, world, rank, local):
                    "input_bytes_per_gpu": int(in_bytes),
                    "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
                    "parallelism": f"dp{world} (one compaction per rank, no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "build stage: lsm_sst_image_sizes + "
+        "roofline": {"bound": "hbm", "kernel": "build stage: lsm_sst_layout + "
                                                "lsm_build_sst_views (events around the stage)",
                      "achieved": round(b_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(b_ach / HBM_PEAK_GBS, 4), "traffic": None,

@@ -1242,12 +1242,6 @@ struct VViewArgs {
 constexpr uint32_t kVvMap = 2048;
 constexpr uint32_t kVvUnroll = 8;
 
-__device__ __forceinline__ uint32_t ld_any32(const uint8_t *p) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const gptr_t<const uint32_t> q = gbl_at<const uint32_t>(a & ~(uintptr_t)3);
-    return funnel(q[0], q[1], (uint32_t)a);
-}
-
 __device__ __forceinline__ void vv_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

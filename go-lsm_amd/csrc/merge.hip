@@ -414,7 +414,7 @@ struct WalkArgs {
     uint64_t threshold;
     MergeFile *files;
     uint32_t *out;
-    uint64_t *counts;   // [0] = written pairs, [1] = files
+    uint64_t *counts;   // [0] = written pairs, [1] = files, [2] = most pairs in one file
 };
 
 // smallest k in [lo, hi] with sc[k].s >= t, given sc[hi].s >= t
@@ -457,8 +457,7 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
     const uint32_t n = a.m.n, lane = lane_id();
     const SumPair tail = a.sc[n];
     uint32_t p = 0, nf = 0, span = 0;
-    uint64_t o = 0;
-    uint32_t fast = 0, slow = 0;
+    uint64_t o = 0, most = 0;
     while (p < n) {
         // speculative round: lane 0 reads flags[p] and sc[p]; every lane reads
         // sc at four positions of the window [w0, w0 + 256) around the
@@ -542,7 +541,6 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
                 done = true;
             }
         }
-        if (done) fast++; else slow++;
         if (!done) {
             const uint64_t Sg = g < n ? uni64(a.sc[g].s) : tail.s;
             const uint64_t t = Sg + (a.threshold - wsize);
@@ -557,6 +555,7 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
             if (w != kNone) a.out[o] = a.perm[w];
         }
         o += nw;
+        most = nw > most ? nw : most;
         nf++;
         span = end - g;
         p = end;
@@ -590,8 +589,8 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
             if (!hit || Cn == Cj) break;
             if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
             o += Cn - Cj;
+            most = Cn - Cj > most ? Cn - Cj : most;
             nf++;
-            fast++;
             span = k - p;
             p = k;
             Cj = Cn;
@@ -603,8 +602,7 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
         a.files[nf] = MergeFile{n, kNone, o};
         a.counts[0] = o;
         a.counts[1] = nf;
-        a.counts[2] = fast;  // diagnostics (LSM_MERGE_DBG)
-        a.counts[3] = slow;
+        a.counts[2] = most;
     }
 }
 
@@ -812,6 +810,35 @@ __global__ __launch_bounds__(kMergeThreads) void sst_sizes_kernel(const uint64_t
     size[f] = hdr + filter + 4 * nr + (voff[r1] - voff[r0]) + 12 * nr + (koff[r1] - koff[r0]) + 32;
 }
 
+// The images' layout on the device: each file's size (as sst_sizes_kernel)
+// and its offset in one output buffer, sizes rounded up to `align`;
+// file_off[nfile] = the total.  One workgroup (a few thousand files at most
+// per compaction), tile after tile with a carry.
+__global__ __launch_bounds__(kMergeThreads) void sst_layout_kernel(const uint64_t *koff,
+                                                                   const uint64_t *voff,
+                                                                   const uint64_t *file_start,
+                                                                   uint32_t nfile, uint64_t filter,
+                                                                   uint64_t align, uint64_t *size,
+                                                                   uint64_t *file_off) {
+    uint64_t carry = 0;
+    for (uint32_t f0 = 0; f0 < nfile; f0 += kMergeThreads) {
+        const uint32_t f = f0 + threadIdx.x;
+        uint64_t sz = 0;
+        if (f < nfile) {
+            const uint64_t r0 = file_start[f], r1 = file_start[f + 1], nr = r1 - r0;
+            uint64_t hdr = 8;
+            if (r1 > r0) hdr += (koff[r0 + 1] - koff[r0]) + (koff[r1] - koff[r1 - 1]);
+            sz = hdr + filter + 4 * nr + (voff[r1] - voff[r0]) + 12 * nr + (koff[r1] - koff[r0]) + 32;
+            size[f] = sz;
+        }
+        SumPair tot;
+        const SumPair x = block_excl_scan2((sz + align - 1) / align * align, 0, &tot);
+        if (f < nfile) file_off[f] = carry + x.s;
+        carry += tot.s;
+    }
+    if (threadIdx.x == 0) file_off[nfile] = carry;
+}
+
 // ---- positional join of decoded .sst files (loadLevelData) ----------------
 
 __device__ __forceinline__ uint64_t sst_pair_count(const lsm_sst_meta &m) {
@@ -969,7 +996,7 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     if (tie != LSM_TIE_INPUT && tie != LSM_TIE_GOHEAP) return LSM_EINVAL;
     if (n && (!d_bytes || !d_key_desc || !d_out || !d_ws)) return LSM_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    h_counts[0] = h_counts[1] = 0;
+    h_counts[0] = h_counts[1] = h_counts[2] = 0;
     if (n == 0) {
         if (d_file_start) LSM_HIP_CHECK(hipMemsetAsync(d_file_start, 0, 8, s));
         return 0;
@@ -1100,11 +1127,10 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
                        w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);
     LSM_HIP_CHECK(hipGetLastError());
-    uint64_t c4[4];
-    LSM_HIP_CHECK(hipMemcpyAsync(c4, w.stats, 32, hipMemcpyDeviceToHost, s));
+    uint64_t c3[3];
+    LSM_HIP_CHECK(hipMemcpyAsync(c3, w.stats, sizeof c3, hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
-    h_counts[0] = c4[0];
-    h_counts[1] = c4[1];
+    for (int i = 0; i < 3; i++) h_counts[i] = c3[i];
     return 0;
 }
 
@@ -1163,6 +1189,19 @@ extern "C" int lsm_sst_image_sizes(lsm_ctx *ctx, const uint64_t *d_koff, const u
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(sst_sizes_kernel, dim3(grid_for(nfile)), dim3(kMergeThreads), 0, s, d_koff,
                        d_voff, d_file_start, nfile, lsm_filter_block_size(m), d_size);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_sst_layout(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff,
+                              const uint64_t *d_file_start, uint32_t nfile, uint64_t m,
+                              uint32_t align, uint64_t *d_size, uint64_t *d_file_off,
+                              void *stream) {
+    if (!ctx || align == 0 || !d_file_off) return LSM_EINVAL;
+    if (nfile && (!d_koff || !d_voff || !d_file_start || !d_size)) return LSM_EINVAL;
+    hipLaunchKernelGGL(sst_layout_kernel, dim3(1), dim3(kMergeThreads), 0,
+                       static_cast<hipStream_t>(stream), d_koff, d_voff, d_file_start, nfile,
+                       lsm_filter_block_size(m), (uint64_t)align, d_size, d_file_off);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

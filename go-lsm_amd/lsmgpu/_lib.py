@@ -118,6 +118,9 @@ SIGNATURES = {
     "lsm_sst_image_sizes": (ctypes.c_int, [ctypes.c_void_p, c_u64p, c_u64p, c_u64p,
                                            ctypes.c_uint32, ctypes.c_uint64, c_u64p,
                                            ctypes.c_void_p]),
+    "lsm_sst_layout": (ctypes.c_int, [ctypes.c_void_p, c_u64p, c_u64p, c_u64p, ctypes.c_uint32,
+                                      ctypes.c_uint64, ctypes.c_uint32, c_u64p, c_u64p,
+                                      ctypes.c_void_p]),
     "lsm_sst_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64p, ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, c_u64p, ctypes.c_void_p]),
@@ -138,7 +141,7 @@ SIGNATURES = {
     "lsm_stream_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 3   # LSM_ABI_VERSION this binding is written against
+ABI_VERSION = 4   # LSM_ABI_VERSION this binding is written against
 INPUT_SLACK = 32  # LSM_INPUT_SLACK: device inputs are padded by this much
 
 _lib = None

@@ -518,19 +518,40 @@ def segment_files(ctx: Context, koff: np.ndarray, voff: np.ndarray,
     return starts[: nf + 1].copy()
 
 
-@dataclass
 class SstBuild:
-    out: torch.Tensor
-    file_start: np.ndarray
-    file_off: np.ndarray
-    file_size: np.ndarray
-    footer: torch.Tensor
-    workspace: torch.Tensor
-    d_file_start: torch.Tensor
-    d_file_off: torch.Tensor
-    max_recs: int
-    m: int
-    k: int
+    """Inputs / outputs of lsm_build_sst for nfile images.  The layout
+    (file_start, file_off, file_size) lives on the device; the host copies
+    are made on first use (prepare_sst_device computes the layout on the
+    device, so nothing is read back before the build)."""
+
+    def __init__(self, out, footer, workspace, d_file_start, d_file_off, max_recs, m, k, nfile,
+                 file_start=None, file_off=None, file_size=None, d_file_size=None):
+        self.out, self.footer, self.workspace = out, footer, workspace
+        self.d_file_start, self.d_file_off, self.d_file_size = d_file_start, d_file_off, d_file_size
+        self.max_recs, self.m, self.k, self.nfile = max_recs, m, k, nfile
+        self._file_start, self._file_off, self._file_size = file_start, file_off, file_size
+
+    @staticmethod
+    def _host(t, n):
+        return t[:n].cpu().numpy().view(np.uint64).copy()
+
+    @property
+    def file_start(self) -> np.ndarray:
+        if self._file_start is None:
+            self._file_start = self._host(self.d_file_start, self.nfile + 1)
+        return self._file_start
+
+    @property
+    def file_off(self) -> np.ndarray:
+        if self._file_off is None:
+            self._file_off = self._host(self.d_file_off, self.nfile)
+        return self._file_off
+
+    @property
+    def file_size(self) -> np.ndarray:
+        if self._file_size is None:
+            self._file_size = self._host(self.d_file_size, self.nfile)
+        return self._file_size
 
 
 def prepare_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
@@ -556,11 +577,11 @@ def prepare_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
         workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
         d_file_start=torch.from_numpy(file_start.view(np.int64)).to(dev),
         d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
-        max_recs=max_recs, m=m, k=k)
+        max_recs=max_recs, m=m, k=k, nfile=nf)
 
 
 def build_sst_into(ctx: Context, batch: RecordBatch, sb: SstBuild, stream=None) -> None:
-    nf = len(sb.file_start) - 1
+    nf = sb.nfile
     _lib.check(ctx.lib.lsm_build_sst(
         ctx.handle, _ptr(batch.keys), _ptr(batch.koff), _ptr(batch.vals), _ptr(batch.voff),
         _ptr(sb.d_file_start), nf, sb.max_recs, sb.m, sb.k, _ptr(sb.out), _ptr(sb.d_file_off),
@@ -606,6 +627,7 @@ class Merge:
     n: int
     nout: int = 0
     nfiles: int = 0
+    max_recs: int = 0  # the most pairs in one output file
 
 
 def alloc_merge(ctx: Context, n: int) -> Merge:
@@ -625,12 +647,12 @@ def merge_kvs_into(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
     """CompactAndMergeKVs (merge.go:42-94) over pairs given as descriptors
     (key: IDX/KV descriptor, value: V descriptor or None for KV records).
     tie=TIE_GOHEAP: equal keys in container/heap's pop order (exact)."""
-    counts = np.zeros(2, np.uint64)
+    counts = np.zeros(3, np.uint64)
     _lib.check(ctx.lib.lsm_merge_kvs_tie(
         ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), r.n, level, threshold, tie,
         _ptr(r.out), _ptr(r.file_start), counts.ctypes.data, _ptr(r.workspace),
         r.workspace.numel(), _stream_handle(stream)), "lsm_merge_kvs_tie")
-    r.nout, r.nfiles = int(counts[0]), int(counts[1])
+    r.nout, r.nfiles, r.max_recs = int(counts[0]), int(counts[1]), int(counts[2])
     return r
 
 
@@ -674,32 +696,34 @@ def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
 
 
 def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Tensor, nfile: int,
+                       max_recs: int, val_bytes: Optional[int] = None,
                        m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K,
-                       align: int = 16) -> "SstBuild":
-    """prepare_sst for a device-resident batch: image sizes by
-    lsm_sst_image_sizes, then the layout from nfile + 1 small values."""
+                       align: int = 16, stream=None) -> "SstBuild":
+    """prepare_sst for a device-resident batch (a merge's output): the layout
+    by lsm_sst_layout on the device, nothing read back.  max_recs = the merge's
+    most pairs per file (Merge.max_recs); the image buffer is sized from the
+    header's bound (batch.keys bounds the key bytes, val_bytes -- or
+    batch.vals -- the value bytes)."""
     dev = ctx.torch_device
-    d_size = torch.zeros(max(nfile, 1), dtype=torch.int64, device=dev)
-    _lib.check(ctx.lib.lsm_sst_image_sizes(
-        ctx.handle, _ptr(batch.koff), _ptr(batch.voff), _ptr(d_file_start), nfile, m,
-        _ptr(d_size), _stream_handle(None)), "lsm_sst_image_sizes")
-    sizes = d_size[:nfile].cpu().numpy().view(np.uint64)
-    file_start = d_file_start[:nfile + 1].cpu().numpy().view(np.uint64).copy()
-    padded = (sizes + (align - 1)) // align * align
-    file_off = np.zeros(nfile, dtype=np.uint64)
-    if nfile:
-        file_off[1:] = np.cumsum(padded)[:-1]
-    total = int(padded.sum())
-    max_recs = int(np.diff(file_start.astype(np.int64)).max()) if nfile else 0
+    if val_bytes is None:
+        if batch.vals is None:
+            raise ValueError("prepare_sst_device: val_bytes is required for a keys-only batch")
+        val_bytes = int(batch.vals.numel())
+    fbytes = int(ctx.lib.lsm_filter_block_size(m))
+    bound = (nfile * (fbytes + 40 + align - 1) + 16 * batch.n + 3 * int(batch.keys.numel()) +
+             int(val_bytes))
+    d_size = torch.empty(max(nfile, 1), dtype=torch.int64, device=dev)
+    d_off = torch.empty(nfile + 1, dtype=torch.int64, device=dev)
+    _lib.check(ctx.lib.lsm_sst_layout(
+        ctx.handle, _ptr(batch.koff), _ptr(batch.voff), _ptr(d_file_start), nfile, m, align,
+        _ptr(d_size), _ptr(d_off), _stream_handle(stream)), "lsm_sst_layout")
     ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nfile, max_recs, m, k))
     return SstBuild(  # every image byte is written by lsm_build_sst: no fill
-        out=torch.empty(pad16(total), dtype=torch.uint8, device=dev),
-        file_start=file_start, file_off=file_off, file_size=sizes.copy(),
+        out=torch.empty(pad16(bound), dtype=torch.uint8, device=dev),
         footer=torch.zeros(max(nfile, 1) * 4, dtype=torch.int64, device=dev),
         workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
-        d_file_start=d_file_start[:nfile + 1].contiguous(),
-        d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
-        max_recs=max_recs, m=m, k=k)
+        d_file_start=d_file_start[:nfile + 1], d_file_off=d_off, d_file_size=d_size,
+        max_recs=max_recs, m=m, k=k, nfile=nfile)
 
 
 def sst_pairs_into(ctx: Context, r: "SstDecode", key_out: torch.Tensor, val_out: torch.Tensor,
@@ -729,7 +753,7 @@ def build_sst_views_into(ctx: Context, batch: RecordBatch, sb: "SstBuild", d_byt
                          idx: torch.Tensor, stream=None) -> None:
     """lsm_build_sst_views: the images of a keys-only gathered batch, values
     read in place from their views (value i = view of pair idx[i])."""
-    nf = len(sb.file_start) - 1
+    nf = sb.nfile
     _lib.check(ctx.lib.lsm_build_sst_views(
         ctx.handle, _ptr(batch.keys), _ptr(batch.koff), _ptr(d_bytes), _ptr(key_desc),
         _ptr(val_desc), _ptr(idx), _ptr(batch.voff), _ptr(sb.d_file_start), nf, sb.max_recs, sb.m,

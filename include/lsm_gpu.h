@@ -31,8 +31,9 @@ extern "C" {
 #endif
 
 /* v3: the input slack grew from 16 to 32 bytes (a binding built for v2 pads
- * too little); lsm_input_slack() reports it at run time. */
-#define LSM_ABI_VERSION 3
+ * too little); lsm_input_slack() reports it at run time.
+ * v4: lsm_merge_kvs / lsm_merge_kvs_tie write 3 h_counts entries (was 2). */
+#define LSM_ABI_VERSION 4
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
 /* Record grammars (all fixed-width little-endian). */
@@ -382,7 +383,9 @@ int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint
  *
  * Outputs: d_out[0 .. nout) = input indices of the written pairs, in order;
  * d_file_start[0 .. nfiles] = each file's first position in d_out (optional,
- * n + 1 entries), d_file_start[nfiles] = nout; h_counts (host) = {nout, nfiles}.
+ * n + 1 entries), d_file_start[nfiles] = nout; h_counts (host, 3 entries) =
+ * {nout, nfiles, the most pairs in one file} (the last sizes lsm_build_sst's
+ * max_file_records with no second read-back; ABI 4, was 2 entries).
  * Synchronizes the stream (the radix passes are chosen from key statistics). */
 size_t lsm_merge_kvs_workspace_bytes(uint64_t n);
 enum lsm_tie {
@@ -431,6 +434,17 @@ int lsm_sst_pairs(lsm_ctx *ctx, const lsm_sst_meta *d_meta, const uint64_t *d_fi
 int lsm_sst_image_sizes(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff,
                         const uint64_t *d_file_start, uint32_t nfile, uint64_t m,
                         uint64_t *d_size, void *stream);
+
+/* The images' layout without a host round trip: d_size[f] as
+ * lsm_sst_image_sizes, d_file_off[f] = the sum of the earlier sizes, each
+ * rounded up to `align` (> 0), and d_file_off[nfile] = the total (nfile + 1
+ * entries) -- lsm_build_sst's d_file_off, ready on the device.  The output
+ * buffer can be sized from host-known bounds: the total is at most
+ * nfile * (lsm_filter_block_size(m) + 40 + align - 1) + 16 * nrec
+ * + 3 * key bytes + value bytes.  Asynchronous. */
+int lsm_sst_layout(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff,
+                   const uint64_t *d_file_start, uint32_t nfile, uint64_t m, uint32_t align,
+                   uint64_t *d_size, uint64_t *d_file_off, void *stream);
 
 #ifdef __cplusplus
 }

@@ -173,7 +173,8 @@ def test_gather_and_build_match_oracle_images(ctx):
     assert np.array_equal(batch.voff.cpu().numpy().view(np.uint64), voff)
     assert batch.keys[:len(keys)].cpu().numpy().tobytes() == keys
     assert batch.vals[:len(vals)].cpu().numpy().tobytes() == vals
-    sb = lsmgpu.prepare_sst_device(ctx, batch, r.file_start, r.nfiles, m=20_000, k=5)
+    assert r.max_recs == int(np.diff(starts.astype(np.int64)).max())
+    sb = lsmgpu.prepare_sst_device(ctx, batch, r.file_start, r.nfiles, r.max_recs, m=20_000, k=5)
     lsmgpu.build_sst_into(ctx, batch, sb)
     torch.cuda.synchronize()
     img = sb.out.cpu().numpy()
@@ -183,11 +184,18 @@ def test_gather_and_build_match_oracle_images(ctx):
         o = int(sb.file_off[f])
         assert int(sb.file_size[f]) == want.size
         assert np.array_equal(img[o:o + want.size], want), f
+    # lsm_sst_layout: 16-byte aligned exclusive offsets, the total in the last
+    # entry, inside the bound the buffer was sized by
+    pad = (sb.file_size + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    assert np.array_equal(sb.file_off, np.concatenate([[0], np.cumsum(pad)[:-1]]).astype(np.uint64))
+    total = int(sb.d_file_off[r.nfiles].item())
+    assert total == int(pad.sum()) and total <= sb.out.numel()
     # values read in place: keys-only gather + lsm_build_sst_views, same images
     for kv_layout in (False, True):
         r2, d_buf2, d_kd2, d_vd2, got2, _ = run(ctx, pairs, 6, 200_000, kv_layout=kv_layout)
         kb2 = lsmgpu.gather_kvs(ctx, d_buf2, d_kd2, d_vd2, r2.out, r2.nout, kb, None)
-        sb2 = lsmgpu.prepare_sst_device(ctx, kb2, r2.file_start, r2.nfiles, m=20_000, k=5)
+        sb2 = lsmgpu.prepare_sst_device(ctx, kb2, r2.file_start, r2.nfiles, r2.max_recs,
+                                        val_bytes=vb, m=20_000, k=5)
         lsmgpu.build_sst_views_into(ctx, kb2, sb2, d_buf2, d_kd2, d_vd2, r2.out)
         torch.cuda.synchronize()
         img2 = sb2.out.cpu().numpy()
@@ -215,7 +223,8 @@ def test_build_views_dword_aligned_values(ctx):
             koff = np.concatenate([[0], np.cumsum([len(ps[i][0]) for i in got])]).astype(np.uint64)
             voff = np.concatenate([[0], np.cumsum([len(ps[i][1]) for i in got])]).astype(np.uint64)
             kb = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, r.out, r.nout, len(keys), None)
-            sb = lsmgpu.prepare_sst_device(ctx, kb, r.file_start, r.nfiles, m=20_000, k=5)
+            sb = lsmgpu.prepare_sst_device(ctx, kb, r.file_start, r.nfiles, r.max_recs,
+                                           val_bytes=len(vals), m=20_000, k=5)
             lsmgpu.build_sst_views_into(ctx, kb, sb, d_buf, d_kd, d_vd, r.out)
             torch.cuda.synchronize()
             img = sb.out.cpu().numpy()
