@@ -1351,6 +1351,175 @@ __global__ __launch_bounds__(256) void sst_vregion_views_kernel(SstArgs a, VView
     }
 }
 
+// The same data region when the values are V descriptors of decoded data
+// regions (lsm_decode_sst's data_desc): a V record [u32 vlen][value] is
+// byte-identical to the source record its descriptor points at (rec_off is
+// the record's own length prefix, the grammar is the same), so the output is
+// a segmented copy of source records (a descriptor whose source prefix does
+// not hold its length -- any caller-made view -- gets its prefix from the
+// descriptor instead, as a run of its own).  Consecutive records that were
+// consecutive in their source (a run: every stretch of pairs taken from one
+// input file) are one shifted memcpy.  One wave per 64 records: lanes mark
+// where their record does not continue the previous lane's source, the runs
+// (output start, source start) go to LDS, and each lane then writes whole
+// 16-byte output segments: the segment's run by a binary search over the
+// runs, two aligned 16-byte source loads funnel-shifted into one 16-byte
+// store.  Segments that straddle a run boundary are assembled byte by byte;
+// the two segments cut by the wave's range [A, B) are written a byte at a
+// time (the neighbouring waves own their other bytes).
+constexpr uint32_t kVrUnroll = 4;  // segments per lane in flight
+
+__device__ __forceinline__ uint32_t pick8(const u32x4 &x, const u32x4 &y, uint32_t i) {
+    const uint32_t a = (i & 3) == 0 ? x.x : (i & 3) == 1 ? x.y : (i & 3) == 2 ? x.z : x.w;
+    const uint32_t b = (i & 3) == 0 ? y.x : (i & 3) == 1 ? y.y : (i & 3) == 2 ? y.z : y.w;
+    return i < 4 ? a : b;
+}
+
+__global__ __launch_bounds__(256) void sst_vregion_runs_kernel(SstArgs a, VViewArgs v) {
+    constexpr uint32_t W = kSstWaves;
+    __shared__ uint32_t s_d[W][kWave + 1];  // run q's first output byte - A; [nrun] = B - A
+    __shared__ uint64_t s_in[W][kWave];     // run q's first source byte
+    __shared__ uint32_t s_fix[W][kWave];    // run q's prefix from the descriptor: vlen + 1, or 0
+    __shared__ uint32_t s_slow[W][2 * kWave + 4];  // segments not inside one run
+    const uint32_t f = blockIdx.x, w = threadIdx.x / kWave, lane = lane_id();
+    const SstLayout L = sst_layout(a, f);
+    const uint64_t c0 = L.s + (uint64_t)blockIdx.y * kSstChunkRecs + (uint64_t)w * kWave;
+    if (c0 >= L.e) return;
+    const uint32_t cnt = (uint32_t)((L.e - c0) < (uint64_t)kWave ? (L.e - c0) : kWave);
+    const uint64_t Vs = uni64(a.voff[L.s]);
+    // record j's prefix at out + rbase + 4 j + voff[j]
+    const uint64_t rbase = uni64(a.file_off[f]) + L.data_off - 4 * L.s - Vs;
+    uint64_t d0 = 0, in0 = 0, in1 = 0;
+    uint32_t vl = 0;
+    bool bad = false;
+    if (lane < cnt) {
+        const uint64_t j = c0 + lane;
+        const u32x4 d = v.vd[v.idx[j]];
+        in0 = (uint64_t)d.y << 32 | d.x;  // the record's length prefix
+        vl = d.w;
+        in1 = in0 + 4 + vl;
+        d0 = rbase + 4 * j + a.voff[j];
+        const gptr_t<const uint8_t> pb = gbl(v.bytes) + in0;
+        bad = ((uint32_t)pb[0] | (uint32_t)pb[1] << 8 | (uint32_t)pb[2] << 16 |
+               (uint32_t)pb[3] << 24) != vl;
+    }
+    const uint64_t A = lane64(d0, 0);
+    const uint64_t B = uni64(rbase + 4 * (c0 + cnt) + a.voff[c0 + cnt]);
+    const uint64_t prev = __shfl_up(in1, 1);
+    const bool prev_bad = __shfl_up((uint32_t)bad, 1) != 0;
+    const bool brk = lane < cnt && (lane == 0 || prev != in0 || bad || prev_bad);
+    const uint64_t bm = __ballot(brk);
+    const uint32_t nrun = (uint32_t)__builtin_popcountll(bm);
+    if (brk) {
+        const uint32_t q = mbcnt(bm);
+        s_d[w][q] = (uint32_t)(d0 - A);
+        s_in[w][q] = in0;
+        s_fix[w][q] = bad ? vl + 1 : 0;
+    }
+    if (lane == 0) s_d[w][nrun] = (uint32_t)(B - A);
+    vv_sync();
+    const uint64_t X = A & ~(uint64_t)15;
+    const uint32_t nseg = (uint32_t)((B - X + 15) >> 4);
+    const uint32_t head = (uint32_t)(A - X);  // segment 0 starts head bytes before A
+    const uint32_t tot = (uint32_t)(B - A);
+    const gptr_t<uint8_t> out = gbl(a.out);
+    const gptr_t<const uint8_t> vb = gbl(v.bytes);
+    // the run holding output byte r (relative to A): the last q with s_d[q] <= r
+    auto run_of = [&](uint32_t r) {
+        uint32_t lo = 0, hi = nrun;  // s_d[lo] <= r < s_d[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_d[w][mid] <= r) lo = mid; else hi = mid;
+        }
+        return lo;
+    };
+    // 1. whole segments inside one run: one 16-byte store each; the others
+    //    (a run boundary or an end of [A, B) inside) are listed
+    uint32_t nslow = 0;
+    for (uint32_t eb = 0; eb < nseg; eb += kWave * kVrUnroll) {
+        u32x4 x0[kVrUnroll], x1[kVrUnroll];
+        uint32_t sh[kVrUnroll];
+        bool fast[kVrUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kVrUnroll; u++) {
+            const uint32_t e = eb + u * kWave + lane;
+            const int64_t r0 = 16 * (int64_t)e - (int64_t)head;  // segment's first byte - A
+            fast[u] = false;
+            sh[u] = 0;
+            x0[u] = x1[u] = u32x4{0, 0, 0, 0};
+            if (e < nseg && r0 >= 0 && r0 + 16 <= (int64_t)tot) {
+                const uint32_t q = run_of((uint32_t)r0);
+                if ((uint32_t)r0 + 16 <= s_d[w][q + 1] && (!s_fix[w][q] || (uint32_t)r0 >= s_d[w][q] + 4)) {
+                    const uint64_t src = s_in[w][q] + ((uint32_t)r0 - s_d[w][q]);
+                    const gptr_t<const u32x4> p = gbl_at<const u32x4>(
+                        reinterpret_cast<uintptr_t>(v.bytes) + (src & ~(uint64_t)15));
+                    x0[u] = p[0];
+                    x1[u] = p[1];
+                    sh[u] = (uint32_t)src & 15;
+                    fast[u] = true;
+                }
+            }
+            const uint64_t sm = __ballot(e < nseg && !fast[u]);
+            if (e < nseg && !fast[u]) s_slow[w][nslow + mbcnt(sm)] = e;
+            nslow += (uint32_t)__builtin_popcountll(sm);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kVrUnroll; u++) {
+            if (!fast[u]) continue;
+            const uint32_t e = eb + u * kWave + lane;
+            const uint32_t d = sh[u] >> 2;
+            const uint32_t w0 = pick8(x0[u], x1[u], d), w1 = pick8(x0[u], x1[u], d + 1),
+                           w2 = pick8(x0[u], x1[u], d + 2), w3 = pick8(x0[u], x1[u], d + 3),
+                           w4 = pick8(x0[u], x1[u], d + 4);
+            *(gptr_t<u32x4>)(out + X + 16 * (uint64_t)e) =
+                u32x4{funnel(w0, w1, sh[u]), funnel(w1, w2, sh[u]), funnel(w2, w3, sh[u]),
+                      funnel(w3, w4, sh[u])};
+        }
+    }
+    vv_sync();
+    // 2. the listed segments, a lane each: every byte's source first, then
+    //    all 16 loads in flight at once; whole segments by one store, the two
+    //    cut by A and B a byte at a time
+    for (uint32_t i = lane; i < nslow; i += kWave) {
+        const uint32_t e = s_slow[w][i];
+        const int64_t r0 = 16 * (int64_t)e - (int64_t)head;
+        const bool whole = r0 >= 0 && r0 + 16 <= (int64_t)tot;
+        uint64_t src[16];
+        uint32_t fixb = 0, inr = 0;  // bit b: byte b from a descriptor / inside [A, B)
+        uint32_t pre[4] = {0, 0, 0, 0};
+        uint32_t q = run_of(r0 > 0 ? (uint32_t)r0 : 0);
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++) {
+            const int64_t r = r0 + b;
+            src[b] = s_in[w][q];  // harmless when unused
+            if (r < 0 || r >= (int64_t)tot) continue;
+            inr |= 1u << b;
+            while ((uint32_t)r >= s_d[w][q + 1]) q++;
+            const uint32_t t = (uint32_t)r - s_d[w][q];
+            const uint32_t fx = s_fix[w][q];
+            src[b] = s_in[w][q] + t;
+            if (fx && t < 4) {
+                fixb |= 1u << b;
+                pre[b >> 2] |= (((fx - 1) >> (8 * t)) & 0xFFu) << (8 * (b & 3));
+            }
+        }
+        uint32_t by[16];
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++) by[b] = vb[src[b]];
+        uint32_t wd[4] = {pre[0], pre[1], pre[2], pre[3]};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++)
+            if (!((fixb >> b) & 1)) wd[b >> 2] |= by[b] << (8 * (b & 3));
+        if (whole) {
+            *(gptr_t<u32x4>)(out + X + 16 * (uint64_t)e) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 16; b++)
+                if ((inr >> b) & 1) out[X + 16 * (uint64_t)e + b] = (uint8_t)(wd[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
 // Header, filter-block prefix and footer of file f (one wave; byte stores,
 // since the neighbouring bytes belong to other kernels).  The filter words
 // themselves are stored by the bloom kernels.
@@ -2289,8 +2458,14 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
         LSM_TRY(hipGetLastError());
         if (views && rc == 0) {
-            hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, rs, a,
-                               *views);
+            // V descriptors: the records are copied whole (runs); KV
+            // descriptors: each record assembled from its value view
+            if (views->vd)
+                hipLaunchKernelGGL(sst_vregion_runs_kernel, dim3(nfile, chunks), dim3(256), 0, rs, a,
+                                   *views);
+            else
+                hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, rs,
+                                   a, *views);
             LSM_TRY(hipGetLastError());
         }
     }

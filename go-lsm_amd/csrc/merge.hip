@@ -234,9 +234,11 @@ __device__ __forceinline__ uint64_t pext64(uint64_t v, uint64_t mask) {
     return r;
 }
 
-// sort key of sorted position j for one pass
+// sort key of sorted position j for one pass (32-bit keys when the pass
+// holds at most 32 varying bits: a third less traffic per radix pass)
+template <class K>
 __global__ __launch_bounds__(kMergeThreads) void merge_extract_kernel(MergeIn m, const uint32_t *perm,
-                                                                      SortGroup g, uint64_t *keys) {
+                                                                      SortGroup g, K *keys) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j >= m.n) return;
     const uint32_t i = perm ? perm[j] : j;
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_extract_kernel(MergeIn m,
         const uint32_t bits = (uint32_t)__builtin_popcountll(g.mask[t]);
         key = (bits >= 64 ? 0 : key << bits) | pext64(x, g.mask[t]);
     }
-    keys[j] = key;
+    keys[j] = (K)key;
 }
 
 __global__ __launch_bounds__(kMergeThreads) void merge_iota_kernel(uint32_t *perm, uint32_t n) {
@@ -893,10 +895,12 @@ struct MergeWs {
 };
 
 size_t sort_tmp_bytes(uint32_t n) {
-    size_t b = 0;
+    size_t b = 0, b32 = 0;
     (void)rocprim::radix_sort_pairs(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr,
                                     (uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 64);
-    return b;
+    (void)rocprim::radix_sort_pairs(nullptr, b32, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, 32);
+    return b > b32 ? b : b32;
 }
 
 MergeWs merge_ws_layout(uint8_t *base, uint32_t n) {
@@ -1067,16 +1071,26 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
             g.field[t] = fields[f1 - 1 - t].first;
             g.mask[t] = fields[f1 - 1 - t].second;
         }
-        hipLaunchKernelGGL(merge_extract_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m,
-                           have_perm ? w.perm[cur] : nullptr, g, w.keys[0]);
+        const bool k32 = bits <= 32;
+        uint32_t *keys32[2] = {reinterpret_cast<uint32_t *>(w.keys[0]),
+                               reinterpret_cast<uint32_t *>(w.keys[1])};
+        if (k32)
+            hipLaunchKernelGGL(merge_extract_kernel<uint32_t>, dim3(grid_for(n)), dim3(kMergeThreads),
+                               0, s, m, have_perm ? w.perm[cur] : nullptr, g, keys32[0]);
+        else
+            hipLaunchKernelGGL(merge_extract_kernel<uint64_t>, dim3(grid_for(n)), dim3(kMergeThreads),
+                               0, s, m, have_perm ? w.perm[cur] : nullptr, g, w.keys[0]);
         if (!have_perm) {
             hipLaunchKernelGGL(merge_iota_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s,
                                w.perm[cur], N);
             have_perm = true;
         }
         size_t tb = w.sort_bytes;
-        const hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, tb, w.keys[0], w.keys[1],
-                                                       w.perm[cur], w.perm[cur ^ 1], N, 0, bits, s);
+        const hipError_t e =
+            k32 ? rocprim::radix_sort_pairs(w.sort_tmp, tb, keys32[0], keys32[1], w.perm[cur],
+                                            w.perm[cur ^ 1], N, 0, bits, s)
+                : rocprim::radix_sort_pairs(w.sort_tmp, tb, w.keys[0], w.keys[1], w.perm[cur],
+                                            w.perm[cur ^ 1], N, 0, bits, s);
         if (e != hipSuccess) return -(1000 + (int)e);
         cur ^= 1;
         f0 = f1;

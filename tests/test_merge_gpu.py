@@ -338,3 +338,46 @@ def test_full_size_compaction_merge_goheap(ctx):
                                   v["rec_off"] + 4, v["val_len"], 1, MiB2, ora.TIE_GOHEAP)
     assert np.array_equal(got, want) and np.array_equal(starts, wstarts)
     print(f"merge of {k.size} pairs: TIE_INPUT {t[0] * 1e3:.2f} ms, TIE_GOHEAP {t[1] * 1e3:.2f} ms")
+
+
+def test_full_size_compaction_build(ctx):
+    """Exactly what the compact bench times, at full size: decode -> join ->
+    merge -> keys-only gather -> lsm_sst_layout -> lsm_build_sst_views, whose
+    data regions are copied as runs of whole source records.  The images must
+    equal, byte for byte, those lsm_build_sst writes from a gathered copy of
+    the values, and three files must equal the oracle's build."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench_compact import build_images, level0_runs
+    from lsmgpu import synth
+    n1 = 100_000 * 33
+    img, file_off, file_size = build_images(ctx, level0_runs(n1, 0, 0) + [synth.kv_stream(n1)])
+    r = lsmgpu.alloc_sst_decode(ctx, file_off, file_size, int(img.numel()))
+    lsmgpu.decode_sst_into(ctx, img, r)
+    kd, vd, prefix = lsmgpu.sst_pairs(ctx, r)
+    meta = r.meta_numpy()
+    key_bytes = int(meta["idx_size"].astype(np.int64).sum())
+    val_bytes = int(meta["data_size"].astype(np.int64).sum())
+    m = lsmgpu.merge_kvs(ctx, img, kd, vd, level=1)
+    kb = lsmgpu.gather_kvs(ctx, img, kd, vd, m.out, m.nout, key_bytes, None)
+    sb = lsmgpu.prepare_sst_device(ctx, kb, m.file_start, m.nfiles, m.max_recs, val_bytes=val_bytes)
+    lsmgpu.build_sst_views_into(ctx, kb, sb, img, kd, vd, m.out)
+    full = lsmgpu.gather_kvs(ctx, img, kd, vd, m.out, m.nout, key_bytes, val_bytes)
+    sb2 = lsmgpu.prepare_sst_device(ctx, full, m.file_start, m.nfiles, m.max_recs)
+    lsmgpu.build_sst_into(ctx, full, sb2)
+    torch.cuda.synchronize()
+    assert m.nfiles >= 200 and m.max_recs == int(np.diff(sb.file_start.astype(np.int64)).max())
+    assert np.array_equal(sb.file_off, sb2.file_off) and np.array_equal(sb.file_size, sb2.file_size)
+    total = int(sb.d_file_off[m.nfiles].item())
+    assert torch.equal(sb.out[:total], sb2.out[:total])
+    koff = full.koff[:m.nout + 1].cpu().numpy().view(np.uint64)
+    voff = full.voff[:m.nout + 1].cpu().numpy().view(np.uint64)
+    keys = full.keys[:int(koff[-1]) + 16].cpu().numpy()
+    vals = full.vals[:int(voff[-1]) + 16].cpu().numpy()
+    out = sb.out[:total].cpu().numpy()
+    for f in (0, m.nfiles // 2, m.nfiles - 1):
+        want, _ = ora.build_sst(keys, koff, vals, voff, int(sb.file_start[f]), int(sb.file_start[f + 1]))
+        o = int(sb.file_off[f])
+        assert int(sb.file_size[f]) == want.size
+        assert np.array_equal(out[o:o + want.size], want), f
