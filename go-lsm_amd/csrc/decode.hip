@@ -26,6 +26,25 @@ constexpr uint32_t kRingChunks = 8;  // 8 KiB ring: 4 KiB blocks fit whole, 64 K
 // once; keeping the stream out of the L2/MALL's normal replacement measured
 // 80.5 -> 71.7 us for decode4k's memory pattern (tools/block_probe.py).
 constexpr int kBlockLoadAux = 2;
+// Per ring size (A/B on one box, wall GiB/s: resident / rotated copies / one
+// 1M-block launch): the 8 KiB ring (4 KiB blocks) stores its descriptors nt
+// too: 4,800 / 4,045 / 4,100 with plain stores, 4,836 / 4,800 / 4,650 with nt
+// stores.  ARENA on the 8 KiB ring also loads the blocks with the default
+// policy (2,150 -> 2,290 GiB/s).  The 16 KiB ring (64 KiB blocks) and the
+// 2 KiB ring (mixed, scheduled) keep plain stores: nt stores measured 4,530
+// -> 4,140 and 5,030 -> 4,850 GiB/s there.
+template <uint32_t NCH, bool ARENA>
+struct RingPolicy {
+    static constexpr int load_aux = (ARENA && NCH == 8) ? 0 : kBlockLoadAux;
+    static constexpr bool nt_desc = NCH == 8;
+};
+template <uint32_t NCH, bool ARENA>
+__device__ __forceinline__ void store_desc(u32x4 *p, const u32x4 &d) {
+    if (RingPolicy<NCH, ARENA>::nt_desc)
+        __builtin_nontemporal_store(d, p);
+    else
+        *p = d;
+}
 
 
 struct DecodeArgs {
@@ -63,7 +82,7 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t k) {
 #undef LSM_VMW
 }
 
-template <uint32_t NCH>
+template <uint32_t NCH, int AUX = kBlockLoadAux>
 struct BlockReaderT {
     uint32_t *ring;
     rsrc_t rsrc;
@@ -105,7 +124,7 @@ struct BlockReaderT {
             for (uint32_t c = hi_c > c0 ? hi_c : c0; c < last; c++)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rsrc, (__attribute__((address_space(3))) void *)&ring[(c % NCH) * (kChunk / 4)],
-                    16, voff + c * kChunk, 0, 0, kBlockLoadAux);
+                    16, voff + c * kChunk, 0, 0, AUX);
             hi_c = last;
         }
         uint64_t need_end = (uint64_t)s0 + want;
@@ -490,7 +509,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     // then always indexed modulo its size, which is the same for such blocks)
     const bool lin = ARENA ? lin_rt : LIN;
     const uint32_t lane = lane_id();
-    BlockReaderT<NCH> rd;
+    BlockReaderT<NCH, RingPolicy<NCH, ARENA>::load_aux> rd;
     rd.init(ring, a.in, off, n);
     RingBytes<NCH, LIN> rb{ring, rd.rsrc, 0, 0};
 
@@ -535,7 +554,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                 d.y = (uint32_t)(ro >> 32);
                 d.z = s_k;
                 d.w = s_v;
-                a.desc[base + s_first + lane] = d;
+                store_desc<NCH, ARENA>(&a.desc[base + s_first + lane], d);
                 if (G == LSM_GRAMMAR_IDX && a.idx_value)
                     a.idx_value[base + s_first + lane] = (int64_t)((uint64_t)s_xhi << 32 | s_xlo);
             }
@@ -746,7 +765,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
                 d.y = (uint32_t)(ro >> 32);
                 d.z = K;
                 d.w = V;
-                a.desc[base + nr + lane] = d;
+                store_desc<NCH, ARENA>(&a.desc[base + nr + lane], d);
                 if (G == LSM_GRAMMAR_IDX && a.idx_value) a.idx_value[base + nr + lane] = (int64_t)xx;
             }
             if (ARENA && j + pend) {

@@ -15,7 +15,7 @@ for line in ${LINES:-decode4k}; do
   for v in $VARIANTS; do
     lib=ab/$v.so; [ $v = prod ] && lib=go-lsm_amd/liblsm_gpu.so
     timeout -k 10 240 python scripts/ab_lib.py $lib $args --steps ${STEPS:-100} --warmup 10 > gpurun_out/abp_$v.json 2> gpurun_out/abp_$v.err || { tail -5 gpurun_out/abp_$v.err; exit 1; }
-    python3 -c "import json,sys; j=json.load(open('gpurun_out/abp_$v.json')); r=j['roofline']; print('$v', '$line', j['value'], j['ms_per_step'], r['kernel_ms'], r.get('kernel_ms_median'), r['frac'])"
+    python3 -c "import json,sys; j=json.load(open('gpurun_out/abp_$v.json')); r=j['roofline']; print('$v', '$line', j['value'], j['ms_per_step'], r['kernel_ms'], r.get('kernel_ms_median'), r['frac'], 'cold', (j.get('cold_input') or {}).get('value'))"
   done
 done
 done
