@@ -1973,7 +1973,8 @@ __global__ __launch_bounds__(256) void wal_compact_kernel(WalArgs a) {
     u32x4 *dst = reinterpret_cast<u32x4 *>(a.out.desc);
     const u32x4 *src = a.scratch + (q * 2 + (cf >> 31)) * kWalSegSlots;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
-        if ((uint64_t)pre + j < cap) dst[base + pre + j] = src[j];
+        if ((uint64_t)pre + j < cap)  // nt: written once (A/B: 997 -> 1,017 GiB/s)
+            __builtin_nontemporal_store(src[j], &dst[base + pre + j]);
 }
 
 }  // namespace
