@@ -1135,6 +1135,7 @@ struct SstWork {
     uint32_t k0, spec_cnt;     // index stride hypothesis: key length, entries to test
     uint32_t idx_overrun;      // IndexHandle.Size runs past the end of the file
     uint32_t data_neg;         // DataHandle.Offset < 0: the seek fails
+    uint32_t spec_ok;          // the stride hypothesis held for the whole index (fixup)
 };
 
 // SSTable.DecodeFrom's framing (sstable.go:87-128) as the oracle restates it
@@ -1191,7 +1192,8 @@ struct SstArgs {
     int64_t *idx_value;
     u32x4 *data_desc;
     SstWork *work;
-    uint32_t *fail;  // [2f] first unverified index entry, [2f+1] first unverified value
+    uint32_t *fail;  // [3f] first unverified index entry, [3f+1] first unverified value,
+                     // [3f+2] the same under the stride hypothesis (sst_index_kernel)
 };
 
 __device__ __forceinline__ void sst_slots(const SstArgs &a, uint32_t f, uint64_t foff, uint64_t n,
@@ -1225,11 +1227,24 @@ __global__ __launch_bounds__(256) void sst_index_kernel(SstArgs a) {
     }
     __syncthreads();
     if (W.m.stage != 0) return;
+    // Entry i at io + i S (the stride hypothesis: every key has the first
+    // key's length), and in the same pass value i, located by the entry's
+    // offset and checked against the next entry's (sst_data_verify_kernel's
+    // rule).  The value checks stand only if the hypothesis holds for the
+    // whole index; sst_index_fixup_kernel decides, and otherwise
+    // sst_data_verify_kernel checks the values again from the final offsets.
     const uint64_t S = 12ull + W.k0;
+    const uint64_t doff = (uint64_t)W.m.data_off, dl = W.dl;
+    const bool whole = (uint64_t)W.spec_cnt * S == W.il && !W.idx_overrun;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W.spec_cnt;
          i += gridDim.x * blockDim.x) {
         const uint64_t p = W.io + (uint64_t)i * S;
-        if (R.u32(p) == W.k0) {
+        const bool ok = R.u32(p) == W.k0;
+        // the next entry's key length and offset: one round trip with this one's
+        const bool has_next = i + 1 < W.spec_cnt;
+        const uint32_t k_next = has_next ? R.u32(p + S) : W.k0;
+        const uint64_t o_next = has_next ? R.u64(p + S + 4 + W.k0) : 0;
+        if (ok) {
             const uint64_t ro = foff + p;
             u32x4 d;
             d.x = (uint32_t)ro;
@@ -1239,9 +1254,28 @@ __global__ __launch_bounds__(256) void sst_index_kernel(SstArgs a) {
             // nt: the views are read by a later call, not by this one
             // (the f1 line: 141 -> 135 us per call)
             __builtin_nontemporal_store(d, &a.idx_desc[W.base + i]);
-            a.idx_value[W.base + i] = (int64_t)R.u64(p + 4 + W.k0);
+            const uint64_t v = R.u64(p + 4 + W.k0);
+            a.idx_value[W.base + i] = (int64_t)v;
+            if (!W.data_neg && (has_next ? k_next == W.k0 : whole)) {
+                const uint64_t pos = v - doff;  // value i, region-relative
+                bool bad = dl < 4 || pos > dl - 4 || (i == 0 && pos != 0);
+                if (!bad) {
+                    const uint32_t vl = R.u32(W.dof + pos);
+                    const uint64_t e = pos + 4 + vl;  // where value i ends
+                    const uint64_t next = has_next ? o_next - doff : dl;
+                    bad = e > dl || e != next;
+                    const uint64_t vo = foff + W.dof + pos;
+                    u32x4 dd;
+                    dd.x = (uint32_t)vo;
+                    dd.y = (uint32_t)(vo >> 32);
+                    dd.z = 0;
+                    dd.w = vl;
+                    __builtin_nontemporal_store(dd, &a.data_desc[W.base + i]);
+                }
+                if (bad) atomicMin(&a.fail[3 * f + 2], i);
+            }
         } else {
-            atomicMin(&a.fail[2 * f], i);
+            atomicMin(&a.fail[3 * f], i);
         }
     }
 }
@@ -1252,13 +1286,14 @@ __global__ __launch_bounds__(64) void sst_index_fixup_kernel(SstArgs a) {
     SstWork &W = a.work[f];
     if (uni((uint32_t)W.m.stage) != 0) return;
     const uint32_t spec = uni(W.spec_cnt);
-    const uint32_t fl = uni(a.fail[2 * f]);
+    const uint32_t fl = uni(a.fail[3 * f]);
     const uint32_t i0 = fl < spec ? fl : spec;
     const uint64_t S = 12ull + uni(W.k0), il = uni64(W.il);
     const bool overrun = uni(W.idx_overrun) != 0;
     uint32_t nidx;
     int32_t st = LSM_OK;
-    if (i0 == spec && (uint64_t)spec * S == il && !overrun) {
+    const bool hyp = i0 == spec && (uint64_t)spec * S == il && !overrun;
+    if (hyp) {
         nidx = spec;
     } else {
         DecodeArgs d = {};
@@ -1275,6 +1310,8 @@ __global__ __launch_bounds__(64) void sst_index_fixup_kernel(SstArgs a) {
     }
     if (lane_id() == 0) {
         W.m.nidx = nidx;
+        W.spec_ok = hyp;  // the values were checked with the index (sst_index_kernel)
+        if (hyp) a.fail[3 * f + 1] = a.fail[3 * f + 2];
         if (st != LSM_OK) {
             W.m.stage = LSM_SST_INDEX;
             W.m.status = st;
@@ -1287,7 +1324,7 @@ __global__ __launch_bounds__(256) void sst_data_verify_kernel(SstArgs a) {
     const uint32_t f = blockIdx.y;
     if (threadIdx.x == 0) W = a.work[f];
     __syncthreads();
-    if (W.m.stage != 0 || W.data_neg) return;
+    if (W.m.stage != 0 || W.data_neg || W.spec_ok) return;
     const uint64_t foff = a.file_off[f];
     ImgReader R;
     R.init(a.img, foff, a.file_len[f]);
@@ -1310,7 +1347,7 @@ __global__ __launch_bounds__(256) void sst_data_verify_kernel(SstArgs a) {
             d.w = v;
             __builtin_nontemporal_store(d, &a.data_desc[W.base + i]);
         }
-        if (bad) atomicMin(&a.fail[2 * f + 1], i);
+        if (bad) atomicMin(&a.fail[3 * f + 1], i);
     }
 }
 
@@ -1326,7 +1363,7 @@ __global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
         if (uni(W.data_neg)) {
             stage = LSM_SST_DATA;  // seek to a negative offset
         } else {
-            const uint32_t fl = uni(a.fail[2 * f + 1]);
+            const uint32_t fl = uni(a.fail[3 * f + 1]);
             const uint32_t f0 = nidx == 0 ? 0u : (fl < nidx ? fl : nidx);
             int32_t st = LSM_OK;
             if (nidx > 0 && f0 == nidx) {
@@ -2246,7 +2283,7 @@ extern "C" int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t
 }
 
 extern "C" size_t lsm_decode_sst_workspace_bytes(uint32_t nfile) {
-    return (size_t)nfile * (sizeof(SstWork) + 8) + 16;
+    return (size_t)nfile * (sizeof(SstWork) + 12) + 16;
 }
 
 extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
@@ -2275,7 +2312,7 @@ extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t
     a.work = static_cast<SstWork *>(d_workspace);
     a.fail = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_workspace) +
                                           (size_t)nfile * sizeof(SstWork));
-    LSM_HIP_CHECK(hipMemsetAsync(a.fail, 0xFF, (size_t)nfile * 8, s));
+    LSM_HIP_CHECK(hipMemsetAsync(a.fail, 0xFF, (size_t)nfile * 12, s));
     // parallel passes: ~kSstWgs workgroups over the batch, at most 64 per file
     constexpr uint32_t kSstWgs = 2048;
     uint32_t g = (kSstWgs + nfile - 1) / nfile;
