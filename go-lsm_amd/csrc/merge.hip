@@ -273,9 +273,12 @@ __device__ __forceinline__ bool is_tombstone(const uint8_t *b, const View &v) {
 }
 
 // flags[j]: bit 0 = starts a group, bit 1 = may be written (not a tombstone
-// dropped at level 6)
+// dropped at level 6); csize[j] = the pair's EstimateSize (16 + key + value,
+// kv.go:118-121), which merge_candidate_kernel keeps or zeroes in place (the
+// view is loaded here anyway: no second gather through perm)
 __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, const uint32_t *perm,
-                                                                    int level, uint8_t *flags) {
+                                                                    int level, uint8_t *flags,
+                                                                    uint32_t *csize) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j >= m.n) return;
     const View v = view(m, perm[j]);
@@ -283,6 +286,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, c
     if (!gs) gs = !keys_equal(m.bytes, v, view(m, perm[j - 1]));
     const bool wr = level < 6 || !is_tombstone(m.bytes, v);
     flags[j] = (uint8_t)((gs ? 1 : 0) | (wr ? 2 : 0));
+    csize[j] = 16 + v.kl + v.vl;
 }
 
 // eq[j] = 1 when sorted position j holds the same key as j - 1 (plain key
@@ -299,7 +303,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_eq_kernel(MergeIn m, cons
 // dropped tombstones is scanned by one pair only (O(n) in total).
 // csize[j] = EstimateSize of a candidate (kv.go:118-121, >= 16), else 0.
 __global__ __launch_bounds__(kMergeThreads) void merge_candidate_kernel(MergeIn m,
-                                                                        const uint32_t *perm,
                                                                         const uint8_t *flags,
                                                                         uint32_t *csize) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
@@ -313,12 +316,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_candidate_kernel(MergeIn 
             if (g & 1) break;
         }
     }
-    uint32_t sz = 0;
-    if (c) {
-        const View v = view(m, perm[j]);
-        sz = 16 + v.kl + v.vl;
-    }
-    csize[j] = sz;
+    if (!c) csize[j] = 0;  // candidates keep the size merge_flags_kernel wrote
 }
 
 // ---- interleaved exclusive sums of candidate sizes and counts -----------
@@ -1126,9 +1124,9 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
 
     // 3. groups and candidates; 4. sums and the file walk; 5. emit
     hipLaunchKernelGGL(merge_flags_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m, perm,
-                       level, w.flags);
+                       level, w.flags, w.csize);
     hipLaunchKernelGGL(merge_candidate_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m,
-                       perm, w.flags, w.csize);
+                       w.flags, w.csize);
     const uint32_t ntiles = (N + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(merge_scan_tiles, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
                        w.scan_part);

@@ -17,5 +17,5 @@ if [ -n "$CFG" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$CFG -o run \
     -- python bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-cold > gpurun_out/prof_${TAG}_$CFG.log 2>&1 \
     || { tail -20 gpurun_out/prof_${TAG}_$CFG.log; exit 1; }
-  python scripts/kstats.py gpurun_out/prof_${TAG}_$CFG/run_kernel_stats.csv 63 | head -12
+  python scripts/kstats.py gpurun_out/prof_${TAG}_$CFG/run_kernel_stats.csv 63 | head -12 || true
 fi
