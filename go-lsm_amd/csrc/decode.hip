@@ -868,7 +868,7 @@ __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
 // ---- planning: exclusive scans over per-block quantities -----------------
 
 constexpr uint32_t kScanThreads = 256;
-constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanPer = 2;  // 16 (lanes 128 B apart) measured 1% slower on the compaction
 constexpr uint32_t kScanTile = kScanThreads * kScanPer;
 
 __device__ __forceinline__ uint64_t plan_value(int mode, uint32_t len) {
