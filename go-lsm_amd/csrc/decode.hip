@@ -33,9 +33,15 @@ constexpr int kBlockLoadAux = 2;
 // policy (2,150 -> 2,290 GiB/s).  The 16 KiB ring (64 KiB blocks) and the
 // 2 KiB ring (mixed, scheduled) keep plain stores: nt stores measured 4,530
 // -> 4,140 and 5,030 -> 4,850 GiB/s there.
-template <uint32_t NCH, bool ARENA>
+// A launch of more than kBigLaunch blocks on the 8 KiB ring (gigabytes of
+// input, far past the 256 MB MALL) loads its blocks with the default policy:
+// 1M blocks 4,610 -> 5,030 GiB/s, 500k 4,835 -> 4,945; at 250k and below nt
+// loads stay ahead (250k: 4,880 against 4,776; 100k, resident: 4,850 against
+// 4,600).
+constexpr uint32_t kBigLaunch = 400000;
+template <uint32_t NCH, bool ARENA, bool BIG = false>
 struct RingPolicy {
-    static constexpr int load_aux = (ARENA && NCH == 8) ? 0 : kBlockLoadAux;
+    static constexpr int load_aux = ((ARENA || BIG) && NCH == 8) ? 0 : kBlockLoadAux;
     static constexpr bool nt_desc = NCH == 8;
 };
 template <uint32_t NCH, bool ARENA>
@@ -501,7 +507,7 @@ struct ArenaCur {
 // `stop` are not decoded (a clean stop; stop = n decodes the whole range).
 // ARENA: keys and values are also packed into a.key_arena / a.val_arena from
 // the cursors `ac` (tab: the 129-dword LDS table of arena_emit_batch).
-template <int G, uint32_t NCH, bool LIN, bool ARENA = false>
+template <int G, uint32_t NCH, bool LIN, bool ARENA = false, bool BIG = false>
 __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t off, uint32_t n,
                                 uint64_t base, uint32_t ncap, uint32_t &nr_out, int32_t &st_out,
                                 uint32_t stop, uint32_t &pos_out, ArenaCur ac = {},
@@ -511,7 +517,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     // then always indexed modulo its size, which is the same for such blocks)
     const bool lin = ARENA ? lin_rt : LIN;
     const uint32_t lane = lane_id();
-    BlockReaderT<NCH, RingPolicy<NCH, ARENA>::load_aux> rd;
+    BlockReaderT<NCH, RingPolicy<NCH, ARENA, BIG>::load_aux> rd;
     rd.init(ring, a.in, off, n);
     RingBytes<NCH, LIN> rb{ring, rd.rsrc, 0, 0};
 
@@ -803,7 +809,7 @@ __device__ void decode_range_v2(const DecodeArgs &a, uint32_t *ring, uint64_t of
     pos_out = pos;
 }
 
-template <int G, uint32_t NCH, bool LIN, bool ARENA>
+template <int G, uint32_t NCH, bool LIN, bool ARENA, bool BIG = false>
 __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring, uint32_t *tab,
                                 uint64_t off, uint32_t n, bool lin_rt = LIN) {
     uint64_t base, cap;
@@ -815,7 +821,7 @@ __device__ void decode_block_v2(const DecodeArgs &a, uint32_t b, uint32_t *ring,
         ac.k = a.arena_base ? uni64(a.arena_base[b]) : off;
         ac.v = ac.k;
     }
-    decode_range_v2<G, NCH, LIN, ARENA>(a, ring, off, n, uni64(base),
+    decode_range_v2<G, NCH, LIN, ARENA, BIG>(a, ring, off, n, uni64(base),
                                         uni(cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu), nr,
                                         st, n, end, ac, tab, lin_rt);
     if (lane_id() == 0) {
@@ -839,7 +845,7 @@ __device__ void decode_range_any(const DecodeArgs &a, uint32_t *ring, uint64_t o
 
 // One wave (and one workgroup) per block; NCH x 1 KiB ring plus a guard
 // dword so linear reads of a block's last field stay inside the array.
-template <int G, uint32_t NCH, bool ARENA>
+template <int G, uint32_t NCH, bool ARENA, bool BIG = false>
 __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[NCH * kChunk / 4 + 4];
     __shared__ uint32_t tab[ARENA ? 129 : 1];
@@ -859,9 +865,9 @@ __global__ __launch_bounds__(64) void decode_v2_kernel(DecodeArgs a) {
         // what each alone does in 96
         decode_block_v2<G, NCH, false, true>(a, b, ring, tab, off, n, lin);
     } else if (lin) {
-        decode_block_v2<G, NCH, true, false>(a, b, ring, tab, off, n);
+        decode_block_v2<G, NCH, true, false, BIG>(a, b, ring, tab, off, n);
     } else {
-        decode_block_v2<G, NCH, false, false>(a, b, ring, tab, off, n);
+        decode_block_v2<G, NCH, false, false, BIG>(a, b, ring, tab, off, n);
     }
 }
 
@@ -965,7 +971,10 @@ int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void
 template <int G, bool ARENA, uint32_t NCH = kRingChunks>
 int launch_decode(const DecodeArgs &a, hipStream_t s) {
     static_assert(NCH >= 2, "a record header may straddle two ring chunks");
-    hipLaunchKernelGGL((decode_v2_kernel<G, NCH, ARENA>), dim3(a.nblk), dim3(kWave), 0, s, a);
+    if (!ARENA && NCH == kRingChunks && a.nblk > kBigLaunch && !a.order)
+        hipLaunchKernelGGL((decode_v2_kernel<G, NCH, false, true>), dim3(a.nblk), dim3(kWave), 0, s, a);
+    else
+        hipLaunchKernelGGL((decode_v2_kernel<G, NCH, ARENA>), dim3(a.nblk), dim3(kWave), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

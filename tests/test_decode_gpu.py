@@ -338,6 +338,38 @@ def test_bench_path_config2_full_size(ctx):
         bench.verify_decode(args, r, d_off, d_len, nblk)
 
 
+def test_large_launch_closed_form(ctx):
+    """A launch above kBigLaunch blocks (450k x 4 KiB config-2 blocks, 1.8 GB)
+    takes the large-launch instantiation (blocks loaded with the default
+    cache policy): every descriptor in closed form on the device, 64 sampled
+    blocks against the oracle."""
+    nblk = 450_000
+    buf, blk_off, blk_len = synth.uniform_kv_blocks(np.arange(nblk))
+    dev = ctx.torch_device
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.tensor(blk_off.view(np.int64), device=dev)
+    d_len = torch.tensor(blk_len.view(np.int32), device=dev)
+    r = lsmgpu.alloc_decode_offset(ctx, lsmgpu.GRAMMAR_KV, nblk, int(d_in.numel()))
+    r.desc.fill_(-1)
+    lsmgpu.decode_into(ctx, lsmgpu.GRAMMAR_KV, d_in, d_off, d_len, r)
+    torch.cuda.synchronize()
+    assert int((r.status[:nblk] != 0).sum()) == 0
+    assert bool((r.nrec[:nblk] == 33).all())
+    idx = (torch.arange(nblk, device=dev)[:, None] * 512
+           + torch.arange(33, device=dev)[None, :]).reshape(-1)
+    d = r.desc[idx].view(torch.int32).reshape(-1, 4).to(torch.int64)
+    want = (torch.arange(nblk, device=dev)[:, None] * 4096
+            + torch.arange(33, device=dev)[None, :] * 124).reshape(-1)
+    got = d[:, 0] + (d[:, 1] << 32)
+    assert torch.equal(got, want)
+    assert bool((d[:, 2] == 16).all()) and bool((d[:, 3] == 100).all())
+    sample = np.random.default_rng(3).choice(nblk, 64, replace=False)
+    for b in sample:
+        st, od, _ = ora.decode_block(1, buf, int(blk_off[b]), int(blk_len[b]))
+        rows = r.desc[b * 512: b * 512 + 33].cpu().numpy().view(np.uint8).view(lsmgpu.DESC_DTYPE).reshape(-1)
+        assert st == 0 and np.array_equal(rows, od), b
+
+
 def test_config5_mixed_sample(ctx):
     buf, blk_off, blk_len, nrec = synth.mixed_kv_blocks(24 << 20, seed=11)
     dev = ctx.torch_device
