@@ -1379,7 +1379,7 @@ __device__ __forceinline__ uint32_t pick8(const u32x4 &x, const u32x4 &y, uint32
 
 __global__ __launch_bounds__(256) void sst_vregion_runs_kernel(SstArgs a, VViewArgs v) {
     constexpr uint32_t W = kSstWaves;
-    __shared__ uint32_t s_d[W][kWave + 1];  // run q's first output byte - A; [nrun] = B - A
+    __shared__ uint64_t s_d[W][kWave + 1];  // run q's first output byte - A; [nrun] = B - A
     __shared__ uint64_t s_in[W][kWave];     // run q's first source byte
     __shared__ uint32_t s_fix[W][kWave];    // run q's prefix from the descriptor: vlen + 1, or 0
     __shared__ uint32_t s_slow[W][2 * kWave + 4];  // segments not inside one run
@@ -1414,20 +1414,20 @@ __global__ __launch_bounds__(256) void sst_vregion_runs_kernel(SstArgs a, VViewA
     const uint32_t nrun = (uint32_t)__builtin_popcountll(bm);
     if (brk) {
         const uint32_t q = mbcnt(bm);
-        s_d[w][q] = (uint32_t)(d0 - A);
+        s_d[w][q] = d0 - A;
         s_in[w][q] = in0;
         s_fix[w][q] = bad ? vl + 1 : 0;
     }
-    if (lane == 0) s_d[w][nrun] = (uint32_t)(B - A);
+    if (lane == 0) s_d[w][nrun] = B - A;
     vv_sync();
     const uint64_t X = A & ~(uint64_t)15;
     const uint32_t nseg = (uint32_t)((B - X + 15) >> 4);
     const uint32_t head = (uint32_t)(A - X);  // segment 0 starts head bytes before A
-    const uint32_t tot = (uint32_t)(B - A);
+    const uint64_t tot = B - A;  // 64 values may exceed 4 GB
     const gptr_t<uint8_t> out = gbl(a.out);
     const gptr_t<const uint8_t> vb = gbl(v.bytes);
     // the run holding output byte r (relative to A): the last q with s_d[q] <= r
-    auto run_of = [&](uint32_t r) {
+    auto run_of = [&](uint64_t r) {
         uint32_t lo = 0, hi = nrun;  // s_d[lo] <= r < s_d[hi]
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -1450,9 +1450,9 @@ __global__ __launch_bounds__(256) void sst_vregion_runs_kernel(SstArgs a, VViewA
             sh[u] = 0;
             x0[u] = x1[u] = u32x4{0, 0, 0, 0};
             if (e < nseg && r0 >= 0 && r0 + 16 <= (int64_t)tot) {
-                const uint32_t q = run_of((uint32_t)r0);
-                if ((uint32_t)r0 + 16 <= s_d[w][q + 1] && (!s_fix[w][q] || (uint32_t)r0 >= s_d[w][q] + 4)) {
-                    const uint64_t src = s_in[w][q] + ((uint32_t)r0 - s_d[w][q]);
+                const uint32_t q = run_of((uint64_t)r0);
+                if ((uint64_t)r0 + 16 <= s_d[w][q + 1] && (!s_fix[w][q] || (uint64_t)r0 >= s_d[w][q] + 4)) {
+                    const uint64_t src = s_in[w][q] + ((uint64_t)r0 - s_d[w][q]);
                     const gptr_t<const u32x4> p = gbl_at<const u32x4>(
                         reinterpret_cast<uintptr_t>(v.bytes) + (src & ~(uint64_t)15));
                     x0[u] = p[0];
@@ -1489,15 +1489,15 @@ __global__ __launch_bounds__(256) void sst_vregion_runs_kernel(SstArgs a, VViewA
         uint64_t src[16];
         uint32_t fixb = 0, inr = 0;  // bit b: byte b from a descriptor / inside [A, B)
         uint32_t pre[4] = {0, 0, 0, 0};
-        uint32_t q = run_of(r0 > 0 ? (uint32_t)r0 : 0);
+        uint32_t q = run_of(r0 > 0 ? (uint64_t)r0 : 0);
 #pragma unroll
         for (uint32_t b = 0; b < 16; b++) {
             const int64_t r = r0 + b;
             src[b] = s_in[w][q];  // harmless when unused
             if (r < 0 || r >= (int64_t)tot) continue;
             inr |= 1u << b;
-            while ((uint32_t)r >= s_d[w][q + 1]) q++;
-            const uint32_t t = (uint32_t)r - s_d[w][q];
+            while ((uint64_t)r >= s_d[w][q + 1]) q++;
+            const uint64_t t = (uint64_t)r - s_d[w][q];
             const uint32_t fx = s_fix[w][q];
             src[b] = s_in[w][q] + t;
             if (fx && t < 4) {
