@@ -611,14 +611,27 @@ __global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
 __global__ __launch_bounds__(kMergeThreads) void merge_emit_kernel(
     const uint32_t *perm, const SumPair *sc, const uint32_t *csize, const MergeFile *files,
     const uint64_t *counts, uint32_t n, uint32_t *out, uint64_t *file_start) {
-    const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
+    __shared__ uint32_t s_lo;
+    const uint32_t j0 = blockIdx.x * kMergeThreads, j = j0 + threadIdx.x;
     const uint32_t nf = (uint32_t)counts[1];
     if (j <= nf && file_start) file_start[j] = files[j].o;
+    // the file of the workgroup's first position: one search per workgroup;
+    // a position's file is then at most a few files further (a file spans
+    // about threshold / pair size positions), else searched again
+    auto last_le = [&](uint32_t lo, uint32_t hi, uint32_t x) {  // last file in [lo, hi) with p <= x
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (files[mid].p <= x) lo = mid; else hi = mid;
+        }
+        return lo;
+    };
+    if (threadIdx.x == 0) s_lo = nf ? last_le(0, nf, j0) : 0;
+    __syncthreads();
     if (j >= n || !csize[j]) return;
-    uint32_t lo = 0, hi = nf;  // last file with p <= j
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (files[mid].p <= j) lo = mid; else hi = mid;
+    uint32_t lo = s_lo;
+    for (uint32_t step = 0; lo + 1 < nf && files[lo + 1].p <= j; step++) {
+        if (step == 4) { lo = last_le(lo, nf, j); break; }
+        lo++;
     }
     if (nf == 0 || files[lo].p > j || j >= files[lo + 1].p) return;  // past the last file
     const MergeFile F = files[lo];
