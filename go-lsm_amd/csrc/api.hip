@@ -6,6 +6,11 @@
 
 extern "C" int lsm_abi_version(void) { return LSM_ABI_VERSION; }
 extern "C" int lsm_input_slack(void) { return LSM_INPUT_SLACK; }
+#ifndef LSM_BUILD_ID
+#define LSM_BUILD_ID "unknown"
+#endif
+// hash of the sources this library was compiled from (go-lsm_amd/build_id.py)
+extern "C" const char *lsm_build_id(void) { return LSM_BUILD_ID; }
 
 extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
     if (!out) return LSM_EINVAL;

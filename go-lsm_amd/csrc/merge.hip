@@ -1163,8 +1163,15 @@ extern "C" int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec
                              const lsm_rec_desc *d_val_desc, uint64_t n, int level,
                              uint64_t threshold, uint32_t *d_out, uint64_t *d_file_start,
                              uint64_t *h_counts, void *d_ws, size_t ws_bytes, void *stream) {
-    return lsm_merge_kvs_tie(ctx, d_bytes, d_key_desc, d_val_desc, n, level, threshold,
-                             LSM_TIE_INPUT, d_out, d_file_start, h_counts, d_ws, ws_bytes, stream);
+    // the v2 / v3 contract: exactly two counts, {nout, nfiles}; only
+    // lsm_merge_kvs_tie reports the third (the most pairs in one file)
+    if (!h_counts) return LSM_EINVAL;
+    uint64_t c3[3] = {0, 0, 0};
+    const int rc = lsm_merge_kvs_tie(ctx, d_bytes, d_key_desc, d_val_desc, n, level, threshold,
+                                     LSM_TIE_INPUT, d_out, d_file_start, c3, d_ws, ws_bytes, stream);
+    h_counts[0] = c3[0];
+    h_counts[1] = c3[1];
+    return rc;
 }
 
 extern "C" size_t lsm_gather_kvs_workspace_bytes(uint64_t nout) {

@@ -915,7 +915,7 @@ std::vector<SSTable> CompactAndMergeKVs(const std::vector<kv::KeyValuePair> &kvs
     d.H2D(d_buf, h, pad16(total));
     d.H2D(d_kd, kd.data(), n * sizeof(lsm_rec_desc));
     d.H2D(d_vd, vd.data(), n * sizeof(lsm_rec_desc));
-    uint64_t counts[3] = {0, 0, 0};
+    uint64_t counts[2] = {0, 0};
     check(lsm_merge_kvs(d.ctx(), (const uint8_t *)d_buf, (const lsm_rec_desc *)d_kd,
                         (const lsm_rec_desc *)d_vd, n, level, kMaxSSTableSize, (uint32_t *)d_out,
                         (uint64_t *)d_fs, counts, d_ws, ws, d.stream()),

@@ -35,6 +35,7 @@ class DecodeOut(ctypes.Structure):
 SIGNATURES = {
     "lsm_abi_version": (ctypes.c_int, []),
     "lsm_input_slack": (ctypes.c_int, []),
+    "lsm_build_id": (ctypes.c_char_p, []),
     "lsm_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "lsm_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "lsm_ctx_num_cus": (ctypes.c_int, [ctypes.c_void_p]),
@@ -165,6 +166,19 @@ def load():
         raise RuntimeError(
             f"{LIB_PATH}: ABI {lib.lsm_abi_version()} / input slack {lib.lsm_input_slack()}, "
             f"this binding expects ABI {ABI_VERSION} / slack {INPUT_SLACK}: rebuild")
+    # the library must be built from the sources beside it (build_id.py): a
+    # stale prebuilt liblsm_gpu.so never stands in for the current tree
+    pkg = os.path.dirname(_PKG_DIR)
+    if os.path.isdir(os.path.join(pkg, "csrc")):
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("_lsm_build_id", os.path.join(pkg, "build_id.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        want, have = mod.source_id(pkg), lib.lsm_build_id().decode()
+        if want != have:
+            raise RuntimeError(
+                f"{LIB_PATH} was built from other sources (build id {have}, the tree's "
+                f"sources hash to {want}): rebuild with `make -C go-lsm_amd`")
     _lib = lib
     return lib
 

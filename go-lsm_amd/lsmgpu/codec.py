@@ -53,12 +53,24 @@ def pad16(n: int) -> int:
     return ((n + 15) // 16) * 16 + INPUT_SLACK
 
 
+def _writable(a: np.ndarray) -> np.ndarray:
+    """A contiguous array torch.from_numpy may wrap: read-only inputs (e.g.
+    np.frombuffer over bytes) are copied first, since torch cannot mark the
+    tensor read-only and warns of undefined behaviour."""
+    a = np.ascontiguousarray(a)
+    return a if a.flags.writeable else a.copy()
+
+
+def _dev_i64(a: np.ndarray, dev) -> torch.Tensor:
+    return torch.from_numpy(_writable(a).view(np.int64)).to(dev)
+
+
 def to_device_bytes(buf: np.ndarray, device) -> torch.Tensor:
     """Copy a host byte array into a 16-byte padded device buffer."""
     n = int(buf.nbytes)
     t = torch.zeros(pad16(n), dtype=torch.uint8, device=device)
     if n:
-        t[:n].copy_(torch.from_numpy(np.ascontiguousarray(buf).view(np.uint8).reshape(-1)))
+        t[:n].copy_(torch.from_numpy(_writable(buf).view(np.uint8).reshape(-1)))
     return t
 
 
@@ -389,8 +401,8 @@ def alloc_sst_decode(ctx: Context, file_off: np.ndarray, file_len: np.ndarray,
         idx_value=torch.zeros(cap, dtype=torch.int64, device=dev),
         data_desc=torch.zeros((cap, 4), dtype=torch.int32, device=dev),
         workspace=torch.empty(max(ws, 16), dtype=torch.uint8, device=dev),
-        d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
-        d_file_len=torch.from_numpy(file_len.view(np.int64)).to(dev),
+        d_file_off=_dev_i64(file_off, dev),
+        d_file_len=_dev_i64(file_len, dev),
         file_off=file_off, nfile=nf)
 
 
@@ -459,9 +471,9 @@ def batch_to_device(ctx: Context, keys: np.ndarray, koff: np.ndarray, vals: np.n
     voff = np.ascontiguousarray(voff, dtype=np.uint64)
     return RecordBatch(
         keys=to_device_bytes(keys, dev),
-        koff=torch.from_numpy(koff.view(np.int64)).to(dev),
+        koff=_dev_i64(koff, dev),
         vals=to_device_bytes(vals, dev),
-        voff=torch.from_numpy(voff.view(np.int64)).to(dev),
+        voff=_dev_i64(voff, dev),
         n=len(koff) - 1, koff_host=koff, voff_host=voff)
 
 
@@ -493,8 +505,8 @@ def encode_blocks(ctx: Context, grammar: int, batch: RecordBatch, rec_start: np.
     if out_bytes is None:
         out_bytes = int((out_off + sizes).max()) if nblk else 0
     d_out = torch.zeros(pad16(out_bytes), dtype=torch.uint8, device=dev)
-    d_rs = torch.from_numpy(rec_start.view(np.int64)).to(dev)
-    d_oo = torch.from_numpy(out_off.view(np.int64)).to(dev)
+    d_rs = _dev_i64(rec_start, dev)
+    d_oo = _dev_i64(out_off, dev)
     d_io = None
     if grammar == GRAMMAR_IDX:
         d_io = torch.from_numpy(np.ascontiguousarray(idx_off, dtype=np.int64)).to(dev)
@@ -575,8 +587,8 @@ def prepare_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
         file_start=file_start, file_off=file_off, file_size=sizes,
         footer=torch.zeros(max(nf, 1) * 4, dtype=torch.int64, device=dev),
         workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
-        d_file_start=torch.from_numpy(file_start.view(np.int64)).to(dev),
-        d_file_off=torch.from_numpy(file_off.view(np.int64)).to(dev),
+        d_file_start=_dev_i64(file_start, dev),
+        d_file_off=_dev_i64(file_off, dev),
         max_recs=max_recs, m=m, k=k, nfile=nf)
 
 

@@ -32,7 +32,8 @@ extern "C" {
 
 /* v3: the input slack grew from 16 to 32 bytes (a binding built for v2 pads
  * too little); lsm_input_slack() reports it at run time.
- * v4: lsm_merge_kvs / lsm_merge_kvs_tie write 3 h_counts entries (was 2). */
+ * v4: lsm_merge_kvs_tie writes 3 h_counts entries; lsm_merge_kvs keeps the
+ * v2 / v3 contract of exactly 2 ({nout, nfiles}). */
 #define LSM_ABI_VERSION 4
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
@@ -107,6 +108,10 @@ typedef struct lsm_ctx lsm_ctx;
 int lsm_abi_version(void);
 /* LSM_INPUT_SLACK of the loaded library: a binding checks it at load time. */
 int lsm_input_slack(void);
+/* Identity of the sources the library was compiled from (16 hex digits,
+ * go-lsm_amd/build_id.py): a binding shipped beside the sources compares it
+ * and refuses a stale prebuilt library.  Not part of the Go surface. */
+const char *lsm_build_id(void);
 /* One context per goroutine / OS thread (callers are concurrent goroutines,
  * sstable_test.go:379-400); no hidden global mutable state. */
 int lsm_ctx_create(int device, lsm_ctx **out);
@@ -383,16 +388,17 @@ int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff, uint
  *
  * Outputs: d_out[0 .. nout) = input indices of the written pairs, in order;
  * d_file_start[0 .. nfiles] = each file's first position in d_out (optional,
- * n + 1 entries), d_file_start[nfiles] = nout; h_counts (host, 3 entries) =
- * {nout, nfiles, the most pairs in one file} (the last sizes lsm_build_sst's
- * max_file_records with no second read-back; ABI 4, was 2 entries).
+ * n + 1 entries), d_file_start[nfiles] = nout; lsm_merge_kvs_tie's h_counts
+ * (host, 3 entries) = {nout, nfiles, the most pairs in one file} (the last
+ * sizes lsm_build_sst's max_file_records with no second read-back; ABI 4).
  * Synchronizes the stream (the radix passes are chosen from key statistics). */
 size_t lsm_merge_kvs_workspace_bytes(uint64_t n);
 enum lsm_tie {
     LSM_TIE_INPUT = 0,   /* equal keys in input order (merge.go:41's contract)              */
     LSM_TIE_GOHEAP = 1,  /* equal keys in container/heap's pop order (merge.go:47-66, exact) */
 };
-/* lsm_merge_kvs = lsm_merge_kvs_tie(..., LSM_TIE_INPUT, ...).  Same workspace. */
+/* lsm_merge_kvs = lsm_merge_kvs_tie(..., LSM_TIE_INPUT, ...) with h_counts
+ * holding 2 entries, {nout, nfiles} (unchanged since v2).  Same workspace. */
 int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
                       const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
                       int tie, uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts,

@@ -94,3 +94,35 @@ def test_code_object_is_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
     for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
         assert other not in blob
+
+
+def test_build_id_ties_library_to_sources(tmp_path):
+    """liblsm_gpu.so carries the hash of the sources it was built from
+    (go-lsm_amd/build_id.py); load() refuses a library whose id differs from
+    the tree's, so a stale prebuilt .so cannot stand in for the sources."""
+    import importlib.util
+    import shutil
+    pkg = os.path.join(ROOT, "go-lsm_amd")
+    spec = importlib.util.spec_from_file_location("bid", os.path.join(pkg, "build_id.py"))
+    bid = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bid)
+    assert _lib.load().lsm_build_id().decode() == bid.source_id(pkg)
+    # a copy of the tree with one source byte changed: the same library is refused
+    alt = tmp_path / "go-lsm_amd"
+    shutil.copytree(os.path.join(pkg, "csrc"), alt / "csrc")
+    shutil.copy(os.path.join(pkg, "Makefile"), alt / "Makefile")
+    shutil.copy(os.path.join(pkg, "build_id.py"), alt / "build_id.py")
+    os.makedirs(tmp_path / "include")
+    shutil.copy(HEADER, tmp_path / "include" / "lsm_gpu.h")
+    assert bid.source_id(str(alt)) == bid.source_id(pkg)
+    with open(alt / "csrc" / "common.h", "a") as f:
+        f.write("\n// changed\n")
+    assert bid.source_id(str(alt)) != bid.source_id(pkg)
+    os.makedirs(alt / "lsmgpu")
+    shutil.copy(os.path.join(pkg, "lsmgpu", "_lib.py"), alt / "lsmgpu" / "_lib.py")
+    shutil.copy(os.path.join(pkg, "liblsm_gpu.so"), alt / "liblsm_gpu.so")
+    spec = importlib.util.spec_from_file_location("alt_lib", str(alt / "lsmgpu" / "_lib.py"))
+    alt_lib = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(alt_lib)
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        alt_lib.load()
