@@ -278,8 +278,7 @@ def bench_decode(args, world, rank, local):
     times, kern_ms = kernel_times(step, stream, args.steps)
     # the timed output is checked after the timed region: the line fails on a
     # single wrong descriptor (kv/kv.go:77-115 record chain, closed form)
-    if args.placement == "offset":
-        verify_decode(args, r, d_off, d_len, nblk)
+    verify_decode(args, r, d_off, d_len, nblk)
 
     parsed = float(blk_len.astype(np.float64).sum())
     cold = (cold_input_pass(args, ctx, buf, d_off, d_len, nblk, hint, stream, parsed)
@@ -463,7 +462,11 @@ def verify_decode(args, r, d_off, d_len, nblk):
     assert int((r.status[:nblk] != 0).sum()) == 0, "decode reported errors"
     off = d_off.to(torch.int64)
     ln = d_len.to(torch.int64) & 0xFFFFFFFF
-    base = off // lsmgpu.codec.MIN_RECORD[lsmgpu.GRAMMAR_KV]
+    # each block's first record slot: the dense plan's rec_base (--placement
+    # plan), else offset addressing
+    base = (r.rec_base[:nblk].to(torch.int64) if r.rec_base is not None
+            else off // lsmgpu.codec.MIN_RECORD[lsmgpu.GRAMMAR_KV])
+    abase = (r.arena_base[:nblk].to(torch.int64) if r.arena_base is not None else off)
     chunk = 1 << 16
     for b0 in range(0, nblk, chunk):
         b1 = min(nblk, b0 + chunk)
@@ -490,16 +493,19 @@ def verify_decode(args, r, d_off, d_len, nblk):
             recs = UNIFORM[args.config]["recs"]
             assert bool((n == recs).all()), "decode: nrec"
             if getattr(args, "arena", False) and r.key_arena is not None:
-                # ARENA: block b's keys / values packed at blk_off[b], equal to
-                # the record fields of the input (kv.go:88-111 make + ReadFull)
+                # ARENA: block b's keys / values packed at its arena base
+                # (blk_off[b], or the plan's arena_base), equal to the record
+                # fields of the input (kv.go:88-111 make + ReadFull)
                 slot = UNIFORM[args.config]["slot"]
-                rows = r.key_arena[: nblk * slot].view(nblk, slot)[b0:b1]
+                ka = abase[b0:b1].unsqueeze(1) + torch.arange(recs * 16, device=dev)
+                rows = r.key_arena[ka]
                 recs_in = args._d_in[: nblk * slot].view(nblk, slot)[b0:b1, : recs * 124]
                 recs_in = recs_in.reshape(b1 - b0, recs, 124)
-                assert torch.equal(rows[:, : recs * 16].reshape(b1 - b0, recs, 16),
+                assert torch.equal(rows.reshape(b1 - b0, recs, 16),
                                    recs_in[:, :, 4:20]), "arena: keys"
-                vrows = r.val_arena[: nblk * slot].view(nblk, slot)[b0:b1]
-                assert torch.equal(vrows[:, : recs * 100].reshape(b1 - b0, recs, 100),
+                va = abase[b0:b1].unsqueeze(1) + torch.arange(recs * 100, device=dev)
+                vrows = r.val_arena[va]
+                assert torch.equal(vrows.reshape(b1 - b0, recs, 100),
                                    recs_in[:, :, 24:124]), "arena: values"
             assert bool(((klen == 16) & (vlen == 100)).all()), "decode: record lengths"
             assert bool((rec_off == off[blk] + 124 * j).all()), "decode: record offsets"

@@ -129,6 +129,7 @@ def bench_compact(args, world, rank, local):
     build_alg = key_b + val_b + 36.0 * mg.nout + float(sb.file_size.astype(np.float64).sum())
     from bench import HBM_PEAK_GBS
     b_ach = build_alg / (stage_ms["build"] * 1e-3) / 1e9
+    chain_alg = in_bytes + float(sb.file_size.astype(np.float64).sum())
     out = {
         "metric": "GiB/s of input .sst bytes compacted (decode + merge + rebuild)",
         "value": round(total * steps / elapsed / GIB, 3),
@@ -143,12 +144,24 @@ def bench_compact(args, world, rank, local):
                    "input_bytes_per_gpu": int(in_bytes),
                    "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
                    "parallelism": f"dp{world} (one compaction per rank, no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "build stage: lsm_sst_layout + "
-                                               "lsm_build_sst_views (events around the stage)",
-                     "achieved": round(b_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(b_ach / HBM_PEAK_GBS, 4), "traffic": None,
-                     "alg_bytes_per_launch": int(build_alg),
-                     "kernel_ms": round(stage_ms["build"], 5)},
+        # the whole chain: an ideal compaction reads every input image byte
+        # once and writes every output image byte once; everything between
+        # (descriptors, the permutation, packed keys) is this implementation's
+        # own traffic and counts against it
+        "roofline": {"bound": "hbm",
+                     "kernel": "whole compaction per step (decode + join + merge + gather + "
+                               "build), wall time of the timed region",
+                     "achieved": round(chain_alg / (elapsed / steps) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(chain_alg / (elapsed / steps) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "alg_bytes_per_launch": int(chain_alg),
+                     "alg_bytes_def": "input image bytes read once + output image bytes written once",
+                     "kernel_ms": round(elapsed * 1e3 / steps, 5),
+                     "build_stage": {"kernel": "lsm_sst_layout + lsm_build_sst_views (events)",
+                                     "alg_bytes": int(build_alg), "ms": round(stage_ms["build"], 5),
+                                     "achieved": round(b_ach, 1),
+                                     "frac": round(b_ach / HBM_PEAK_GBS, 4)}},
     }
     return out, (img.cpu().numpy(), file_off, file_size)
 

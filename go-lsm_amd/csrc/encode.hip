@@ -863,6 +863,7 @@ constexpr uint32_t kOrSlices = 2;  // bloom_or_kernel workgroups per filter
 constexpr uint32_t kSplitMaxK = 16;  // three carries per class fit the record
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // The 24-byte hash record of a key from its sum256 digest: the residues mod m
 // of the four location classes and of the two class steps, carry bits of the
@@ -1559,11 +1560,94 @@ __device__ void sst_meta_body(const SstArgs &a, uint32_t f) {
 
 __global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body(a, blockIdx.x); }
 
+// ORs one key's k locations (its hash record, store_hash_rec) into the LDS
+// slice.  The ORs are bound by VALU issue, not by the LDS (PMC,
+// profiles/r04_pmc_sst_lds.txt: LDS array busy 21 % of the kernel, 256 VALU
+// per key in the round-3 form), so per location the work is three VALU to
+// place the bit and three to step the class's residue, and nothing else:
+//  * no slice test: the word's LDS address ((p >> 5) << 2) - lo / 8 of a
+//    location outside the slice lies outside the workgroup's LDS allocation
+//    (above it, or wrapped below zero), and the LDS drops out-of-range
+//    accesses (tools/lds_or_probe.py modes 7, 8, 10: bitmaps identical to
+//    the exec-masked form) -- no compare, no exec-mask branch per location;
+//  * the class steps are chosen once per key (a step whose 64-bit add wraps
+//    loses 2^64: its residue less 2^64 mod m), by bitfield insert.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <uint32_t K>
+__device__ __forceinline__ void or_key_locations(const u32x4 x, const u32x2 y, uint32_t k, uint32_t m,
+                                                 uint32_t c64, uint32_t base) {
+    const uint32_t raw[6] = {x.x, x.y, x.z, x.w, y.x, y.y};
+    uint32_t r[4];
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) r[c] = raw[c] & 0x3FFFFFFFu;
+    const uint32_t d2 = raw[4] & 0x3FFFFFFFu, d3 = raw[5] & 0x3FFFFFFFu;
+    const uint32_t t2 = d2 - c64, t3 = d3 - c64;
+    const uint32_t w2 = min(t2, t2 + m), w3 = min(t3, t3 + m);
+    uint32_t st[4][3];
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {
+        const bool a2 = c == 0 || c == 3;
+#pragma unroll
+        for (uint32_t n = 0; n < 3; n++) {
+            // all-ones where the step from location 4n + c carries (carry bit
+            // 3c + n = bit 30 + b of dword q), then one bitfield insert (the
+            // compiler's and / compare / cndmask form is three VALU)
+            const uint32_t bit = 3 * c + n, q = bit >> 1, b = bit & 1;
+            const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)raw[q], 30 + b, 1);
+            uint32_t v;
+            __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(v) : "v"(msk), "v"(a2 ? w2 : w3), "v"(a2 ? d2 : d3));
+            st[c][n] = v;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t c = j & 3, n = j >> 2;  // compile-time: r[] stays in registers
+        if (K == 0 && j >= k) break;           // wave-uniform
+        if (K != 0 && j >= K) break;
+        const uint32_t p = r[c];
+        // LDS byte address of the bit's word, out of range outside the slice
+        // (shift + shift-add: the compiler's shift / and / add form is three)
+        uint32_t a;
+        __asm__("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(p >> 5), "v"(base));
+        __hip_atomic_fetch_or((lds_u32 *)(size_t)a, 1u << (p & 31), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (n < 3) {
+            const uint32_t t = p + st[c][n];
+            r[c] = min(t, t - m);
+        }
+    }
+}
+
 // Filter blockIdx.x, slice blockIdx.y: every key's k locations rebuilt from
 // its record, the slice's bits ORed in LDS, then stored big-endian into the
-// image; the first slice's workgroup also writes the file's framing.  (One workgroup per filter holding 152 KiB and listing the rest was
-// measured slower: the ORs are bound by LDS atomic throughput, about 1.4
-// lanes per clock per CU for scattered words, not by the rebuild.)
+// image; the first slice's workgroup also writes the file's framing.
+template <uint32_t K>
+__device__ __forceinline__ void bloom_or_body(const BloomOrArgs &a, uint64_t s, uint64_t e,
+                                              uint32_t base) {
+    const uint32_t m = a.m, c64 = a.c64;
+    const uint64_t k0 = uni64(a.file_start[0]);
+    // the file's records through one buffer resource: the record offset is
+    // a 32-bit register stepping by 24 KiB per round, and the loads two
+    // rounds ahead past the last key return zeros (never used)
+    const rsrc_t rs = make_rsrc(a.rec + kHashRecDwords * (s - k0), (uint32_t)(24 * (e - s)));
+    uint32_t vo = 24 * threadIdx.x;
+    constexpr uint32_t kStep = 24 * 1024;
+    u32x4 xa = ld_b128(rs, vo), xb = ld_b128(rs, vo + kStep);
+    u32x2 ya = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + 16, 0, 0);
+    u32x2 yb = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + kStep + 16, 0, 0);
+    for (uint64_t i = s + threadIdx.x; i < e; i += 1024) {
+        const u32x4 x = xa;
+        const u32x2 y = ya;
+        xa = xb;
+        ya = yb;
+        vo += kStep;
+        xb = ld_b128(rs, vo + kStep);
+        yb = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + kStep + 16, 0, 0);
+        or_key_locations<K>(x, y, a.k, m, c64, base);
+    }
+}
+
 __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs sa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
     const uint32_t f = blockIdx.x, sl = blockIdx.y;
@@ -1574,52 +1658,11 @@ __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs s
     for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_bits[i] = 0;
     __syncthreads();
     const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
-    const uint32_t m = a.m, c64 = a.c64;
-    const uint64_t k0 = uni64(a.file_start[0]);
-    // records two rounds ahead in flight (indices past the filter clamped;
-    // a filter without keys loads nothing and stores its zero words)
-    const gptr_t<const uint32_t> rec = gbl(a.rec);
-    auto ld = [&](uint64_t i, u32x4 &x, u32x2 &y) {
-        const uint64_t j = (i < e ? i : e - 1) - k0;
-        x = *(gptr_t<const u32x4>)(rec + kHashRecDwords * j);
-        y = *(gptr_t<const u32x2>)(rec + kHashRecDwords * j + 4);
-    };
-    u32x4 xa, xb;
-    u32x2 ya, yb;
-    if (e > s) {
-        ld(s + threadIdx.x, xa, ya);
-        ld(s + threadIdx.x + blockDim.x, xb, yb);
-    }
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const u32x4 x = xa;
-        const u32x2 y = ya;
-        xa = xb;
-        ya = yb;
-        ld(i + 2 * blockDim.x, xb, yb);
-        const uint32_t raw[6] = {x.x, x.y, x.z, x.w, y.x, y.y};
-        uint32_t cy = 0, r[4];
-#pragma unroll
-        for (uint32_t d = 0; d < 6; d++) cy |= (raw[d] >> 30) << (2 * d);
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++) r[c] = raw[c] & 0x3FFFFFFFu;
-        const uint32_t d2 = raw[4] & 0x3FFFFFFFu, d3 = raw[5] & 0x3FFFFFFFu;
-        // a step whose 64-bit add wraps loses 2^64: its residue less 2^64 mod m
-        const uint32_t w2 = d2 >= c64 ? d2 - c64 : d2 + m - c64;
-        const uint32_t w3 = d3 >= c64 ? d3 - c64 : d3 + m - c64;
-#pragma unroll
-        for (uint32_t j = 0; j < kSplitMaxK; j++) {
-            const uint32_t c = j & 3, n = j >> 2;  // compile-time: r[] stays in registers
-            if (j >= a.k) continue;                 // wave-uniform
-            const uint32_t p = r[c];
-            if (p >= lo && p < hi) atomicOr(&lds_bits[(p - lo) >> 5], 1u << ((p - lo) & 31));
-            if (n < 3) {
-                const bool a2 = c == 0 || c == 3;
-                const bool carry = (cy >> (3 * c + n)) & 1;
-                const uint32_t t = p + (carry ? (a2 ? w2 : w3) : (a2 ? d2 : d3));
-                r[c] = min(t, t - m);
-            }
-        }
-    }
+    // lo is a multiple of 64: the slice's bit p sits in LDS word (p - lo) >> 5,
+    // bit p & 31; base = -lo / 8 bytes, plus the array's own LDS address
+    const uint32_t base = (uint32_t)(size_t)(lds_u32 *)lds_bits - lo / 8;
+    if (a.k == kSplitMaxK) bloom_or_body<kSplitMaxK>(a, s, e, base);
+    else bloom_or_body<0>(a, s, e, base);
     __syncthreads();
     const uint64_t hdr = sst_header_bytes(a.koff, s, e);
     store_filter_slice(WgGroup{}, lds_bits, lo / 64, hi == a.m ? a.nwords : (uint64_t)(hi + 63) / 64,
@@ -2225,6 +2268,364 @@ McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) 
     return w;
 }
 
+// ---- batched level search: Manager.searchFromLevelWithSparseIndex ---------
+//
+// For a level >= 1 (sstable/manager.go:178-207): sort.Search over the
+// level's tables in sparse-index order (sorted by MinKey, :290-303) for the
+// first whose MinKey > key, index-- when > 0, then searchFromTable's
+// SSTable.MayContain (:209-212, sstable.go:300-305) of that one table.  Per
+// probe the answer is 5 bytes (candidate table, may bit) instead of a row of
+// the nkeys x nfile matrix lsm_may_contain writes.
+//
+//  lv_classify_kernel: each workgroup takes 2,048 probes: Go's sort.Search
+//    (h = (i + j) >> 1) over the tables' 16-byte MinKey prefixes in LDS (the
+//    full keys only on a prefix tie), the candidate stored coalesced; a probe
+//    the range check rejects gets its 0 here; the others are hashed once
+//    (sum256) and counting-sorted by table in LDS into the workgroup's slots,
+//    and the workgroup's (start, count) per table goes to a table-major grid.
+//  lv_test_kernel: one workgroup per table: its row of the grid (scanned in
+//    LDS) locates its probes in every classify workgroup's slots, the
+//    filter's first 144 KiB are staged in LDS (the tail read through L2) and
+//    each probe's k bits tested there.
+// Tables beyond kLvMaxFiles take lv_probe_kernel (search over the table
+// list in global memory, bits read from the image).
+constexpr uint32_t kLvThreads = 1024;
+constexpr uint32_t kLvPer = 2;  // probes per thread
+constexpr uint32_t kLvProbes = kLvThreads * kLvPer;
+constexpr uint32_t kLvMaxFiles = 2048;
+constexpr uint32_t kLvMaxWgs = 1024;  // classify workgroups per pass (2M probes)
+
+struct LvWs {
+    McFile *files;
+    uint32_t *grid;   // [nfile][nwg]: the table's first slot in the workgroup
+    uint32_t *cnt;    // [nfile][nwg]: the table's probes in the workgroup
+    uint32_t *ids;    // [nwg * 2048] probe of each slot
+    uint64_t *hash;   // [nwg * 2048 * 4] its sum256
+};
+
+LvWs lv_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
+    LvWs w{};
+    size_t at = 0;
+    auto take = [&](size_t bytes) -> uint8_t * {
+        uint8_t *p = base ? base + at : nullptr;
+        at += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    const uint64_t pass = nkeys < (uint64_t)kLvMaxWgs * kLvProbes ? nkeys : (uint64_t)kLvMaxWgs * kLvProbes;
+    const uint64_t nwg = (pass + kLvProbes - 1) / kLvProbes;
+    const size_t nf = nfile ? nfile : 1;
+    w.files = reinterpret_cast<McFile *>(take(sizeof(McFile) * nf));
+    w.grid = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
+    w.cnt = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
+    w.ids = reinterpret_cast<uint32_t *>(take(4 * (nwg ? nwg : 1) * kLvProbes));
+    w.hash = reinterpret_cast<uint64_t *>(take(32 * (nwg ? nwg : 1) * kLvProbes));
+    if (total) *total = at;
+    return w;
+}
+
+// The search view of table f: MinKey / MaxKey prefixes whenever the header
+// decoded (stage != 1); a table whose header did not decode searches as the
+// zero Header (MinKey "", what the oracle restates).  ok: header and filter
+// decoded (MayContain is answered only then).
+__device__ __forceinline__ McFile lv_file(const uint8_t *img, const uint64_t *file_off,
+                                          const lsm_sst_meta &M, uint32_t f) {
+    McFile F = mc_file(img, file_off, M, f);
+    if (M.stage == 2) {  // header decoded, filter not: search by its MinKey
+        const uint8_t *base = img + file_off[f];
+        for (uint32_t j = 0; j < 4; j++) {
+            F.lo[j] = be_word_at(base + M.min_key_off, M.min_key_len, j);
+            F.hi[j] = be_word_at(base + M.max_key_off, M.max_key_len, j);
+        }
+    } else if (M.stage == 1) {
+        F.lo_len = F.hi_len = 0;
+    }
+    return F;
+}
+
+__global__ __launch_bounds__(256) void lv_prep_kernel(const uint8_t *img, const uint64_t *file_off,
+                                                      const lsm_sst_meta *meta, uint32_t nfile,
+                                                      LvWs w) {
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f < nfile) w.files[f] = lv_file(img, file_off, meta[f], f);
+}
+
+// sort.Search(n, MinKey_h > key) exactly as Go's sort.go runs it.
+template <typename LoAt>
+__device__ __forceinline__ uint32_t lv_search(uint32_t nfile, LoAt lo_prefix, const McFile *files,
+                                              const uint8_t *img, const uint32_t kw[4], uint64_t kl,
+                                              const uint8_t *kp) {
+    uint32_t i = 0, j = nfile;
+    while (i < j) {
+        const uint32_t h = (uint32_t)(((uint64_t)i + j) >> 1);
+        uint32_t bw[4];
+        lo_prefix(h, bw);
+        int c = prefix_cmp(bw, kw);
+        if (c == 0) {
+            const McFile &F = files[h];
+            c = bound_cmp(bw, F.lo_len, img + F.lo_at, kw, kl, kp);
+        }
+        if (c <= 0) i = h + 1;  // !f(h)
+        else j = h;
+    }
+    return i;
+}
+
+__global__ __launch_bounds__(kLvThreads) void lv_classify_kernel(const uint8_t *img, uint32_t nfile,
+                                                                 const uint8_t *keys, const uint64_t *koff,
+                                                                 uint64_t k_begin, uint64_t nkeys, LvWs w,
+                                                                 uint32_t nwg, int32_t *table,
+                                                                 uint8_t *may) {
+    __shared__ uint4 slo[kLvMaxFiles];
+    __shared__ uint32_t lh[kLvMaxFiles];
+    __shared__ uint32_t part[kLvThreads];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t f = t; f < nfile; f += kLvThreads) {
+        const McFile &F = w.files[f];
+        slo[f] = make_uint4(F.lo[0], F.lo[1], F.lo[2], F.lo[3]);
+        lh[f] = 0;
+    }
+    uint64_t k0[kLvPer], kl[kLvPer], f0[kLvPer], f1[kLvPer];
+#pragma unroll
+    for (uint32_t p = 0; p < kLvPer; p++) {
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kLvProbes + p * kLvThreads + t;
+        k0[p] = i < nkeys ? koff[i] : 0;
+        kl[p] = i < nkeys ? koff[i + 1] - k0[p] : 0;
+    }
+#pragma unroll
+    for (uint32_t p = 0; p < kLvPer; p++) {
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kLvProbes + p * kLvThreads + t;
+        f0[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p]) : 0;
+        f1[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p] + 8) : 0;
+    }
+    uint32_t kw[kLvPer][4];
+#pragma unroll
+    for (uint32_t p = 0; p < kLvPer; p++) {
+        const uint64_t l = kl[p];
+        if (l < 8) { f0[p] &= l ? (~0ull >> (64 - 8 * l)) : 0; f1[p] = 0; }
+        else if (l < 16) f1[p] &= l > 8 ? (~0ull >> (128 - 8 * l)) : 0;
+        kw[p][0] = __builtin_bswap32((uint32_t)f0[p]);
+        kw[p][1] = __builtin_bswap32((uint32_t)(f0[p] >> 32));
+        kw[p][2] = __builtin_bswap32((uint32_t)f1[p]);
+        kw[p][3] = __builtin_bswap32((uint32_t)(f1[p] >> 32));
+    }
+    __syncthreads();
+    auto lo_lds = [&](uint32_t h, uint32_t bw[4]) {
+        const uint4 v = slo[h];
+        bw[0] = v.x; bw[1] = v.y; bw[2] = v.z; bw[3] = v.w;
+    };
+    uint32_t cand[kLvPer], rank[kLvPer];
+    uint64_t hh[kLvPer][4];
+#pragma unroll
+    for (uint32_t p = 0; p < kLvPer; p++) {
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kLvProbes + p * kLvThreads + t;
+        cand[p] = kMcNone;
+        if (i >= nkeys) continue;
+        const uint8_t *kp = keys + k0[p];
+        const uint32_t lo = lv_search(nfile, lo_lds, w.files, img, kw[p], kl[p], kp);
+        const uint32_t idx = lo ? lo - 1 : 0;  // manager.go:189-191
+        table[i] = (int32_t)idx;
+        // MayContain (sstable.go:301): lo > 0 means f(lo - 1) was evaluated
+        // false, i.e. MinKey <= key; then MaxKey >= key and a decoded filter
+        bool test = false;
+        if (lo > 0) {
+            const McFile &F = w.files[idx];
+            if (F.ok) {
+                int r = prefix_cmp(F.hi, kw[p]);
+                if (r == 0) r = bound_cmp(F.hi, F.hi_len, img + F.hi_at, kw[p], kl[p], kp);
+                test = r >= 0;
+            }
+        }
+        if (!test) {
+            may[i] = 0;
+            continue;
+        }
+        cand[p] = idx;
+        rank[p] = atomicAdd(&lh[idx], 1u);
+        sum256_pre(kp, kl[p], f0[p], f1[p], hh[p]);
+    }
+    __syncthreads();
+    // exclusive scan of the per-table counts (<= 2,048 tables, 2 per thread)
+    const uint32_t c0 = 2 * t < nfile ? lh[2 * t] : 0u, c1 = 2 * t + 1 < nfile ? lh[2 * t + 1] : 0u;
+    part[t] = c0 + c1;
+    __syncthreads();
+    for (uint32_t d = 1; d < kLvThreads; d <<= 1) {
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    const uint32_t ex = part[t] - c0 - c1;
+    __syncthreads();  // every lh read before it is overwritten with offsets
+    if (2 * t < nfile) {
+        lh[2 * t] = ex;
+        w.grid[(uint64_t)(2 * t) * nwg + blockIdx.x] = ex;
+        w.cnt[(uint64_t)(2 * t) * nwg + blockIdx.x] = c0;
+    }
+    if (2 * t + 1 < nfile) {
+        lh[2 * t + 1] = ex + c0;
+        w.grid[(uint64_t)(2 * t + 1) * nwg + blockIdx.x] = ex + c0;
+        w.cnt[(uint64_t)(2 * t + 1) * nwg + blockIdx.x] = c1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t p = 0; p < kLvPer; p++) {
+        if (cand[p] == kMcNone) continue;
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kLvProbes + p * kLvThreads + t;
+        const uint64_t slot = (uint64_t)blockIdx.x * kLvProbes + lh[cand[p]] + rank[p];
+        w.ids[slot] = (uint32_t)(i - k_begin);
+        *(gptr_t<u64x2>)(gbl(w.hash) + 4 * slot) = u64x2{hh[p][0], hh[p][1]};
+        *(gptr_t<u64x2>)(gbl(w.hash) + 4 * slot + 2) = u64x2{hh[p][2], hh[p][3]};
+    }
+}
+
+// The filter words of F: the first `cap` bytes into LDS from the 16-byte
+// boundary below them (aligned 16-byte global->LDS loads, all in flight, the
+// wave chunks rotated per file so the fills of files at equal offsets
+// spread over the channels).  -> bytes staged.
+__device__ __forceinline__ uint64_t stage_filter(const uint8_t *src, uint64_t nbits, uint8_t *lds,
+                                                 uint32_t cap, uint32_t rot_seed, uint32_t &delta) {
+    const uint64_t nb = 8 * (nbits / 64 + ((nbits & 63) != 0));
+    delta = (uint32_t)((uintptr_t)src & 15);
+    const uint64_t in_lds = nb < cap - 16 ? nb : cap - 16;
+    const uint4 *src16 = reinterpret_cast<const uint4 *>(src - delta);
+    const uint32_t n16 = (uint32_t)((delta + in_lds + 15) / 16);
+    const uint32_t nwc = (n16 + kWave - 1) / kWave, wave = threadIdx.x / kWave;
+    const uint32_t rot = nwc ? (rot_seed * 37u) % nwc : 0;
+    const uint32_t nwaves = blockDim.x / kWave;
+    for (uint32_t cl = wave; cl < nwc; cl += nwaves) {
+        const uint32_t c = cl + rot < nwc ? cl + rot : cl + rot - nwc;
+        const uint32_t xw = c * kWave, x = xw + (threadIdx.x & (kWave - 1));
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)(src16 + (x < n16 ? x : n16 - 1)),
+            (__attribute__((address_space(3))) void *)(lds + 16 * xw), 16, 0, 0);
+    }
+    return n16 ? in_lds : 0;
+}
+
+// Filter.Test (bloom.go:371-379) of one probe against F, the bytes below
+// in_lds from LDS (lb), the rest from the image through L2.
+__device__ __forceinline__ uint32_t filter_test(const McFile &F, const uint64_t h[4], const uint8_t *lb,
+                                                uint64_t in_lds, const uint8_t *src) {
+    // k == 0: true; m == 0 < k: Go panics, answered false
+    uint32_t r = F.k == 0 || F.m != 0;
+    const bool small = F.m <= (1ull << 30);
+    const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
+    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
+        uint32_t bits = 1;
+#pragma unroll
+        for (uint32_t u = 0; u < 16; u++) {
+            const uint32_t j = j0 + u;
+            if (j < F.k) {
+                const uint64_t x = location(h[0], h[1], h[2], h[3], j);
+                const uint64_t p = small ? mod_small(x, m32, rl, rh) : mod_barrett(x, F.m, F.mr);
+                if (p >= F.nbits) {
+                    bits = 0;  // bitset.Test is false past its length
+                } else {
+                    const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+                    const uint32_t byte = q < in_lds ? lb[q] : gbl(src)[q];
+                    bits &= byte >> (p & 7);
+                }
+            }
+        }
+        r = bits & 1;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
+                                                             uint32_t nwg, LvWs w, uint64_t k_begin,
+                                                             uint8_t *may) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
+    __shared__ uint32_t sb[kLvMaxWgs + 1];  // first probe of each workgroup's segment
+    __shared__ uint32_t part[kLvThreads];
+    const uint32_t f = blockIdx.x, t = threadIdx.x;
+    // the table's segments: counts scanned (nwg <= 1,024: one per thread)
+    const uint32_t c = t < nwg ? w.cnt[(uint64_t)f * nwg + t] : 0u;
+    part[t] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < kLvThreads; d <<= 1) {
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    if (t < nwg) sb[t] = part[t] - c;
+    if (t == 0) sb[nwg] = part[kLvThreads - 1];
+    __syncthreads();
+    const uint32_t total = sb[nwg];
+    if (total == 0) return;
+    const McFile F = w.files[f];
+    // the slot of the table's probe q: binary search of its segment
+    auto slot_of = [&](uint32_t q) -> uint64_t {
+        uint32_t a = 0, b = nwg;  // last segment with sb <= q
+        while (b - a > 1) {
+            const uint32_t mid = (a + b) >> 1;
+            if (sb[mid] <= q) a = mid;
+            else b = mid;
+        }
+        return (uint64_t)a * kLvProbes + w.grid[(uint64_t)f * nwg + a] + (q - sb[a]);
+    };
+    uint32_t q = t, id = 0;
+    uint64_t h[4] = {0, 0, 0, 0};
+    if (q < total) {  // the first probe's hash in flight during the fill
+        const uint64_t sl = slot_of(q);
+        id = w.ids[sl];
+        for (int j = 0; j < 4; j++) h[j] = w.hash[4 * sl + j];
+    }
+    const uint8_t *src = img + F.words_at;
+    uint32_t delta;
+    const uint64_t in_lds = stage_filter(src, F.nbits, fbytes, kMcLdsBytes, f, delta);
+    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint8_t *lb = fbytes + delta;
+    while (q < total) {
+        const uint32_t qn = q + kLvThreads;
+        uint32_t idn = 0;
+        uint64_t hn[4] = {0, 0, 0, 0};
+        if (qn < total) {
+            const uint64_t sl = slot_of(qn);
+            idn = w.ids[sl];
+            for (int j = 0; j < 4; j++) hn[j] = w.hash[4 * sl + j];
+        }
+        may[k_begin + id] = (uint8_t)filter_test(F, h, lb, in_lds, src);
+        q = qn;
+        id = idn;
+        for (int j = 0; j < 4; j++) h[j] = hn[j];
+    }
+}
+
+// More tables than the LDS search holds: per probe, the search over the
+// table list in global memory and the bits read from the image.
+__global__ __launch_bounds__(256) void lv_probe_kernel(const uint8_t *img, uint32_t nfile,
+                                                       const uint8_t *keys, const uint64_t *koff,
+                                                       uint64_t nkeys, LvWs w, int32_t *table,
+                                                       uint8_t *may) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nkeys;
+         i += (uint64_t)gridDim.x * 256) {
+        const uint64_t k0 = koff[i], kl = koff[i + 1] - k0;
+        const uint8_t *kp = keys + k0;
+        uint32_t kw[4];
+        for (uint32_t j = 0; j < 4; j++) kw[j] = be_word_at(kp, kl, j);
+        auto lo_g = [&](uint32_t h, uint32_t bw[4]) {
+            for (int j = 0; j < 4; j++) bw[j] = w.files[h].lo[j];
+        };
+        const uint32_t lo = lv_search(nfile, lo_g, w.files, img, kw, kl, kp);
+        const uint32_t idx = lo ? lo - 1 : 0;
+        table[i] = (int32_t)idx;
+        uint8_t r = 0;
+        if (lo > 0 && w.files[idx].ok) {
+            const McFile &F = w.files[idx];
+            if (bound_cmp_fast(F.hi, F.hi_len, img + F.hi_at, kw, kl, kp) >= 0) {
+                uint64_t h[4];
+                sum256(kp, kl, h);
+                const uint8_t *src = img + F.words_at;
+                r = (uint8_t)filter_test(F, h, src, ~0ull, src);
+            }
+        }
+        may[i] = r;
+    }
+}
+
 template <int G>
 int launch_encode_blocks(const EncodeBlocksArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(encode_blocks_kernel<G>, dim3(a.nblk), dim3(kWave * kEncWaves), 0, s, a);
@@ -2332,9 +2733,12 @@ static uint32_t bloom_slices(uint64_t m) {
     return (uint32_t)((m + sb - 1) / sb);
 }
 static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slices(m) <= 2; }
-// two slices and k <= 16: the split build (hash in sst_regions_kernel, bloom_or_kernel)
-static bool split_bloom(uint64_t m, uint32_t k) {
-    return hash_once_bloom(m) && bloom_slices(m) == 2 && k <= kSplitMaxK;
+// two slices and k <= 16: the split build (hash in sst_regions_kernel,
+// bloom_or_kernel; a file's hash records are addressed by one 32-bit buffer
+// offset, so at most 2^27 records per file)
+static bool split_bloom(uint64_t m, uint32_t k, uint64_t max_file_records) {
+    return hash_once_bloom(m) && bloom_slices(m) == 2 && k <= kSplitMaxK &&
+           max_file_records <= (1ull << 27);
 }
 
 extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records,
@@ -2342,7 +2746,7 @@ extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_fil
     // the slice-1 position lists of the two-slice hash-once filter
     if (!hash_once_bloom(m) || bloom_slices(m) < 2) return 16;
     const uint64_t kk = k ? k : 1;
-    if (split_bloom(m, (uint32_t)kk))  // a hash record per key
+    if (split_bloom(m, (uint32_t)kk, max_file_records))  // a hash record per key
         return (size_t)(4ull * kHashRecDwords * nfile * (uint64_t)max_file_records + 16);
     return (size_t)(kk * nfile * (uint64_t)max_file_records * 4 + 16);
 }
@@ -2387,7 +2791,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     if (hash_once_bloom(m)) {
         const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
         if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
-        if (split_bloom(m, kk)) {
+        if (split_bloom(m, kk, max_file_records)) {
             // Filter.Add's key hash runs inside the region writer (the keys
             // are gathered there anyway, sstable.go:322-326 feeds data, index
             // and filter in one pass); the per-slice ORs follow on the same
@@ -2581,6 +2985,52 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
     hipLaunchKernelGGL(may_contain_kernel, dim3(pgrid), dim3(kMcThreads), 0, s, d_img,
                        d_file_off, d_meta, nfile, d_keys, d_koff, nkeys, d_hit,
                        (const uint32_t *)w.flag);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" size_t lsm_level_may_contain_workspace_bytes(uint32_t nfile, uint64_t nkeys) {
+    size_t total = 0;
+    lv_ws_layout(nullptr, nfile, nkeys, &total);
+    return total;
+}
+
+extern "C" int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                                     const lsm_sst_meta *d_meta, uint32_t nfile,
+                                     const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
+                                     int32_t *d_table, uint8_t *d_may, void *d_workspace,
+                                     size_t ws_bytes, void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nkeys == 0) return 0;
+    if (!d_keys || !d_koff || !d_table || !d_may) return LSM_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (nfile == 0) {  // an empty level: no candidate (manager.go:194), nothing may be there
+        LSM_HIP_CHECK(hipMemsetAsync(d_table, 0xFF, 4 * nkeys, s));
+        LSM_HIP_CHECK(hipMemsetAsync(d_may, 0, nkeys, s));
+        return 0;
+    }
+    if (!d_img || !d_file_off || !d_meta || !d_workspace) return LSM_EINVAL;
+    size_t need = 0;
+    const LvWs w = lv_ws_layout(static_cast<uint8_t *>(d_workspace), nfile, nkeys, &need);
+    if (ws_bytes < need) return LSM_ESPACE;
+    hipLaunchKernelGGL(lv_prep_kernel, dim3((nfile + 255) / 256), dim3(256), 0, s, d_img, d_file_off,
+                       d_meta, nfile, w);
+    if (nfile > kLvMaxFiles || nkeys > 0xFFFFFFFFull) {
+        const uint64_t g = (nkeys + 255) / 256;
+        hipLaunchKernelGGL(lv_probe_kernel, dim3(g < 4096 ? (uint32_t)g : 4096u), dim3(256), 0, s,
+                           d_img, nfile, d_keys, d_koff, nkeys, w, d_table, d_may);
+    } else {
+        // passes of up to 2M probes (the test kernel's segment table)
+        const uint64_t pass = (uint64_t)kLvMaxWgs * kLvProbes;
+        for (uint64_t k0 = 0; k0 < nkeys; k0 += pass) {
+            const uint64_t n = nkeys - k0 < pass ? nkeys - k0 : pass;
+            const uint32_t nwg = (uint32_t)((n + kLvProbes - 1) / kLvProbes);
+            hipLaunchKernelGGL(lv_classify_kernel, dim3(nwg), dim3(kLvThreads), 0, s, d_img, nfile,
+                               d_keys, d_koff, k0, k0 + n, w, nwg, d_table, d_may);
+            hipLaunchKernelGGL(lv_test_kernel, dim3(nfile), dim3(kLvThreads), kMcLdsBytes, s, d_img,
+                               nfile, nwg, w, k0, d_may);
+        }
+    }
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

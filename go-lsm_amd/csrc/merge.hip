@@ -28,10 +28,11 @@
 //      empty key is its own group because "" is never deduplicated) and the
 //      candidate of each group: its first pair that may be written;
 //   4. one scan of the candidates' (size, count) into interleaved sums, then
-//      one wave walks the file boundaries -- one probe round per file when it
-//      starts a group, and the windows around the next files' predicted ends
-//      ride in the same round trip (up to kWalkAhead files per round); a flush inside a group makes the next writable pair of
-//      that group a write of its own (the "extra" of the next file);
+//      one workgroup walks the file boundaries -- the windows around the next
+//      kWalkWins files' predicted ends are loaded in one round trip and the
+//      chain runs through them in LDS; a flush inside a group makes the next
+//      writable pair of that group a write of its own (the "extra" of the
+//      next file);
 //   5. emit: each candidate's output slot from its file's start.
 // Steps 3-5 are exact for any input; only the tie order is specified above.
 
@@ -53,6 +54,7 @@ constexpr uint32_t kMaxChunks = kKeyCap / 8 + 1;  // 1 MiB keys
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanPer = 2;  // 16: lanes 256 B apart (strided stores); A/B compact 1.359 -> 1.348 ms
 constexpr uint32_t kScanTile = kMergeThreads * kScanPer;
+constexpr uint32_t kMergePathMin = 4096;  // fewer pairs: the radix passes alone
 
 // Go's kv.DeletedValue, "～DELETED～" (kv/kv.go:29), 13 bytes
 __constant__ uint8_t kTomb[13] = {0xEF, 0xBD, 0x9E, 'D', 'E', 'L', 'E', 'T',
@@ -127,22 +129,48 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
     return v;
 }
 
-// Per-block partial statistics: [0] max key length, [1] min key length,
-// [2] OR / [3] AND of the key lengths, then for chunks d < kFastChunks the OR
-// and AND of chunk d over keys longer than 8d (shorter keys hold 0 there:
-// the host folds that in with the minimum key length).
-constexpr uint32_t kStatWords = 4 + 2 * kFastChunks;
+// Go string order of two keys (bytes.Compare / string <): big-endian 8-byte
+// chunks zero padded past the shorter key, then the lengths.
+__device__ __forceinline__ int key_cmp(const uint8_t *b, const View &x, const View &y) {
+    const uint32_t l = x.kl > y.kl ? x.kl : y.kl;
+    for (uint32_t d = 0; 8 * d < l; d++) {
+        const uint64_t cx = key_chunk(b + x.ko, x.kl, d), cy = key_chunk(b + y.ko, y.kl, d);
+        if (cx != cy) return cx < cy ? -1 : 1;
+    }
+    return x.kl < y.kl ? -1 : x.kl > y.kl ? 1 : 0;
+}
 
-__global__ __launch_bounds__(kMergeThreads) void merge_stats_kernel(MergeIn m, uint64_t *part) {
-    __shared__ uint64_t red[kMergeThreads / kWave][kStatWords];
-    uint64_t s[kStatWords];
+// Per-block partial statistics over a contiguous tile of the input: [0] max
+// key length, [1] min key length, [2] OR / [3] AND of the key lengths, then
+// for chunks d < kFastChunks the OR and AND of chunk d over keys longer than
+// 8d (shorter keys hold 0 there: the host folds that in with the minimum key
+// length); then the tile's run summary (sorted runs of the input, a run
+// breaking at each descent key(i) < key(i - 1)): the first and last descent,
+// their count and, when the tile holds at most 64 descents, its longest run
+// strictly inside the tile -- the host picks the input's longest sorted run
+// from these (the merge path, merge_kvs_impl).
+constexpr uint32_t kStatCore = 4 + 2 * kFastChunks;
+constexpr uint32_t kStatWords = kStatCore + 5;
+
+__global__ __launch_bounds__(kMergeThreads) void merge_stats_kernel(MergeIn m, uint32_t chunk,
+                                                                    uint64_t *part) {
+    __shared__ uint64_t red[kMergeThreads / kWave][kStatCore];
+    __shared__ uint32_t s_desc[kWave];
+    __shared__ uint32_t s_first, s_last, s_cnt;
+    uint64_t s[kStatCore];
     s[0] = 0; s[1] = ~0ull; s[2] = 0; s[3] = ~0ull;
     for (uint32_t d = 0; d < kFastChunks; d++) {
         s[4 + 2 * d] = 0;
         s[5 + 2 * d] = ~0ull;
     }
-    for (uint32_t i = blockIdx.x * kMergeThreads + threadIdx.x; i < m.n;
-         i += gridDim.x * kMergeThreads) {
+    if (threadIdx.x == 0) {
+        s_first = kNone;
+        s_last = 0;
+        s_cnt = 0;
+    }
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * chunk, hi = lo + chunk < m.n ? lo + chunk : m.n;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += kMergeThreads) {
         const View v = view(m, i);
         s[0] = v.kl > s[0] ? v.kl : s[0];
         s[1] = v.kl < s[1] ? v.kl : s[1];
@@ -156,18 +184,25 @@ __global__ __launch_bounds__(kMergeThreads) void merge_stats_kernel(MergeIn m, u
                 s[5 + 2 * d] &= c;
             }
         }
+        if (i > 0 && key_cmp(m.bytes, v, view(m, i - 1)) < 0) {  // a descent: a run starts at i
+            atomicMin(&s_first, i);
+            atomicMax(&s_last, i);
+            const uint32_t at = atomicAdd(&s_cnt, 1u);
+            if (at < kWave) s_desc[at] = i;
+        }
     }
     s[0] = wave_max64(s[0]);
     s[1] = wave_min64(s[1]);
-    for (uint32_t t = 2; t < kStatWords; t += 2) {
+    for (uint32_t t = 2; t < kStatCore; t += 2) {
         s[t] = wave_or64(s[t]);
         s[t + 1] = wave_and64(s[t + 1]);
     }
     const uint32_t w = threadIdx.x / kWave;
     if (lane_id() == 0)
-        for (uint32_t t = 0; t < kStatWords; t++) red[w][t] = s[t];
+        for (uint32_t t = 0; t < kStatCore; t++) red[w][t] = s[t];
     __syncthreads();
-    if (threadIdx.x < kStatWords) {
+    uint64_t *out = part + (uint64_t)blockIdx.x * kStatWords;
+    if (threadIdx.x < kStatCore) {
         const uint32_t t = threadIdx.x;
         uint64_t r = red[0][t];
         for (uint32_t x = 1; x < kMergeThreads / kWave; x++) {
@@ -177,7 +212,32 @@ __global__ __launch_bounds__(kMergeThreads) void merge_stats_kernel(MergeIn m, u
             else if (t & 1) r &= y;
             else r |= y;
         }
-        part[(uint64_t)blockIdx.x * kStatWords + t] = r;
+        out[t] = r;
+    }
+    if (w == 1) {
+        // the longest run between two of the tile's descents (<= 64 of them)
+        const uint32_t cnt = s_cnt, lane = lane_id();
+        uint64_t bs = 0, be = 0;
+        if (cnt >= 2 && cnt <= kWave) {
+            const uint32_t x = lane < cnt ? s_desc[lane] : kNone;
+            uint32_t nx = kNone;  // the next descent after x
+            for (uint32_t l = 0; l < cnt; l++) {
+                const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
+                if (y > x && y < nx) nx = y;
+            }
+            const uint64_t len = lane < cnt && nx != kNone ? (uint64_t)(nx - x) : 0;
+            const uint64_t key = len << 32 | x;
+            const uint64_t best = wave_max64(key);
+            bs = (uint32_t)best;
+            be = bs + (best >> 32);
+        }
+        if (lane == 0) {
+            out[kStatCore + 0] = s_first;
+            out[kStatCore + 1] = s_last;
+            out[kStatCore + 2] = cnt;
+            out[kStatCore + 3] = bs;
+            out[kStatCore + 4] = be;
+        }
     }
 }
 
@@ -255,6 +315,82 @@ __global__ __launch_bounds__(kMergeThreads) void merge_extract_kernel(MergeIn m,
 __global__ __launch_bounds__(kMergeThreads) void merge_iota_kernel(uint32_t *perm, uint32_t n) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j < n) perm[j] = j;
+}
+
+// The merge path (one sorted run holds most pairs -- a level-1 run with a
+// few level-0 files merged into it): the pairs outside the run are sorted by
+// the radix passes, and every pair's sorted position is its rank in its own
+// sequence plus its rank in the other, by (packed key, input index) --
+// stable, exactly the order the LSD passes give, in one pass over the run.
+// packed key of pair i (as merge_extract_kernel)
+template <class K>
+__device__ __forceinline__ K packed_key(const MergeIn &m, const SortGroup &g, uint32_t i) {
+    const View v = view(m, i);
+    uint64_t key = 0;
+    for (uint32_t t = 0; t < g.nf; t++) {
+        const uint64_t x = g.field[t] == kNone ? v.kl : key_chunk(m.bytes + v.ko, v.kl, g.field[t]);
+        const uint32_t bits = (uint32_t)__builtin_popcountll(g.mask[t]);
+        key = (bits >= 64 ? 0 : key << bits) | pext64(x, g.mask[t]);
+    }
+    return (K)key;
+}
+
+// the run [s, e): keys[r] = key of s + r; the others: keys[j], idx[j] of the
+// j-th pair outside the run (input order)
+template <class K>
+__global__ __launch_bounds__(kMergeThreads) void merge_extract_split_kernel(MergeIn m, SortGroup g,
+                                                                            uint32_t s, uint32_t e,
+                                                                            K *run_keys, K *oth_keys,
+                                                                            uint32_t *oth_idx) {
+    const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
+    if (j >= m.n) return;
+    if (j >= s && j < e) {
+        run_keys[j - s] = packed_key<K>(m, g, j);
+    } else {
+        const uint32_t q = j < s ? j : j - (e - s);
+        oth_keys[q] = packed_key<K>(m, g, j);
+        oth_idx[q] = j;
+    }
+}
+
+// sorted position of run pair s + r: r + the others before it
+template <class K>
+__global__ __launch_bounds__(kMergeThreads) void merge_rank_run_kernel(const K *run_keys, uint32_t nrun,
+                                                                       uint32_t s, const K *ok,
+                                                                       const uint32_t *oi, uint32_t no,
+                                                                       uint32_t *perm) {
+    const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
+    if (r >= nrun) return;
+    const K k = run_keys[r];
+    const uint32_t i = s + r;
+    uint32_t lo = 0, hi = no;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const K x = ok[mid];
+        if (x < k || (x == k && oi[mid] < i)) lo = mid + 1;
+        else hi = mid;
+    }
+    perm[r + lo] = i;
+}
+
+// sorted position of the q-th sorted other: q + the run pairs before it
+template <class K>
+__global__ __launch_bounds__(kMergeThreads) void merge_rank_others_kernel(const K *run_keys, uint32_t nrun,
+                                                                          uint32_t s, const K *ok,
+                                                                          const uint32_t *oi, uint32_t no,
+                                                                          uint32_t *perm) {
+    const uint32_t q = blockIdx.x * kMergeThreads + threadIdx.x;
+    if (q >= no) return;
+    const K k = ok[q];
+    const uint32_t i = oi[q];
+    uint32_t lo = 0, hi = nrun;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const K x = run_keys[mid];
+        if (x < k || (x == k && s + mid < i)) lo = mid + 1;
+        else hi = mid;
+    }
+    perm[q + lo] = i;
 }
 
 __device__ __forceinline__ bool keys_equal(const uint8_t *b, const View &x, const View &y) {
@@ -417,192 +553,204 @@ struct WalkArgs {
     uint64_t *counts;   // [0] = written pairs, [1] = files, [2] = most pairs in one file
 };
 
-// smallest k in [lo, hi] with sc[k].s >= t, given sc[hi].s >= t
-__device__ uint32_t wave_lower_bound(const SumPair *sc, uint32_t lo, uint32_t hi, uint64_t t) {
-    const uint32_t lane = lane_id();
-    while (hi > lo) {
-        // lane l probes lo + l*step, the last lane probes hi (>= t), so the
-        // first lane at or above t exists and the lane before it is below
-        const uint32_t span = hi - lo;
-        const uint32_t step = span >= 63 ? (span + 62) / 63 : 1;
-        uint32_t k = lo + lane * step;
-        if (k > hi || lane == kWave - 1) k = hi;
-        const uint64_t ge = __ballot(sc[k].s >= t);
-        const uint32_t f = (uint32_t)__builtin_ctzll(ge);
-        if (f == 0) return uni(lo);
-        uint32_t kf = lo + f * step;
-        if (kf > hi || f == kWave - 1) kf = hi;
-        lo = uni(lo + (f - 1) * step + 1);
-        hi = uni(kf);
-    }
-    return uni(lo);
-}
-
-// One wave walks the files (merge.go:57-91): file f starts at sorted position
-// p; if p continues a group whose pair was written just before the flush,
+// The file walk (merge.go:57-91): file f starts at sorted position p; if p
+// continues a group whose pair was written just before the flush,
 // lastWrittenKey is "" again and the group's next writable pair is written
 // (the file's "extra"); then come the candidates of later groups until the
-// size reaches the threshold.  The common case -- p starts a group and the
-// file spans about as many positions as the last one -- takes one round of
-// loads: lane 0 reads flags[p] and sc[p] while lanes 1..63 probe sc around
-// the predicted end.
-constexpr uint32_t kWalkAhead = 8;  // windows (files) per round trip of the walk
+// size reaches the threshold.  The chain of files is sequential, so its cost
+// is the round trips it waits on.  One workgroup walks it:
+//  * prediction: each of its kWalkWins waves loads, in one round trip, the
+//    (S, C, flags) of a kWalkWin-position window around the predicted end of
+//    one of the next kWalkWins files (file j of the round ends near
+//    p + (j + 1) * span, span = the last file's positions) into LDS;
+//  * chain (wave 0, LDS only): a file that starts a group ends at the first
+//    position whose S reaches S(p) + threshold; found inside its window with
+//    the position before it below the target, it is exact, and the next file
+//    starts there with its S, C and flags from the same window;
+//  * a file whose end falls outside its window, or that continues a group,
+//    is walked by the whole workgroup (group end and extra by a parallel
+//    scan of the flags, the end by a 1,024-way search over S).
+// Round 3's one-wave walk (8 windows of 256 positions per round trip, loads
+// of one wave) took 160 us for 208 files.
+constexpr uint32_t kWalkThreads = 768;
+constexpr uint32_t kWalkWins = kWalkThreads / kWave;  // files predicted per round
+constexpr uint32_t kWalkWin = 512;                    // positions per window
 
-__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t l) {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32 |
-           (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
-}
+struct WalkState {
+    uint32_t p, nf, span, stop;   // stop: 1 = walk done, 2 = general step next
+    uint64_t o, most;
+};
 
-__global__ __launch_bounds__(64) void merge_walk_kernel(WalkArgs a) {
-    const uint32_t n = a.m.n, lane = lane_id();
+__global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
+    __shared__ uint64_t ws[kWalkWins][kWalkWin];
+    __shared__ uint64_t wc[kWalkWins][kWalkWin];
+    __shared__ uint8_t wf[kWalkWins][kWalkWin];
+    __shared__ WalkState st;
+    __shared__ uint32_t s_min[2];
+    const uint32_t n = a.m.n, t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     const SumPair tail = a.sc[n];
-    uint32_t p = 0, nf = 0, span = 0;
-    uint64_t o = 0, most = 0;
-    while (p < n) {
-        // speculative round: lane 0 reads flags[p] and sc[p]; every lane reads
-        // sc at four positions of the window [w0, w0 + 256) around the
-        // predicted end (all five loads in one round trip)
-        const uint32_t w0 = span > 128 ? p + span - 127 : p + 1;
-        SumPair q[4];
+    const uint64_t T = a.threshold;
+    if (t == 0) st = WalkState{0, 0, 0, n == 0 ? 1u : 0u, 0, 0};
+    __syncthreads();
+    for (;;) {
+        WalkState S0 = st;
+        if (S0.stop == 1) break;
+        __syncthreads();
+        if (S0.span > 0 && S0.stop == 0) {
+            // prediction: window w around the predicted end of the round's file w
+            const uint64_t c = (uint64_t)S0.p + (uint64_t)(wave + 1) * S0.span;
+            const uint64_t b = c > S0.p + kWalkWin / 2 ? c - kWalkWin / 2 : S0.p + 1;
 #pragma unroll
-        for (uint32_t i = 0; i < 4; i++) {
-            const uint32_t k = w0 + lane + kWave * i;
-            q[i] = a.sc[k <= n ? k : n];
-        }
-        // ... and, in the same round trip, the windows around the next
-        // kWalkAhead - 1 predicted ends and the flags of every window: files
-        // that start a group chain through them without another round
-        const bool ahead = span > 128;
-        const uint32_t span0 = span;
-        SumPair qx[kWalkAhead - 1][4];
-        uint8_t fx[kWalkAhead][4];
-#pragma unroll
-        for (uint32_t j = 0; j < kWalkAhead; j++) {
-#pragma unroll
-            for (uint32_t i = 0; i < 4; i++) {
-                const uint64_t k = (uint64_t)w0 + (uint64_t)j * span0 + lane + kWave * i;
-                const uint32_t kc = k <= n ? (uint32_t)k : n;
-                if (j) qx[j - 1][i] = a.sc[kc];  // unconditional: no branch per load
-                fx[j][i] = a.flags[kc < n ? kc : n - 1];
+            for (uint32_t i = 0; i < kWalkWin / kWave; i++) {
+                const uint64_t k = b + kWave * i + lane;
+                const uint32_t kc = k < n ? (uint32_t)k : n;
+                const SumPair q = a.sc[kc];
+                ws[wave][kWave * i + lane] = q.s;
+                wc[wave][kWave * i + lane] = q.c;
+                wf[wave][kWave * i + lane] = k < n ? a.flags[kc] : (uint8_t)1;
             }
-        }
-        const SumPair q0 = a.sc[p];
-        const uint8_t fl0 = lane == 0 ? a.flags[p] : 0;
-        const bool starts = p == 0 || (__builtin_amdgcn_readfirstlane(fl0) & 1);
-        const uint64_t S0 = uni64(q0.s), C0 = uni64(q0.c);
-        uint32_t g = p, w = kNone, e = kNone;
-        uint64_t wsize = 0, Cg = C0;
-        bool done = false, have_ce = false;
-        uint64_t Ce = 0, Sk = 0;  // at the end found in window 0
-        uint32_t fk = 0;
-        if (starts) {
-            const uint64_t t = S0 + a.threshold;
-            if (tail.s < t) {
-                done = true;  // the rest fits in this file
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < 4; i++) {
-                    const uint64_t ge = __ballot(q[i].s >= t);
-                    if (!ge) continue;
-                    const uint32_t f = (uint32_t)__builtin_ctzll(ge);
-                    const uint32_t k = w0 + kWave * i + f;  // first probe at or above t
-                    if (k > w0 || k == p + 1) {  // the position before k is below t
-                        e = k - 1;
-                        done = true;
-                        Ce = lane_u64(q[i].c, f);
-                        Sk = lane_u64(q[i].s, f);
-                        fk = (uint32_t)__builtin_amdgcn_readlane((uint32_t)fx[0][i], f);
-                        have_ce = true;
+            __syncthreads();
+            if (wave == 0) {
+                // the round's first file: its S, C and flags from global
+                uint32_t p = S0.p;
+                uint64_t Sp = uni64(a.sc[p].s), Cp = uni64(a.sc[p].c);
+                uint32_t fp = (uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? a.flags[p] : 0);
+                uint64_t o = S0.o, most = S0.most;
+                uint32_t nf = S0.nf, span = S0.span, stop = 2;
+                for (uint32_t j = 0; j < kWalkWins; j++) {
+                    if (p >= n) { stop = 1; break; }
+                    if (!(p == 0 || (fp & 1))) break;  // continues a group: general step
+                    const uint64_t tg = Sp + T;
+                    if (tail.s < tg) {  // the rest fits in this file (merge.go:125-128)
+                        const uint64_t nw = tail.c - Cp;
+                        if (nw) {
+                            if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
+                            o += nw;
+                            most = nw > most ? nw : most;
+                            nf++;
+                        }
+                        p = n;
+                        stop = 1;
+                        break;
                     }
-                    break;
+                    const uint64_t c = (uint64_t)S0.p + (uint64_t)(j + 1) * S0.span;
+                    const uint64_t b = c > S0.p + kWalkWin / 2 ? c - kWalkWin / 2 : S0.p + 1;
+                    int hit = -1;
+#pragma unroll
+                    for (uint32_t i = 0; i < kWalkWin / kWave; i++) {
+                        const uint64_t ge = __ballot(ws[j][kWave * i + lane] >= tg);
+                        if (!ge) continue;
+                        const uint32_t x = kWave * i + (uint32_t)__builtin_ctzll(ge);
+                        // exact when the position before it is in the window
+                        // (below the target there) or is p itself
+                        if (x > 0 || b <= (uint64_t)p + 1) hit = (int)x;
+                        break;
+                    }
+                    if (hit < 0) break;  // the end lies outside the window: general step
+                    const uint32_t k = (uint32_t)(b + (uint32_t)hit);
+                    const uint64_t Ck = wc[j][hit];
+                    const uint64_t nw = Ck - Cp;
+                    if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
+                    o += nw;
+                    most = nw > most ? nw : most;
+                    nf++;
+                    span = k - p;
+                    p = k;
+                    Sp = ws[j][hit];
+                    Cp = Ck;
+                    fp = wf[j][hit];
                 }
+                if (lane == 0) st = WalkState{p, nf, span, p >= n ? 1u : stop, o, most};
             }
-        } else {
-            // the rest of the group: its end and its first writable pair
-            for (uint32_t q0 = p;; q0 += kWave) {
-                const uint32_t qq = q0 + lane;
+            __syncthreads();
+            S0 = st;
+            if (S0.stop == 1) break;
+            __syncthreads();
+        }
+        // general step: the file starting at S0.p, by the whole workgroup
+        const uint32_t p = S0.p;
+        const bool starts = p == 0 || (a.flags[p] & 1);
+        uint32_t g = p, w = kNone;
+        uint64_t wsize = 0;
+        if (!starts) {
+            // the rest of the group: its end g and its first writable pair w
+            for (uint32_t q0 = p;; q0 += kWalkThreads) {
+                if (t < 2) s_min[t] = kNone;
+                __syncthreads();
+                const uint32_t qq = q0 + t;
                 const uint8_t f = qq < n ? a.flags[qq] : 1;
-                const bool end = qq >= n || (qq > p && (f & 1));
-                const uint64_t em = __ballot(end);
-                const uint64_t wm = __ballot(!end && (f & 2)) & (em ? (em & -em) - 1 : ~0ull);
-                if (w == kNone && wm) w = uni(q0 + (uint32_t)__builtin_ctzll(wm));
-                if (em) {
-                    g = uni(q0 + (uint32_t)__builtin_ctzll(em));
-                    break;
-                }
+                const bool endg = qq >= n || (qq > p && (f & 1));
+                if (endg) atomicMin(&s_min[0], qq < n ? qq : n);
+                __syncthreads();
+                const uint32_t ge = s_min[0];
+                if (!endg && qq < ge && (f & 2)) atomicMin(&s_min[1], qq);
+                __syncthreads();
+                if (w == kNone && s_min[1] != kNone) w = s_min[1];
+                const bool fin = ge != kNone;
+                if (fin) g = ge;
+                __syncthreads();
+                if (fin) break;
             }
             if (w != kNone) {
                 const View v = view(a.m, a.perm[w]);
                 wsize = 16 + (uint64_t)v.kl + v.vl;
             }
-            Cg = g < n ? uni64(a.sc[g].c) : tail.c;
-            if (w != kNone && wsize >= a.threshold) {
-                e = w;
-                done = true;
+        }
+        const uint64_t Sg = g < n ? a.sc[g].s : tail.s, Cg = g < n ? a.sc[g].c : tail.c;
+        uint32_t end = n;
+        if (w != kNone && wsize >= T) {
+            end = w + 1;  // the extra alone fills the file
+        } else {
+            const uint64_t tg = Sg + (T - wsize);
+            if (tail.s >= tg) {
+                // first k in [g + 1, n] with S(k) >= tg: 768-way search rounds
+                uint32_t lo = g + 1, hi = n;
+                while (hi > lo) {
+                    const uint32_t span = hi - lo;
+                    const uint32_t step = span >= kWalkThreads - 1 ? (span + kWalkThreads - 2) / (kWalkThreads - 1) : 1;
+                    uint32_t k = lo + t * step;
+                    if (k > hi || t == kWalkThreads - 1) k = hi;
+                    if (t == 0) s_min[0] = kNone;
+                    __syncthreads();
+                    const uint64_t sk = k < n ? a.sc[k].s : tail.s;
+                    if (sk >= tg) atomicMin(&s_min[0], t);
+                    __syncthreads();
+                    const uint32_t f = s_min[0];
+                    __syncthreads();
+                    if (f == 0) { hi = lo; break; }
+                    uint32_t kf = lo + f * step;
+                    if (kf > hi || f == kWalkThreads - 1) kf = hi;
+                    lo = lo + (f - 1) * step + 1;
+                    hi = kf;
+                }
+                end = lo;  // the first position at or above the target; e = end - 1
             }
         }
-        if (!done) {
-            const uint64_t Sg = g < n ? uni64(a.sc[g].s) : tail.s;
-            const uint64_t t = Sg + (a.threshold - wsize);
-            if (tail.s >= t) e = wave_lower_bound(a.sc, g + 1, n, t) - 1;
-        }
-        const uint32_t end = e == kNone ? n : e + 1;
-        if (!have_ce) Ce = end < n ? uni64(a.sc[end].c) : tail.c;
+        const uint64_t Ce = end < n ? a.sc[end].c : tail.c;
         const uint64_t nw = (w != kNone ? 1 : 0) + (end > g ? Ce - Cg : 0);
-        if (nw == 0) break;  // nothing left to write: no file (builder.size == 0)
-        if (lane == 0) {
-            a.files[nf] = MergeFile{p, w, o};
-            if (w != kNone) a.out[o] = a.perm[w];
-        }
-        o += nw;
-        most = nw > most ? nw : most;
-        nf++;
-        span = end - g;
-        p = end;
-        if (!(starts && have_ce && ahead)) continue;
-        // chain: file j starts at p (found in window j - 1, with its S, C and
-        // flags); its end is exact when it lies inside window j
-        uint64_t Sj = Sk, Cj = Ce;
-        uint32_t fj = fk;
-#pragma unroll
-        for (uint32_t j = 1; j < kWalkAhead; j++) {
-            if (p >= n || !(fj & 1)) break;  // done, or a group continues: general round
-            const uint64_t t = Sj + a.threshold;
-            if (tail.s < t) break;  // the last file: general round
-            const uint64_t wj = (uint64_t)w0 + (uint64_t)j * span0;
-            bool hit = false;
-            uint32_t k = 0, fn = 0;
-            uint64_t Cn = 0, Sn = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < 4; i++) {
-                const uint64_t ge = __ballot(qx[j - 1][i].s >= t);
-                if (!ge) continue;
-                const uint32_t f = (uint32_t)__builtin_ctzll(ge);
-                const uint64_t kk = wj + kWave * i + f;
-                hit = kk > wj || kk == (uint64_t)p + 1;  // the position before is below t
-                k = (uint32_t)kk;
-                Cn = lane_u64(qx[j - 1][i].c, f);
-                Sn = lane_u64(qx[j - 1][i].s, f);
-                fn = (uint32_t)__builtin_amdgcn_readlane((uint32_t)fx[j][i], f);
-                break;
+        if (t == 0) {
+            WalkState x = S0;
+            if (nw == 0) {
+                x.stop = 1;  // nothing left to write: no file (builder.size == 0)
+            } else {
+                a.files[x.nf] = MergeFile{p, w, x.o};
+                if (w != kNone) a.out[x.o] = a.perm[w];
+                x.o += nw;
+                x.most = nw > x.most ? nw : x.most;
+                x.nf++;
+                x.span = end > g ? end - g : 0;  // 0: no prediction next round
+                x.p = end;
+                x.stop = end >= n ? 1u : 0u;
             }
-            if (!hit || Cn == Cj) break;
-            if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
-            o += Cn - Cj;
-            most = Cn - Cj > most ? Cn - Cj : most;
-            nf++;
-            span = k - p;
-            p = k;
-            Cj = Cn;
-            Sj = Sn;
-            fj = fn;
+            st = x;
         }
+        __syncthreads();
     }
-    if (lane == 0) {
-        a.files[nf] = MergeFile{n, kNone, o};
-        a.counts[0] = o;
-        a.counts[1] = nf;
-        a.counts[2] = most;
+    if (t == 0) {
+        a.files[st.nf] = MergeFile{n, kNone, st.o};
+        a.counts[0] = st.o;
+        a.counts[1] = st.nf;
+        a.counts[2] = st.most;
     }
 }
 
@@ -1002,6 +1150,33 @@ extern "C" size_t lsm_merge_kvs_workspace_bytes(uint64_t n) {
     return merge_ws_layout(nullptr, (uint32_t)n).total;
 }
 
+// The merge path (merge_rank_*): the pairs outside the run [rs, re) are
+// packed and radix-sorted (with their input index), the run's keys packed,
+// and each pair's sorted position written to w.perm[0].  Workspace: the
+// run's keys in w.keys[0]; the others' keys (two buffers) in w.keys[1] and
+// their indices in w.perm[1] (no <= n / 2).
+template <class K>
+static int merge_path(const MergeWs &w, const MergeIn &m, const SortGroup &g, uint32_t bits,
+                      uint32_t rs, uint32_t re, uint32_t no, hipStream_t s) {
+    const uint32_t N = m.n, nrun = re - rs;
+    K *run_keys = reinterpret_cast<K *>(w.keys[0]);
+    K *ok0 = reinterpret_cast<K *>(w.keys[1]), *ok1 = ok0 + no;
+    uint32_t *oi0 = w.perm[1], *oi1 = w.perm[1] + no;
+    hipLaunchKernelGGL(merge_extract_split_kernel<K>, dim3(grid_for(N)), dim3(kMergeThreads), 0, s, m,
+                       g, rs, re, run_keys, ok0, oi0);
+    if (no) {
+        size_t tb = w.sort_bytes;
+        const hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, tb, ok0, ok1, oi0, oi1, no, 0, bits, s);
+        if (e != hipSuccess) return -(1000 + (int)e);
+        hipLaunchKernelGGL(merge_rank_others_kernel<K>, dim3(grid_for(no)), dim3(kMergeThreads), 0, s,
+                           run_keys, nrun, rs, ok1, oi1, no, w.perm[0]);
+    }
+    hipLaunchKernelGGL(merge_rank_run_kernel<K>, dim3(grid_for(nrun)), dim3(kMergeThreads), 0, s,
+                       run_keys, nrun, rs, ok1, oi1, no, w.perm[0]);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
                                  const lsm_rec_desc *d_key_desc, const lsm_rec_desc *d_val_desc,
                                  uint64_t n, int level, uint64_t threshold, int tie,
@@ -1022,22 +1197,36 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     const MergeIn m{d_bytes, d_key_desc, d_val_desc, N};
     const uint32_t sb = grid_for(n) < kStatBlocks ? grid_for(n) : kStatBlocks;
 
-    // 1. key statistics: one pass, per-block partials reduced here
-    hipLaunchKernelGGL(merge_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, w.part);
+    // 1. key statistics and the sorted runs: one pass over contiguous
+    //    tiles, per-tile partials reduced here
+    const uint32_t chunk = (N + sb - 1) / sb;
+    hipLaunchKernelGGL(merge_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, chunk, w.part);
     std::vector<uint64_t> part((size_t)sb * kStatWords);
     LSM_HIP_CHECK(hipMemcpyAsync(part.data(), w.part, part.size() * 8, hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
-    uint64_t st[kStatWords];
-    for (uint32_t t = 0; t < kStatWords; t++) st[t] = part[t];
-    for (uint32_t b = 1; b < sb; b++) {
+    uint64_t st[kStatCore];
+    for (uint32_t t = 0; t < kStatCore; t++) st[t] = part[t];
+    uint64_t run_s = 0, run_e = 0, cur_s = 0;  // the longest run found, the open one
+    auto run = [&](uint64_t a, uint64_t b) {
+        if (b - a > run_e - run_s) { run_s = a; run_e = b; }
+    };
+    for (uint32_t b = 0; b < sb; b++) {
         const uint64_t *q = &part[(size_t)b * kStatWords];
-        st[0] = q[0] > st[0] ? q[0] : st[0];
-        st[1] = q[1] < st[1] ? q[1] : st[1];
-        for (uint32_t t = 2; t < kStatWords; t += 2) {
-            st[t] |= q[t];
-            st[t + 1] &= q[t + 1];
+        if (b) {
+            st[0] = q[0] > st[0] ? q[0] : st[0];
+            st[1] = q[1] < st[1] ? q[1] : st[1];
+            for (uint32_t t = 2; t < kStatCore; t += 2) {
+                st[t] |= q[t];
+                st[t + 1] &= q[t + 1];
+            }
         }
+        const uint64_t *r = q + kStatCore;  // first, last descent, count, inner run
+        if (r[2] == 0) continue;
+        run(cur_s, r[0]);
+        if (r[4] > r[3]) run(r[3], r[4]);
+        cur_s = r[1];
     }
+    run(cur_s, N);
     const uint32_t D = (uint32_t)((st[0] + 7) / 8), minlen = (uint32_t)st[1];
     if (D > kMaxChunks) return LSM_EINVAL;
     std::vector<uint64_t> orand(2 * (size_t)(D > kFastChunks ? D : kFastChunks));
@@ -1070,6 +1259,26 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     }
     int cur = 0;
     bool have_perm = false;
+    // the merge path: every varying bit in one packed key and one sorted run
+    // holding at least half the pairs
+    uint32_t all_bits = 0;
+    for (const auto &f : fields) all_bits += (uint32_t)__builtin_popcountll(f.second);
+    const uint32_t rs = (uint32_t)run_s, re = (uint32_t)run_e, no = N - (re - rs);
+    if (!fields.empty() && fields.size() <= kGroupFields && all_bits <= 64 && no <= N / 2 &&
+        N >= kMergePathMin) {
+        SortGroup g{};
+        g.nf = (uint32_t)fields.size();
+        for (size_t t = 0; t < g.nf; t++) {  // most significant first
+            g.field[t] = fields[g.nf - 1 - t].first;
+            g.mask[t] = fields[g.nf - 1 - t].second;
+        }
+        const int rc = all_bits <= 32
+                           ? merge_path<uint32_t>(w, m, g, all_bits, rs, re, no, s)
+                           : merge_path<uint64_t>(w, m, g, all_bits, rs, re, no, s);
+        if (rc) return rc;
+        fields.clear();
+        have_perm = true;  // w.perm[0]
+    }
     for (size_t f0 = 0; f0 < fields.size();) {
         size_t f1 = f0;
         uint32_t bits = 0;
@@ -1148,7 +1357,7 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     hipLaunchKernelGGL(merge_scan_apply, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
                        w.scan_part, w.sc);
     WalkArgs wa{m, perm, w.flags, w.sc, threshold, w.files, d_out, w.stats};
-    hipLaunchKernelGGL(merge_walk_kernel, dim3(1), dim3(64), 0, s, wa);
+    hipLaunchKernelGGL(merge_walk_kernel, dim3(1), dim3(kWalkThreads), 0, s, wa);
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
                        w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);
     LSM_HIP_CHECK(hipGetLastError());

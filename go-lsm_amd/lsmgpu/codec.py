@@ -449,6 +449,36 @@ def may_contain(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordB
     return hit
 
 
+def level_may_contain_workspace(ctx: Context, nfile: int, nkeys: int) -> torch.Tensor:
+    n = int(ctx.lib.lsm_level_may_contain_workspace_bytes(nfile, nkeys))
+    return torch.empty(max(n, 16), dtype=torch.uint8, device=ctx.torch_device)
+
+
+def level_may_contain_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                           table: torch.Tensor, may: torch.Tensor,
+                           ws: Optional[torch.Tensor] = None, stream=None) -> None:
+    """lsm_level_may_contain: searchFromLevelWithSparseIndex's candidate table
+    (int32 per key, -1 for an empty level) and its MayContain (uint8 per key)
+    for a level >= 1 whose tables were decoded into r in sparse-index order."""
+    if ws is None:
+        ws = level_may_contain_workspace(ctx, r.nfile, batch.n)
+    _lib.check(ctx.lib.lsm_level_may_contain(
+        ctx.handle, _ptr(d_img) if r.nfile else None, _ptr(r.d_file_off) if r.nfile else None,
+        _ptr(r.meta) if r.nfile else None, r.nfile, _ptr(batch.keys), _ptr(batch.koff), batch.n,
+        _ptr(table), _ptr(may), _ptr(ws), ws.numel(), _stream_handle(stream)),
+        "lsm_level_may_contain")
+
+
+def level_may_contain(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                      stream=None):
+    """-> (table int32[nkeys], may uint8[nkeys]) on the device."""
+    table = torch.empty(max(batch.n, 1), dtype=torch.int32, device=ctx.torch_device)
+    may = torch.empty(max(batch.n, 1), dtype=torch.uint8, device=ctx.torch_device)
+    if batch.n:
+        level_may_contain_into(ctx, d_img, r, batch, table, may, stream=stream)
+    return table[:batch.n], may[:batch.n]
+
+
 # ---- encode -----------------------------------------------------------------
 
 @dataclass
@@ -537,14 +567,18 @@ class SstBuild:
     device, so nothing is read back before the build)."""
 
     def __init__(self, out, footer, workspace, d_file_start, d_file_off, max_recs, m, k, nfile,
-                 file_start=None, file_off=None, file_size=None, d_file_size=None):
+                 file_start=None, file_off=None, file_size=None, d_file_size=None, stream=None):
         self.out, self.footer, self.workspace = out, footer, workspace
         self.d_file_start, self.d_file_off, self.d_file_size = d_file_start, d_file_off, d_file_size
         self.max_recs, self.m, self.k, self.nfile = max_recs, m, k, nfile
         self._file_start, self._file_off, self._file_size = file_start, file_off, file_size
+        self.stream = stream  # the stream the device layout (and the build) run on
 
-    @staticmethod
-    def _host(t, n):
+    def _host(self, t, n):
+        # the layout kernel ran on self.stream, which need not be torch's
+        # current stream: wait for it before the first host copy
+        if self.stream is not None:
+            self.stream.synchronize()
         return t[:n].cpu().numpy().view(np.uint64).copy()
 
     @property
@@ -735,7 +769,8 @@ def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Ten
         footer=torch.zeros(max(nfile, 1) * 4, dtype=torch.int64, device=dev),
         workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
         d_file_start=d_file_start[:nfile + 1], d_file_off=d_off, d_file_size=d_size,
-        max_recs=max_recs, m=m, k=k, nfile=nfile)
+        max_recs=max_recs, m=m, k=k, nfile=nfile,
+        stream=stream if stream is not None else torch.cuda.current_stream(dev))
 
 
 def sst_pairs_into(ctx: Context, r: "SstDecode", key_out: torch.Tensor, val_out: torch.Tensor,

@@ -276,6 +276,24 @@ int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_o
                     const uint64_t *d_koff, uint64_t nkeys, uint8_t *d_hit, void *d_workspace,
                     size_t ws_bytes, void *stream);
 
+/* Batched Manager.searchFromLevelWithSparseIndex (sstable/manager.go:178-207)
+ * up to searchFromTable's MayContain (:209-212) for a level >= 1: the nfile
+ * images are the level's tables in sparse-index order (sorted by MinKey,
+ * manager.go:290-303), d_meta their lsm_decode_sst output.  For key i:
+ * sort.Search (Go's exact bisection) for the first table whose MinKey > key
+ * (bytes.Compare), index-- when > 0 (:186-192), then SSTable.MayContain
+ * (sstable.go:300-305) of that one table: d_table[i] = the candidate (-1 when
+ * the level is empty), d_may[i] = 1 when the table may hold the key.  A table
+ * whose header did not decode searches as the zero Header (MinKey "") and,
+ * like one whose filter did not decode, answers 0; filter deviations as
+ * lsm_may_contain.  Level 0 (searchFromLevel0, :160-176, every table in
+ * order) is lsm_may_contain.  Workspace: lsm_level_may_contain_workspace_bytes. */
+size_t lsm_level_may_contain_workspace_bytes(uint32_t nfile, uint64_t nkeys);
+int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                          const lsm_sst_meta *d_meta, uint32_t nfile, const uint8_t *d_keys,
+                          const uint64_t *d_koff, uint64_t nkeys, int32_t *d_table,
+                          uint8_t *d_may, void *d_workspace, size_t ws_bytes, void *stream);
+
 /* ---- encode ---------------------------------------------------------------- */
 
 /* Batch encode of a columnar record batch (CSR: record i's key is

@@ -628,33 +628,68 @@ static int go_strcmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t l
     return la < lb ? -1 : la > lb ? 1 : 0;
 }
 
+/* SSTable.MayContain (sstable.go:300-305) of one decoded image: the key range
+ * check, then Filter.Test (bloom.go:371-379) with the bits read from the
+ * stored words.  A file whose header or filter did not decode answers 0. */
+static uint8_t may_contain_one(const uint8_t *base, const ora_sst_meta *M, const uint8_t *key,
+                               uint64_t kl) {
+    if (M->stage == 1 || M->stage == 2) return 0;
+    /* sstable.go:301: MinKey > key || MaxKey < key -> false */
+    if (go_strcmp(base + M->min_key_off, M->min_key_len, key, kl) > 0 ||
+        go_strcmp(base + M->max_key_off, M->max_key_len, key, kl) < 0)
+        return 0;
+    uint64_t h[4];
+    ora_sum256(key, kl, h);
+    uint8_t r = 1;
+    for (uint64_t j = 0; j < M->filter_k && r; j++) {
+        if (M->filter_m == 0) return 0; /* Go panics; the ABI answers 0 */
+        const uint64_t q = ora_location(h, j) % M->filter_m;
+        if (q >= M->filter_nbits) return 0;
+        const uint8_t byte = base[M->filter_words_off + 8 * (q >> 6) + 7 - ((q & 63) >> 3)];
+        r = (byte >> (q & 7)) & 1;
+    }
+    return r;
+}
+
 void ora_may_contain_batch(const uint8_t *img, const uint64_t *file_off, const ora_sst_meta *meta,
                            uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
                            uint64_t k1, uint8_t *hit) {
     for (uint64_t i = k0; i < k1; i++) {
         const uint8_t *key = keys + koff[i];
         const uint64_t kl = koff[i + 1] - koff[i];
-        for (uint32_t f = 0; f < nfile; f++) {
-            const ora_sst_meta *M = &meta[f];
-            const uint8_t *base = img + file_off[f];
-            uint8_t r = 0;
-            if (M->stage != 1 && M->stage != 2 &&
-                /* sstable.go:301: MinKey > key || MaxKey < key -> false */
-                go_strcmp(base + M->min_key_off, M->min_key_len, key, kl) <= 0 &&
-                go_strcmp(base + M->max_key_off, M->max_key_len, key, kl) >= 0) {
-                /* Filter.Test bloom.go:371-379, bits read from the stored words */
-                uint64_t h[4];
-                ora_sum256(key, kl, h);
-                r = 1;
-                for (uint64_t j = 0; j < M->filter_k && r; j++) {
-                    if (M->filter_m == 0) { r = 0; break; } /* Go panics; the ABI answers 0 */
-                    const uint64_t q = ora_location(h, j) % M->filter_m;
-                    if (q >= M->filter_nbits) { r = 0; break; }
-                    const uint8_t byte = base[M->filter_words_off + 8 * (q >> 6) + 7 - ((q & 63) >> 3)];
-                    r = (byte >> (q & 7)) & 1;
-                }
-            }
-            hit[(i - k0) * nfile + f] = r;
+        for (uint32_t f = 0; f < nfile; f++)
+            hit[(i - k0) * nfile + f] = may_contain_one(img + file_off[f], &meta[f], key, kl);
+    }
+}
+
+void ora_level_may_contain(const uint8_t *img, const uint64_t *file_off, const ora_sst_meta *meta,
+                           uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
+                           uint64_t k1, int32_t *table, uint8_t *may) {
+    for (uint64_t i = k0; i < k1; i++) {
+        const uint8_t *key = keys + koff[i];
+        const uint64_t kl = koff[i + 1] - koff[i];
+        /* sort.Search(len(sparseIndexes), f) (manager.go:186-188; Go sort.go:
+         * i, j := 0, n; for i < j { h := int(uint(i+j) >> 1); if !f(h) { i = h + 1 }
+         * else { j = h } }), f(h) = bytes.Compare(MinKey_h, key) > 0; a file whose
+         * header did not decode has the zero Header, MinKey "" */
+        uint32_t lo = 0, hi = nfile;
+        while (lo < hi) {
+            const uint32_t h = (uint32_t)(((uint64_t)lo + hi) >> 1);
+            const ora_sst_meta *M = &meta[h];
+            const int hdr = M->stage != 1;
+            const int gt = hdr && go_strcmp(img + file_off[h] + M->min_key_off, M->min_key_len,
+                                            key, kl) > 0;
+            if (!gt) lo = h + 1;
+            else hi = h;
+        }
+        uint32_t idx = lo;
+        if (idx > 0) idx--; /* manager.go:189-191 */
+        if (idx < nfile) {  /* manager.go:194-196: searchFromTable -> MayContain (:209-212) */
+            table[i - k0] = (int32_t)idx;
+            may[i - k0] = may_contain_one(img + file_off[idx], &meta[idx], key, kl);
+        } else {            /* an empty level */
+            table[i - k0] = -1;
+            may[i - k0] = 0;
         }
     }
 }
@@ -706,7 +741,12 @@ static int rd_key(int fd, ora_buf *k) {             /* Key.DecodeFrom kv.go:124-
     if (rd_full(fd, &kl, 4)) return -1;
     k->p = (uint8_t *)malloc(kl ? kl : 1);
     k->n = kl;
-    return rd_full(fd, k->p, kl);
+    if (rd_full(fd, k->p, kl)) {  /* the caller never owns a key it did not get */
+        free(k->p);
+        k->p = NULL;
+        return -1;
+    }
+    return 0;
 }
 
 int64_t ora_sst_decode_file(const char *path) {

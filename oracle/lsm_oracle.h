@@ -163,6 +163,17 @@ void ora_may_contain_batch(const uint8_t *img, const uint64_t *file_off, const o
                            uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
                            uint64_t k1, uint8_t *hit);
 
+/* Manager.searchFromLevelWithSparseIndex (sstable/manager.go:178-207) up to
+ * searchFromTable's MayContain (:209-212), keys [k0, k1) against one level's
+ * tables in sparse-index order (sorted by MinKey, manager.go:290-303):
+ * Go's sort.Search for the first table whose MinKey > key, index-- when > 0,
+ * then SSTable.MayContain of that table.  table[i - k0] = the candidate (-1 for
+ * an empty level), may[i - k0] = its MayContain.  A table whose header did not
+ * decode searches as the zero Header (MinKey "") and answers 0. */
+void ora_level_may_contain(const uint8_t *img, const uint64_t *file_off, const ora_sst_meta *meta,
+                           uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
+                           uint64_t k1, int32_t *table, uint8_t *may);
+
 /* ---- compaction merge ----------------------------- */
 
 enum { ORA_TIE_INPUT = 0, ORA_TIE_GOHEAP = 1 };
@@ -185,11 +196,12 @@ uint64_t ora_merge_kvs(const uint8_t *bytes, const uint64_t *koff, const uint32_
 
 /* ---- CPU baseline (Go allocation pattern) ------------------------------ */
 
+/* config 1 from a file with the reference's read(2)-per-field pattern -> pairs, < 0 on error */
+int64_t ora_sst_decode_file(const char *path);
+
 /* Decode blocks the way the Go path does: a fresh heap buffer per key and
  * per value, append-grown record slices; `threads` pthreads over a static
  * block partition.  Returns total records decoded. */
-/* config 1 from a file with the reference's read(2)-per-field pattern -> pairs, < 0 on error */
-int64_t ora_sst_decode_file(const char *path);
 uint64_t ora_bench_decode_golike(int grammar, const uint8_t *base, const uint64_t *blk_off,
                                  const uint32_t *blk_len, uint64_t nblk, int threads);
 

@@ -53,6 +53,7 @@ def lib():
         "ora_bloom_test": (ctypes.c_int, [vp, u64, u64, vp, u64]),
         "ora_filter_test": (ctypes.c_int, [vp, u64, u64, u64, vp, u64]),
         "ora_may_contain_batch": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp]),
+        "ora_level_may_contain": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp, vp]),
         "ora_estimate_parameters": (None, [u64, ctypes.c_double, vp, vp]),
         "ora_filter_block_size": (u64, [u64]),
         "ora_filter_encode": (u64, [vp, u64, u64, vp]),
@@ -314,3 +315,20 @@ def may_contain_batch(img, file_off, metas, keys, koff, k0, k1):
     lib().ora_may_contain_batch(_p(img), _p(file_off), ctypes.cast(arr, vp), nfile, _p(keys),
                                 _p(koff), k0, k1, _p(hit))
     return hit
+
+
+def level_may_contain(img, file_off, metas, keys, koff, k0, k1):
+    """searchFromLevelWithSparseIndex's candidate table + MayContain for keys
+    [k0, k1) over one level's tables in sparse-index order
+    -> (int32 table (k1-k0,), uint8 may (k1-k0,))."""
+    img = _bytes(img)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64) if len(file_off) else np.zeros(1, np.uint64)
+    keys = _bytes(keys) if len(keys) else np.zeros(1, np.uint8)
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    nfile = len(metas)
+    arr = metas if isinstance(metas, ctypes.Array) else (SstMeta * max(nfile, 1))(*metas)
+    table = np.zeros(max(k1 - k0, 1), np.int32)
+    may = np.zeros(max(k1 - k0, 1), np.uint8)
+    lib().ora_level_may_contain(_p(img), _p(file_off), ctypes.cast(arr, vp), nfile, _p(keys),
+                                _p(koff), k0, k1, _p(table), _p(may))
+    return table[:k1 - k0], may[:k1 - k0]

@@ -383,3 +383,38 @@ def test_full_size_compaction_build(ctx):
         o = int(sb.file_off[f])
         assert int(sb.file_size[f]) == want.size
         assert np.array_equal(out[o:o + want.size], want), f
+
+
+@pytest.mark.parametrize("tie", TIES)
+@pytest.mark.parametrize("shape", ["run_last", "run_first", "run_middle", "sorted", "two_runs"])
+def test_merge_path_one_long_run(ctx, tie, shape):
+    """The merge path (one sorted run holds at least half the pairs): level-0
+    style updates (sorted per file, newest first, duplicates of run keys and
+    of each other, tombstones, empty keys, a key that is a prefix of
+    another) beside one long sorted run; the run at the end, the start or in
+    the middle of the input, a fully sorted input (no others) and two runs
+    of equal length.  Levels 1 and 6, thresholds that flush inside
+    duplicate groups; both tie modes."""
+    rng = random.Random(hash(shape) & 0xFFFF)
+    base = sorted({b"key%05d" % rng.randint(0, 99999) for _ in range(6000)})
+    runp = [(k, b"v" * rng.randint(0, 30)) for k in base]
+    l0 = []
+    for f in range(4):
+        ks = sorted({rng.choice(base) if rng.random() < 0.7 else b"key%05d" % rng.randint(0, 99999)
+                     for _ in range(300)})
+        l0 += [(k, TOMB if rng.random() < 0.1 else b"u%d" % f) for k in ks]
+    l0 += [(b"", b"e"), (b"key0", b"p"), (b"key00000", b"q")]
+    if shape == "run_last":
+        pairs = l0 + runp
+    elif shape == "run_first":
+        pairs = runp + l0
+    elif shape == "run_middle":
+        pairs = l0[:600] + runp + l0[600:]
+    elif shape == "sorted":
+        pairs = runp
+    else:
+        half = len(runp) // 2
+        pairs = runp[half:] + runp[:half]
+    for level in (1, 6):
+        for thr in (MiB2, 4000, 257):
+            run(ctx, pairs, level, thr, seed=level, tie=tie)
