@@ -47,7 +47,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
                     choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal",
-                             "probe", "compact"])
+                             "probe", "level", "compact"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU (weak scaling)")
     ap.add_argument("--global-blocks", type=int, default=None,
                     help="fixed global batch dealt round-robin over the ranks (strong "
@@ -145,6 +145,32 @@ def max_over_ranks(world, x):
 def sum_over_ranks(world, x):
     import torch.distributed as dist
     return _reduce(world, x, dist.ReduceOp.SUM if world > 1 else None)
+
+
+def gather_over_ranks(world, x):
+    """[x of rank 0, x of rank 1, ...] (a scalar per rank; world 1: [x])."""
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
+def aggregate_roofline(world, alg, kern_ms):
+    """N > 1: the job's roofline -- the algorithmic bytes of every rank's
+    launch over the slowest rank's kernel time, against N x the peak -- and
+    the per-rank kernel times it comes from."""
+    algs = gather_over_ranks(world, float(alg))
+    kms = gather_over_ranks(world, float(kern_ms))
+    ach = sum(algs) / (max(kms) * 1e-3) / 1e9
+    return {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+            "frac": round(ach / (HBM_PEAK_GBS * world), 4),
+            "alg_bytes_per_launch": int(sum(algs)), "kernel_ms_max": round(max(kms), 5),
+            "kernel_ms_per_rank": [round(x, 5) for x in kms],
+            "def": "sum of the ranks' algorithmic bytes / max-over-ranks kernel time / (N x peak)"}
 
 
 def shard_block_ids(rank, world, per):
@@ -345,6 +371,8 @@ def bench_decode(args, world, rank, local):
     }
     if cold is not None:
         out["cold_input"] = cold
+    if world > 1:
+        out["roofline"]["aggregate"] = aggregate_roofline(world, alg, kern_ms)
     return out, (buf, blk_off, blk_len)
 
 
@@ -683,11 +711,18 @@ def cpu_baseline(args, data):
 def dry_run(args, world, rank):
     """--dry-run: the launcher and the deal without device work (CPU, gloo).
     Rank 0 prints the deal: blocks per rank and checksums of the dealt ids."""
+    recs = 0
     if args.config in UNIFORM:
         ids, scaling, total = block_ids_for(args, world, rank)
+    elif args.config == "sst":
+        # config 3's deal: whole .sst files of one stream, file f -> rank f mod N
+        from bench_sst import sst_deal
+        batch, starts, ids, total, _ = sst_deal(args, world, rank)
+        scaling, recs = "strong", int(starts[-1])
     else:
         ids, scaling, total = np.arange(rank, rank + 1, dtype=np.int64), "weak", world
     assert bool((ids % world == rank).all())
+    recs_all = gather_over_ranks(world, float(recs))
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([ids.size, int(ids.sum()), int((ids.astype(np.float64) ** 2).sum())],
@@ -700,7 +735,7 @@ def dry_run(args, world, rank):
     return {"dry_run": True, "n_gpus": world, "config": args.config, "scaling": scaling,
             "global_blocks": total, "blocks_per_rank": [int(r[0]) for r in rows],
             "id_sum": int(sum(r[1] for r in rows)), "id_sumsq": float(sum(r[2] for r in rows)),
-            "pid": os.getpid()}
+            "records_per_rank": [int(x) for x in recs_all], "pid": os.getpid()}
 
 
 def main(argv=None):
@@ -737,12 +772,17 @@ def main(argv=None):
     elif args.config == "probe":
         from bench_sstdec import bench_may_contain  # batched MayContain (§8(f) f3)
         out, data = bench_may_contain(args, world, rank, local)
+    elif args.config == "level":
+        from bench_sstdec import bench_level_search  # level search, reference shape (§8(f) f3)
+        out, data = bench_level_search(args, world, rank, local)
     elif args.config == "compact":
         from bench_compact import bench_compact  # L0 -> L1 compaction (§8(f) f1 + f2)
         out, data = bench_compact(args, world, rank, local)
     else:
         out, data = bench_decode(args, world, rank, local)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the CPU baseline on rank 0, after every rank's timed region (at N > 1
+    # over rank 0's shard: the same sample shape as at N = 1)
+    if rank == 0 and not args.no_cpu_baseline:
         if args.config == "sst":
             from bench_sst import cpu_baseline_sst
             out["cpu_baseline"] = cpu_baseline_sst(args, data)
@@ -752,6 +792,9 @@ def main(argv=None):
         elif args.config == "probe":
             from bench_sstdec import cpu_baseline_may_contain
             out["cpu_baseline"] = cpu_baseline_may_contain(args, data)
+        elif args.config == "level":
+            from bench_sstdec import cpu_baseline_level_search
+            out["cpu_baseline"] = cpu_baseline_level_search(args, data)
         elif args.config == "compact":
             from bench_compact import cpu_baseline_compact
             out["cpu_baseline"] = cpu_baseline_compact(args, data)

@@ -21,17 +21,53 @@ from lsmgpu import synth  # noqa: E402
 GIB = float(1 << 30)
 
 
-def bench_sst(args, world, rank, local):
-    from bench import barrier, max_over_ranks, sum_over_ranks, timed_region, kernel_times, HBM_PEAK_GBS
-    ctx = lsmgpu.Context(local)
+def sst_deal(args, world, rank):
+    """Config 3 over N GPUs: the global stream -- 3.3M
+    records by default -- is cut into files by the builder rule
+    (builder.go:34-59) and whole files are dealt round-robin, file f -> rank
+    f mod N (each file's filter is private: no reduction, no collective; the
+    callers, manager.go:74-95 / :349-362, build each table on its own).
+    -> (this rank's CSR batch of its files' records, its local file starts,
+    its global file ids, the global file count, the builder-rule ms)."""
     n = (args.blocks or 100_000) * 33
-    keys, koff, vals, voff = synth.kv_stream(n, first=rank * n)
+    keys, koff, vals, voff = synth.kv_stream(n)
+    tb0 = time.perf_counter()
+    lib = lsmgpu._lib.load()
+    gs = np.zeros(n + 2, dtype=np.uint64)
+    nf = int(lib.lsm_segment_files_host(koff.ctypes.data, voff.ctypes.data, n,
+                                        lsmgpu.MAX_SSTABLE_SIZE, gs.ctypes.data))
+    gs = gs[:nf + 1].astype(np.int64)
+    rule_ms = (time.perf_counter() - tb0) * 1e3
+    mine = np.arange(rank, nf, world, dtype=np.int64)
+    if world == 1:
+        return (keys, koff, vals, voff), gs.astype(np.uint64), mine, nf, rule_ms
+    lk, lv, lko, lvo, starts = [], [], [np.zeros(1, np.int64)], [np.zeros(1, np.int64)], [0]
+    kb = vb = 0
+    for f in mine:
+        s, e = int(gs[f]), int(gs[f + 1])
+        k0, k1, v0, v1 = int(koff[s]), int(koff[e]), int(voff[s]), int(voff[e])
+        lk.append(keys[k0:k1])
+        lv.append(vals[v0:v1])
+        lko.append(koff[s + 1:e + 1].astype(np.int64) - k0 + kb)
+        lvo.append(voff[s + 1:e + 1].astype(np.int64) - v0 + vb)
+        kb += k1 - k0
+        vb += v1 - v0
+        starts.append(starts[-1] + (e - s))
+    batch = (np.concatenate(lk), np.concatenate(lko).astype(np.uint64),
+             np.concatenate(lv), np.concatenate(lvo).astype(np.uint64))
+    return batch, np.array(starts, np.uint64), mine, nf, rule_ms
+
+
+def bench_sst(args, world, rank, local):
+    from bench import (barrier, max_over_ranks, sum_over_ranks, timed_region, kernel_times,
+                       HBM_PEAK_GBS, aggregate_roofline)
+    ctx = lsmgpu.Context(local)
+    (keys, koff, vals, voff), starts, mine, nf_all, rule_ms = sst_deal(args, world, rank)
+    n = len(koff) - 1
     batch = lsmgpu.batch_to_device(ctx, keys, koff, vals, voff)
     # the builder rule (builder.go:34-59: EstimateSize sums, flush at 2 MiB)
     # and the image layout run on the host once per stream; their cost is
     # reported next to the line (builder_rule_ms)
-    tb0 = time.perf_counter()
-    starts = lsmgpu.segment_files(ctx, koff, voff, lsmgpu.MAX_SSTABLE_SIZE)
     tb1 = time.perf_counter()
     sb = lsmgpu.prepare_sst(ctx, batch, starts)
     torch.cuda.synchronize()
@@ -49,6 +85,8 @@ def bench_sst(args, world, rank, local):
     img = float(sb.file_size.astype(np.float64).sum())
     img_all = sum_over_ranks(world, img)
     nf = len(starts) - 1
+    files_all = sum_over_ranks(world, float(nf))
+    assert int(files_all) == nf_all, "every file built exactly once"
     # algorithmic bytes: keys + values + CSR offsets read once, images written
     alg = float(keys.size + vals.size + 16 * (n + 1)) + img
     achieved = alg / (kern_ms * 1e-3) / 1e9
@@ -63,18 +101,19 @@ def bench_sst(args, world, rank, local):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seed 0x5EED, keys k%015d, splitmix64 values)",
-        "config": {"workload": f"encode {n} records (16 B / 100 B) per GPU into {nf} .sst "
-                               f"(2 MiB flush, bloom m=1.6M k=16)",
-                   "files_per_gpu": nf, "image_bytes_per_gpu": int(img),
-                   "builder_rule_ms": round((tb1 - tb0) * 1e3, 3),
+        "config": {"workload": f"encode one {(args.blocks or 100_000) * 33}-record stream "
+                               f"(16 B / 100 B) into {nf_all} .sst (2 MiB flush, bloom m=1.6M "
+                               f"k=16), whole files dealt round-robin over {world} GPU(s)",
+                   "files_total": nf_all, "files_rank0": nf, "image_bytes_rank0": int(img),
+                   "builder_rule_ms": round(rule_ms, 3),
                    "layout_ms": round((tb2 - tb1) * 1e3, 3),
                    "builder_rule": "lsm_segment_files_host (O(files log n) host search over the "
                                    "CSR offsets), outside the timed region; layout incl. H2D",
-                   "parallelism": f"dp{world} (record ranges per rank, no collective)"},
+                   "parallelism": f"dp{world} (file f -> rank f mod {world}, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "lsm_build_sst: sst_regions_kernel (regions + key hash) -> bloom_or_kernel (filter bits + framing)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -83,6 +122,8 @@ def bench_sst(args, world, rank, local):
                      "kernel_ms_median": round(float(np.median(times)), 5),
                      "kernel_ms_min": round(float(times.min()), 5)},
     }
+    if world > 1:
+        out["roofline"]["aggregate"] = aggregate_roofline(world, alg, kern_ms)
     if not args.no_verify:
         verify_sst(ctx, batch, sb, keys, koff)
     out["config"]["verified"] = False if args.no_verify else ("every image parsed by lsm_decode_sst, V/IDX regions equal to the "

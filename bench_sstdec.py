@@ -244,3 +244,115 @@ def cpu_baseline_may_contain(args, data):
             "sample": f"all {nprobe} probes x {nf} files x {passes} passes on {cpu['threads']} "
                       f"threads in {tn:.1f} s; 1 thread: {min(done, nprobe)} probes in {t1:.1f} s",
             "value_1t": round(min(done, nprobe) / t1 / 1e6, 4), "host": cpu}
+
+
+def bench_level_search(args, world, rank, local):
+    """SURVEY.md §8(f) f3 in the reference's own shape: batched
+    Manager.searchFromLevelWithSparseIndex (manager.go:178-207) up to
+    MayContain -- per probe the one candidate table of the level (sort.Search
+    on MinKey, index--) and its MayContain; 1M probes (half held, half above
+    every range) against the 208 config-3 images as one level."""
+    from bench import sum_over_ranks, timed_region, kernel_times, traffic_from_profile
+    ctx = lsmgpu.Context(local)
+    n = (args.blocks or 100_000) * 33
+    keys, koff, vals, voff = synth.kv_stream(n, first=rank * n)
+    batch = lsmgpu.batch_to_device(ctx, keys, koff, vals, voff)
+    starts = lsmgpu.segment_files(ctx, koff, voff, lsmgpu.MAX_SSTABLE_SIZE)
+    sb = lsmgpu.build_sst(ctx, batch, starts)
+    r = lsmgpu.decode_sst(ctx, sb.out, sb.file_off, sb.file_size)
+    torch.cuda.synchronize()
+    del batch
+    nf = len(starts) - 1
+    nprobe = 1 << 20
+    rng = np.random.default_rng(synth.SEED + rank)
+    held = rng.integers(rank * n, rank * n + n, nprobe // 2)
+    absent = rng.integers(10 ** 12, 10 ** 13, nprobe - nprobe // 2)  # above every range
+    ids = rng.permutation(np.concatenate([held, absent]))
+    pk = synth.keys_for(ids).reshape(-1)
+    pko = np.arange(nprobe + 1, dtype=np.uint64) * np.uint64(synth.KEY_LEN)
+    probes = lsmgpu.batch_to_device(ctx, pk, pko, np.zeros(1, np.uint8),
+                                    np.zeros(nprobe + 1, np.uint64))
+    dev = ctx.torch_device
+    table = torch.empty(nprobe, dtype=torch.int32, device=dev)
+    may = torch.empty(nprobe, dtype=torch.uint8, device=dev)
+    ws = lsmgpu.level_may_contain_workspace(ctx, nf, nprobe)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        lsmgpu.level_may_contain_into(ctx, sb.out, r, probes, table, may, ws=ws, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_region(world, step, args.steps)
+    times, kern_ms = kernel_times(step, stream, args.steps)
+    # the timed output: a held key's candidate is the table holding it, and
+    # it may be there; a key above every range has the last table and no hit
+    t_h, m_h = table.cpu().numpy(), may.cpu().numpy()
+    is_held = ids < 10 ** 12
+    rec = ids[is_held] - rank * n
+    want_t = np.searchsorted(starts[1:].astype(np.int64), rec, side="right")
+    assert np.array_equal(t_h[is_held], want_t), "candidate table"
+    assert (m_h[is_held] == 1).all(), "false negative"
+    assert (t_h[~is_held] == nf - 1).all() and (m_h[~is_held] == 0).all(), "absent keys"
+    total = sum_over_ranks(world, float(nprobe))
+    fbits = r.meta_numpy()["filter_nbits"].astype(np.float64)
+    # algorithmic bytes per launch: 5 B out per probe (table + may), the probe
+    # keys and offsets read once, every stored filter word read once
+    alg = 5.0 * nprobe + pk.size + 8.0 * (nprobe + 1) + float((8 * np.ceil(fbits / 64)).sum())
+    traffic, tsrc = traffic_from_profile(f"level:{nf}:{nprobe}")
+    out = {
+        "metric": "M keys/s searched in one level (candidate table + SSTable.MayContain)",
+        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "unit": "M keys/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: the 208 config-3 images as one level; probes half held, half above "
+                "every range",
+        "verified": "every held probe: candidate = its table, may = 1; every absent probe: "
+                    "the last table, may = 0",
+        "config": {"workload": f"{nprobe} keys x one level of {nf} .sst files per GPU "
+                               "(searchFromLevelWithSparseIndex -> MayContain, bloom m=1.6M k=16)",
+                   "files_per_gpu": nf, "probes_per_gpu": nprobe,
+                   "parallelism": f"dp{world} (probe batches per rank, no collective)"},
+        "roofline": {"bound": "hbm", "kernel": "lsm_level_may_contain (all launches)",
+                     "kernel_ms": round(kern_ms, 5),
+                     "kernel_ms_median": round(float(np.median(times)), 5),
+                     "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1),
+                     "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(alg / (kern_ms * 1e-3) / 1e9 / 8000.0, 4),
+                     "traffic": traffic, "traffic_source": tsrc, "alg_bytes_per_launch": int(alg)},
+    }
+    return out, (sb.out.cpu().numpy(), sb.file_off, r.meta_numpy(), pk, nprobe)
+
+
+def cpu_baseline_level_search(args, data):
+    """The oracle's level search (ora_level_may_contain: Go's sort.Search over
+    the MinKeys, then MayContain of the one candidate) over the same images
+    and probes: 1 thread, and the CPU share's threads over probe chunks."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as ora
+    from bench import host_cpu, timed_threads
+    img, file_off, meta, pk, nprobe = data
+    cpu = host_cpu()
+    nf = len(file_off)
+    metas = (ora.SstMeta * nf).from_buffer_copy(np.ascontiguousarray(meta).tobytes())
+    pko = np.arange(nprobe + 1, dtype=np.uint64) * np.uint64(16)
+    chunk = 16384
+
+    def one(c):
+        ora.level_may_contain(img, file_off, metas, pk, pko, c, min(nprobe, c + chunk))
+
+    t1, done = 0.0, 0
+    while (t1 < args.cpu_seconds / 3 or done == 0) and done < nprobe:
+        t0 = time.perf_counter()
+        one(done)
+        t1 += time.perf_counter() - t0
+        done += chunk
+    sample = list(range(0, nprobe, chunk))
+    passes, tn = timed_threads(one, sample, cpu["threads"], args.cpu_seconds)
+    return {"value": round(nprobe * passes / tn / 1e6, 4), "unit": "M keys/s",
+            "cores": cpu["threads"], "kind": "port",
+            "sample": f"all {nprobe} probes x {passes} passes on {cpu['threads']} threads in "
+                      f"{tn:.1f} s; 1 thread: {min(done, nprobe)} probes in {t1:.1f} s",
+            "value_1t": round(min(done, nprobe) / t1 / 1e6, 4), "host": cpu}

@@ -106,3 +106,21 @@ def test_world_mismatch_is_refused():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"],
                        capture_output=True, env=env, cwd=ROOT, timeout=120)
     assert p.returncode != 0 and b"WORLD_SIZE=2" in p.stderr
+
+
+def test_launcher_gpus2_deals_sst_files_exactly():
+    """`bench.py --config sst --gpus N`: config 3's stream is cut into .sst
+    files by the builder rule and whole files are dealt round-robin (file f ->
+    rank f mod N): every file exactly once, every record in
+    exactly one rank's batch."""
+    # 2,000 blocks x 33 records = 66,000 records of 132 B EstimateSize -> 5 files
+    j, _ = _bench_dry("--config", "sst", "--gpus", "2", "--blocks", "2000")
+    nf = j["global_blocks"]
+    assert nf == 5 and j["scaling"] == "strong"
+    assert j["blocks_per_rank"] == [3, 2]
+    assert j["id_sum"] == nf * (nf - 1) // 2 and j["id_sumsq"] == float(sum(f * f for f in range(nf)))
+    assert sum(j["records_per_rank"]) == 66_000
+    last = 66_000 - 4 * 15888                                       # file 4: the partial one
+    assert j["records_per_rank"] == [2 * 15888 + last, 2 * 15888]   # files 0, 2, 4 | 1, 3
+    j, _ = _bench_dry("--config", "sst", "--gpus", "3", "--blocks", "2000")
+    assert j["blocks_per_rank"] == [2, 2, 1] and sum(j["records_per_rank"]) == 66_000
