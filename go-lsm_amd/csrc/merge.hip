@@ -1099,35 +1099,55 @@ uint32_t grid_for(uint64_t n) { return (uint32_t)((n + kMergeThreads - 1) / kMer
 // order merge.go:47-66 pops in, equal keys included.  Entries carry
 // rank << 32 | index, so one load serves the compare and the move.  One host
 // thread: the heap's history is one dependent chain.
+//
+// Pop's down() is run bottom-up (Floyd): the hole left by the root goes down
+// the path of smaller children -- the left one on ties, as down() picks --
+// branch-free, to a leaf, and then the moved element rises while its parent's
+// rank is >= its own.  down() moves up exactly the path elements whose rank
+// is < the element's (it stops at the first child that is not less), and the
+// path's ranks never decrease, so the rise puts back exactly the others: the
+// same array as down() leaves, after every pop.  down()'s child choice is an
+// unpredictable branch per level; here the descent has none, and it prefetches
+// three and four levels ahead (a 64-byte block each).
 void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order) {
     std::vector<uint64_t> h(n ? n : 1);
+    uint64_t *H = h.data();
     for (uint32_t i = 0; i < n; i++) {  // Push: append, up(h, i)
         const uint64_t x = (uint64_t)rank[i] << 32 | i;
         uint32_t j = i;
         while (j > 0) {
             const uint32_t p = (j - 1) / 2;
-            if (!((x >> 32) < (h[p] >> 32))) break;
-            h[j] = h[p];
+            if (!((x >> 32) < (H[p] >> 32))) break;
+            H[j] = H[p];
             j = p;
         }
-        h[j] = x;
+        H[j] = x;
     }
     for (uint32_t r = n; r > 0; r--) {  // Pop: swap(0, r-1), down(0, r-1)
-        const uint64_t top = h[0], x = h[r - 1];
-        const uint32_t m = r - 1;
+        const uint64_t top = H[0], x = H[r - 1];
+        const uint32_t m = r - 1, xr = (uint32_t)(x >> 32);
         uint32_t i = 0;
-        for (;;) {
+        while (2 * i + 2 < m) {  // both children in the heap
             const uint32_t j1 = 2 * i + 1;
-            if (j1 >= m) break;
-            __builtin_prefetch(&h[4 * (uint64_t)i + 3]);  // the grandchildren's line
-            uint32_t j = j1;
-            if (j1 + 1 < m && (h[j1 + 1] >> 32) < (h[j1] >> 32)) j = j1 + 1;
-            if (!((h[j] >> 32) < (x >> 32))) break;
-            h[i] = h[j];
+            __builtin_prefetch(&H[8 * (uint64_t)i + 7]);
+            __builtin_prefetch(&H[16 * (uint64_t)i + 15]);
+            const uint64_t a = H[j1], b = H[j1 + 1];
+            const uint32_t j = j1 + (uint32_t)((b >> 32) < (a >> 32));  // the right one only if less
+            H[i] = H[j];
             i = j;
         }
-        if (m) h[i] = x;
-        h[m] = top;
+        if (2 * i + 1 < m) {  // a left child only
+            H[i] = H[2 * i + 1];
+            i = 2 * i + 1;
+        }
+        while (i > 0) {  // back up past every path element whose rank is >= x's
+            const uint32_t p = (i - 1) / 2;
+            if ((uint32_t)(H[p] >> 32) < xr) break;
+            H[i] = H[p];
+            i = p;
+        }
+        if (m) H[i] = x;
+        H[m] = top;
         order[n - r] = (uint32_t)top;
     }
 }
