@@ -1449,24 +1449,6 @@ struct WalArgs {
     u32x4 *scratch;   // nwal * segs * 2 * kWalSegSlots
 };
 
-// Scratch of segment g = w * segs + s (32 * kWalSegSlots bytes): the two
-// phases' records packed to 8 bytes (wal_pack) in its first half, and, for a
-// segment the stitch has to chase again (neither guess on the chain), full
-// descriptors in its second half; fin marks which (count | phase << 31 |
-// full << 30).
-__device__ __forceinline__ uint64_t *wal_cscratch(const WalArgs &a, uint64_t q) {  // q = 2 g + phase
-    return reinterpret_cast<uint64_t *>(a.scratch) + (q >> 1) * 4 * kWalSegSlots + (q & 1) * kWalSegSlots;
-}
-__device__ __forceinline__ u32x4 *wal_fscratch(const WalArgs &a, uint64_t g) {
-    return a.scratch + (g * 2 + 1) * kWalSegSlots;
-}
-constexpr uint32_t kWalVEsc = (1u << 28) - 1;  // value length re-read from the log
-// record starting rel bytes into its segment (< 2^15), key length (<= 2^20
-// by kv.go:84) and value length (< 2^28, else the escape)
-__device__ __forceinline__ uint64_t wal_pack(uint32_t rel, uint32_t kl, uint32_t vl) {
-    return (uint64_t)rel | (uint64_t)kl << 15 | (uint64_t)(vl < kWalVEsc ? vl : kWalVEsc) << 36;
-}
-
 __device__ __forceinline__ void wal_slots(const WalArgs &a, uint32_t w, uint64_t &base,
                                           uint64_t &cap) {
     if (a.out.rec_base) {
@@ -1663,39 +1645,19 @@ struct WalLog {
     }
 };
 
-// Two waves per segment, sharing one LDS copy of it (twice the waves per
-// CU for the same LDS): the segment is cut into 128 shares, a thread each,
-// whose chains (both field phases) do not depend on the segment's entry; the
-// shares' results go to an LDS table, then wave 0 stitches and writes phase
-// 0 (from g) while wave 1 does phase 1 (from g read as a value length).  In
-// the stitch a lane takes two consecutive shares.
-constexpr uint32_t kWalShares = 2 * kWave;
-constexpr uint32_t kWalNone = 0xFFFFFFFFu;
-
-// a share's choice of chain (0: its phase-0 guess, 1: its phase-1 guess,
-// 2: neither) as a function of the previous share's: h = f(0) | f(1) << 4
-__device__ __forceinline__ uint32_t wal_apply(uint32_t h, uint32_t c) {
-    return c == 2 ? 2u : c == 0 ? (h & 15) : (h >> 4);
-}
-__device__ __forceinline__ uint32_t wal_compose(uint32_t outer, uint32_t inner) {  // outer o inner
-    return wal_apply(outer, inner & 15) | wal_apply(outer, inner >> 4) << 4;
-}
-
-__global__ __launch_bounds__(2 * kWave) void wal_seg_lanes_kernel(WalArgs a) {
+// One wave serves both phases of a segment: the shares' chains do not depend
+// on the segment's entry, only lane 0's does, so they are chased once and
+// stitched twice (from g and from g read as a value length).
+__global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
     constexpr uint32_t STAGE = kWalStage;
     __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 4];
-    __shared__ uint32_t t_e0[kWalShares], t_e1[kWalShares], t_x0[kWalShares], t_x1[kWalShares];
-    __shared__ uint32_t t_c[kWalShares];     // c0 | c1 << 16 (records starting in a share <= 2,049)
-    __shared__ uint8_t t_st[2][kWalShares];  // statuses
-    __shared__ uint32_t s_g[2];
-    const uint32_t s = blockIdx.x, w = blockIdx.y, tid = threadIdx.x, lane = lane_id();
-    const uint32_t wave = tid / kWave;
-    const uint32_t len = a.wal_len[w];
-    const uint64_t off = a.wal_off[w];
+    const uint32_t s = blockIdx.x, w = blockIdx.y, lane = lane_id();
+    const uint32_t len = uni(a.wal_len[w]);
+    const uint64_t off = uni64(a.wal_off[w]);
     const uint64_t q0 = ((uint64_t)w * a.segs + s) * 2;
     const uint32_t start = s * kWalSeg;
     if (start >= len || len > a.max_len) {
-        if (tid == 0) a.seg[q0] = a.seg[q0 + 1] = WalSeg{kWalNone, kWalNone, 0, 0};
+        if (lane == 0) a.seg[q0] = a.seg[q0 + 1] = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
         return;
     }
     WalLog L;
@@ -1706,209 +1668,196 @@ __global__ __launch_bounds__(2 * kWave) void wal_seg_lanes_kernel(WalArgs a) {
     L.s0 = (L.h + start) & ~15u;
     L.sz = STAGE;
     L.lds = stage;
-    // the segment + a tail, 16 bytes per thread per step (all loads in flight)
-    for (uint32_t c = tid; c < STAGE / 16; c += kWalShares)
-        *reinterpret_cast<u32x4 *>(&stage[4 * c]) = ld_b128(L.r, L.s0 + 16 * c);
-    __syncthreads();
-    if (wave == 0) {
-        uint32_t g = start, g1 = kWalNone;  // entries of phase 0 and phase 1
-        if (s > 0) {  // the segment's guess: the first plausible start in its first 2 KiB
-            g = kWalNone;
-            const uint32_t span = len - start < 2048 ? len - start : 2048;
-            for (uint32_t t0 = 0; t0 < span && g == kWalNone; t0 += kWave) {
-                const uint32_t p = start + t0 + lane;
-                const uint64_t m = __ballot(t0 + lane < span && L.plausible(p));
-                if (m) g = start + t0 + (uint32_t)__builtin_ctzll(m);
-            }
-            if (g == kWalNone) g = start;
-            g = uni(g);
-            const uint32_t v = (uint64_t)g + 4 <= len ? L.rd32(g) : kWalNone;
-            g1 = uni((uint64_t)g + 4 + v <= len ? g + 4 + v : len);
+    {
+        // the segment + a tail (the loads are already all in flight: staging
+        // by buffer_load ... lds measured no faster)
+        for (uint32_t c = 0; c < STAGE / 16; c += kWave) {
+            const uint32_t o = L.s0 + 16 * (c + lane);
+            if (c + lane < STAGE / 16)
+                *reinterpret_cast<u32x4 *>(&stage[4 * (c + lane)]) = ld_b128(L.r, o);
         }
-        if (lane == 0) {
-            s_g[0] = g;
-            s_g[1] = g1;
+        __syncthreads();
+    }
+    uint32_t g = start, g1 = 0xFFFFFFFFu;  // entries of phase 0 and phase 1
+    if (s > 0) {  // the segment's guess: the first plausible start in its first 2 KiB
+        g = 0xFFFFFFFFu;
+        const uint32_t span = len - start < 2048 ? len - start : 2048;
+        for (uint32_t t0 = 0; t0 < span && g == 0xFFFFFFFFu; t0 += kWave) {
+            const uint32_t p = start + t0 + lane;
+            const uint64_t m = __ballot(t0 + lane < span && L.plausible(p));
+            if (m) g = start + t0 + (uint32_t)__builtin_ctzll(m);
         }
+        if (g == 0xFFFFFFFFu) g = start;
+        g = uni(g);
+        const uint32_t v = (uint64_t)g + 4 <= len ? L.rd32(g) : 0xFFFFFFFFu;
+        g1 = uni((uint64_t)g + 4 + v <= len ? g + 4 + v : len);
     }
     const uint32_t E = start + kWalSeg < len ? start + kWalSeg : len;
-    // 1. shares of [start, E), a thread each.  A share width of a multiple of
-    //    128 B would start every lane on the same LDS bank; widths of 4 mod 8
-    //    dwords spread them.
-    uint32_t W = (E - start + kWalShares - 1) / kWalShares;
+    // 1. shares of [start, E): lane 0's chains are the two entries themselves.
+    //    A share width of a multiple of 128 B would start every lane on the
+    //    same LDS bank; widths of 4 mod 8 dwords spread them.
+    uint32_t W = (E - start + kWave - 1) / kWave;
     W = (W + 3) & ~3u;
     if ((W / 4) % 8 != 4) W += 4 * ((12 - (W / 4) % 8) % 8);
-    auto share_lo = [&](uint32_t j) { return start + j * W < E ? start + j * W : E; };
-    auto share_hi = [&](uint32_t j) {
-        const uint32_t lo = share_lo(j);
-        return lo + W < E ? lo + W : E;
-    };
-    {
-        const uint32_t ss = share_lo(tid), se = share_hi(tid);
-        uint32_t e0 = kWalNone, e1 = kWalNone, c0 = 0, c1 = 0, x0 = 0, x1 = 0;
-        int32_t st0 = LSM_OK, st1 = LSM_OK;
-        if (tid > 0 && ss < se) {
-            e0 = L.first_plausible(ss, se);
-            if (e0 != kWalNone && (uint64_t)e0 + 4 <= len) {
-                const uint32_t v = L.rd32(e0);
-                if ((uint64_t)e0 + 4 + v <= len) e1 = e0 + 4 + v;
-            }
+    const uint32_t ss = start + lane * W < E ? start + lane * W : E;
+    const uint32_t se = ss + W < E ? ss + W : E;
+    uint32_t e0 = 0xFFFFFFFFu, e1 = 0xFFFFFFFFu, c0 = 0, c1 = 0, x0 = 0, x1 = 0;
+    int32_t st0 = LSM_OK, st1 = LSM_OK;
+    if (lane > 0 && ss < se) {
+        e0 = L.first_plausible(ss, se);
+        if (e0 != 0xFFFFFFFFu && (uint64_t)e0 + 4 <= len) {
+            const uint32_t v = L.rd32(e0);
+            if ((uint64_t)e0 + 4 + v <= len) e1 = e0 + 4 + v;
         }
-        // A guess at or past the share's end is a chain with no records that
-        // passes its position through (exit = the guess); chase() returns
-        // exactly that.  Both guesses' chains at once; a missing guess is a
-        // stopped chain (its count, exit and status keep their initial values).
+    }
+    // A guess at or past the share's end is a chain with no records that
+    // passes its position through (exit = the guess); chase() returns exactly
+    // that.  Leaving its exit unset once made a share holding only a value
+    // field report exit 0 when the previous chain ended on that guess.
+    {
+        // both guesses' chains at once; a missing guess is a stopped chain
+        // (its count, exit and status keep their initial values)
         uint32_t ca, xa, cb, xb;
         int32_t sa, sb;
-        L.chase2(e0 != kWalNone ? e0 : se, e1 != kWalNone ? e1 : se, se, start, ca, xa, sa, cb, xb,
-                 sb);
-        if (e0 != kWalNone) { c0 = ca; x0 = xa; st0 = sa; }
-        if (e1 != kWalNone) { c1 = cb; x1 = xb; st1 = sb; }
-        t_e0[tid] = e0;
-        t_e1[tid] = e1;
-        t_x0[tid] = x0;
-        t_x1[tid] = x1;
-        t_c[tid] = c0 | c1 << 16;
-        t_st[0][tid] = (uint8_t)st0;
-        t_st[1][tid] = (uint8_t)st1;
+        L.chase2(e0 != 0xFFFFFFFFu ? e0 : se, e1 != 0xFFFFFFFFu ? e1 : se, se, start, ca, xa, sa, cb,
+                 xb, sb);
+        if (e0 != 0xFFFFFFFFu) { c0 = ca; x0 = xa; st0 = sa; }
+        if (e1 != 0xFFFFFFFFu) { c1 = cb; x1 = xb; st1 = sb; }
     }
-    __syncthreads();
-    // 2. + 3. wave ph: stitch phase ph from its entry, then write its chains
-    const uint32_t ph = wave;
-    const uint64_t q = q0 + ph;
-    if (ph == 1 && s == 0) {  // segment 0 starts at 0: no phase 1
-        if (lane == 0) a.seg[q] = WalSeg{kWalNone, kWalNone, 0, 0};
-        return;
-    }
-    const uint32_t gp = s_g[ph];
-    if (gp >= E) {
-        if (lane == 0) a.seg[q] = WalSeg{gp, gp, 0, 0};
-        return;
-    }
-    const uint32_t ja = 2 * lane, jb = 2 * lane + 1;  // this lane's shares
-    uint32_t acc_e[2] = {kWalNone, kWalNone}, acc_c[2] = {0, 0};
-    uint32_t e = gp, total = 0;
-    int32_t status = LSM_OK;
-    bool fast = false;
-    {
+    // 2. + 3. per phase: stitch from the entry, then write the accepted chains
+    for (uint32_t ph = 0; ph < 2; ph++) {
+        const uint64_t q = q0 + ph;
+        const uint32_t gp = ph ? g1 : g;
+        if (ph == 1 && s == 0) {  // segment 0 starts at 0
+            if (lane == 0) a.seg[q] = WalSeg{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+            break;
+        }
+        if (gp >= E) {
+            if (lane == 0) a.seg[q] = WalSeg{gp, gp, 0, 0};
+            continue;
+        }
+        uint32_t e = gp, acc_entry = 0xFFFFFFFFu, acc_cnt = 0, total = 0;
+        int32_t status = LSM_OK;
+        bool dead = false;
         // fast stitch: the share k holding the entry is chased exactly; after
-        // it, share j's choice of chain is a function of share j-1's (its
-        // chain's exit matched against share j's guesses); a 6-step scan of
-        // the lanes' two-share maps composes them.  Any miss (a wrong guess,
-        // or a record longer than a share) falls back to the serial stitch.
-        const uint32_t k = (gp - start) / W;
-        const uint32_t lst = (E - 1 - start) / W < kWalShares - 1 ? (E - 1 - start) / W : kWalShares - 1;
-        uint32_t ck, xk;
-        int32_t stk;
-        L.chase(gp, share_hi(k), ck, xk, stk);
-        ck = uni(ck);
-        xk = uni(xk);
-        stk = (int32_t)uni((uint32_t)stk);
-        auto map_of = [&](uint32_t j) -> uint32_t {
-            const uint32_t f0 = t_e0[j], f1 = t_e1[j];
+        // it, lane l's choice of chain (0: from e0, 1: from e1) is a function
+        // of lane l-1's choice (its chain's exit matched against lane l's
+        // entries); a 6-step scan composes these maps across the lanes.  Any
+        // miss (a wrong guess, or a record longer than a share) falls back to
+        // the serial stitch below.
+        bool fast = false;
+        {
+            const uint32_t k = (gp - start) / W;
+            const uint32_t last = (E - 1 - start) / W < kWave - 1 ? (E - 1 - start) / W : kWave - 1;
+            const uint32_t sek = uni(__builtin_amdgcn_readlane(se, k));
+            uint32_t ck, xk;
+            int32_t stk;
+            L.chase(gp, sek, ck, xk, stk);
+            ck = uni(ck);
+            xk = uni(xk);
+            stk = (int32_t)uni((uint32_t)stk);
             auto match = [&](uint32_t x) -> uint32_t {
-                return (f0 != kWalNone && x == f0) ? 0u : (f1 != kWalNone && x == f1) ? 1u : 2u;
+                return (e0 != 0xFFFFFFFFu && x == e0) ? 0u : (e1 != 0xFFFFFFFFu && x == e1) ? 1u : 2u;
             };
-            if (j <= k) return 0u | 1u << 4;  // identity (never used: share k+1's map is constant)
-            if (j == k + 1) {
+            // map from lane l-1's choice to lane l's, as h0 | h1 << 4 (2 = miss)
+            const uint32_t xp0 = __shfl_up(x0, 1), xp1 = __shfl_up(x1, 1);
+            const uint32_t ep0 = __shfl_up(e0, 1), ep1 = __shfl_up(e1, 1);
+            uint32_t h;
+            if (lane <= k) {
+                h = 0u | 1u << 4;  // identity (never used: lane k+1's map is constant)
+            } else if (lane == k + 1) {
                 const uint32_t c = match(xk);
-                return c | c << 4;
+                h = c | c << 4;
+            } else {
+                const uint32_t m0 = ep0 != 0xFFFFFFFFu ? match(xp0) : 2u;
+                const uint32_t m1 = ep1 != 0xFFFFFFFFu ? match(xp1) : 2u;
+                h = m0 | m1 << 4;
             }
-            const uint32_t m0 = t_e0[j - 1] != kWalNone ? match(t_x0[j - 1]) : 2u;
-            const uint32_t m1 = t_e1[j - 1] != kWalNone ? match(t_x1[j - 1]) : 2u;
-            return m0 | m1 << 4;
-        };
-        const uint32_t ha = map_of(ja), hb = map_of(jb);
-        uint32_t H = wal_compose(hb, ha);
 #pragma unroll
-        for (uint32_t d = 1; d < kWave; d <<= 1) {
-            const uint32_t pv = __shfl_up(H, d);
-            if (lane >= d) H = wal_compose(H, pv);
-        }
-        uint32_t Hp = __shfl_up(H, 1);
-        if (lane == 0) Hp = 0u | 1u << 4;
-        const uint32_t ch[2] = {wal_apply(ha, Hp & 15), H & 15};
-        const uint32_t js[2] = {ja, jb};
-        bool live[2], err[2], miss[2];
-        int32_t cst[2];
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            live[i] = js[i] > k && js[i] <= lst;
-            cst[i] = (int32_t)t_st[ch[i] == 0 ? 0 : 1][js[i]];
-            err[i] = live[i] && ch[i] < 2 && cst[i] != LSM_OK;
-        }
-        const uint64_t ea = __ballot(err[0]), eb = __ballot(err[1]);
-        const uint32_t fa = ea ? 2 * (uint32_t)__builtin_ctzll(ea) : kWalNone;
-        const uint32_t fb = eb ? 2 * (uint32_t)__builtin_ctzll(eb) + 1 : kWalNone;
-        const uint32_t first_err = fa < fb ? fa : fb;
-        const uint32_t lim = stk != LSM_OK ? k : first_err != kWalNone ? first_err : lst;
-#pragma unroll
-        for (int i = 0; i < 2; i++) miss[i] = live[i] && ch[i] == 2 && js[i] <= lim;
-        if (!__ballot(miss[0] || miss[1])) {
-            fast = true;
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-                if (js[i] == k) {
-                    acc_e[i] = gp;
-                    acc_c[i] = ck;
-                } else if (live[i] && js[i] <= lim) {
-                    acc_e[i] = ch[i] == 0 ? t_e0[js[i]] : t_e1[js[i]];
-                    acc_c[i] = ch[i] == 0 ? (t_c[js[i]] & 0xFFFFu) : (t_c[js[i]] >> 16);
+            for (uint32_t d = 1; d < kWave; d <<= 1) {
+                const uint32_t pv = __shfl_up(h, d);
+                if (lane >= d) {  // h := h o pv
+                    const uint32_t p0 = pv & 15, p1 = pv >> 4;
+                    const uint32_t n0 = p0 == 2 ? 2u : p0 == 0 ? (h & 15) : (h >> 4);
+                    const uint32_t n1 = p1 == 2 ? 2u : p1 == 0 ? (h & 15) : (h >> 4);
+                    h = n0 | n1 << 4;
                 }
             }
-            if (lim == k) {
-                e = xk;
-                status = stk;
-            } else {
-                const uint32_t cl = uni(__builtin_amdgcn_readlane((int)ch[lim & 1], (int)(lim >> 1)));
-                e = cl == 0 ? t_x0[lim] : t_x1[lim];
-                status = first_err != kWalNone ? (int32_t)t_st[cl == 0 ? 0 : 1][lim] : LSM_OK;
+            const uint32_t ch = h & 15;  // lanes k+1 .. last: the chosen chain
+            const bool live = lane > k && lane <= last;
+            const int32_t cst = ch == 0 ? st0 : st1;
+            const uint64_t errm = __ballot(live && ch < 2 && cst != LSM_OK);
+            const uint32_t lim = stk != LSM_OK ? k : errm ? (uint32_t)__builtin_ctzll(errm) : last;
+            const uint64_t below = lim >= kWave - 1 ? ~0ull : (2ull << lim) - 1;  // lanes <= lim
+            const uint64_t missm = __ballot(live && ch == 2) & below;
+            if (!missm) {
+                fast = true;
+                if (lane == k) {
+                    acc_entry = gp;
+                    acc_cnt = ck;
+                } else if (live && lane <= lim) {
+                    acc_entry = ch == 0 ? e0 : e1;
+                    acc_cnt = ch == 0 ? c0 : c1;
+                }
+                const uint32_t xe = ch == 0 ? x0 : x1;
+                if (lim == k) {
+                    e = xk;
+                    status = stk;
+                } else {
+                    e = uni(__builtin_amdgcn_readlane(xe, lim));
+                    status = errm ? (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)cst, lim)) : LSM_OK;
+                }
+                uint32_t t;
+                wave_excl_scan(acc_cnt, &t);
+                total = t;
             }
         }
-    }
-    for (uint32_t l = 0; !fast && l < kWalShares; l++) {  // serial stitch
-        const uint32_t sl = share_lo(l), el = share_hi(l);
-        if (status != LSM_OK || sl >= el || e >= el) continue;
-        uint32_t cnt, ex;
-        int32_t st;
-        if (l > 0 && t_e0[l] == e) {
-            cnt = t_c[l] & 0xFFFFu;
-            ex = t_x0[l];
-            st = (int32_t)t_st[0][l];
-        } else if (l > 0 && t_e1[l] == e) {
-            cnt = t_c[l] >> 16;
-            ex = t_x1[l];
-            st = (int32_t)t_st[1][l];
-        } else {  // the entry share, or neither guess on the chain: chase from e
-            L.chase(e, el, cnt, ex, st);
-            cnt = uni(cnt);
-            ex = uni(ex);
-            st = (int32_t)uni((uint32_t)st);
+        for (uint32_t l = 0; !fast && l < kWave; l++) {
+            const uint32_t sl = uni(__builtin_amdgcn_readlane(ss, l));
+            const uint32_t el = uni(__builtin_amdgcn_readlane(se, l));
+            if (dead || sl >= el || e >= el) continue;
+            uint32_t cnt, ex;
+            int32_t st;
+            if (l > 0 && uni(__builtin_amdgcn_readlane(e0, l)) == e) {
+                cnt = uni(__builtin_amdgcn_readlane(c0, l));
+                ex = uni(__builtin_amdgcn_readlane(x0, l));
+                st = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)st0, l));
+            } else if (l > 0 && uni(__builtin_amdgcn_readlane(e1, l)) == e) {
+                cnt = uni(__builtin_amdgcn_readlane(c1, l));
+                ex = uni(__builtin_amdgcn_readlane(x1, l));
+                st = (int32_t)uni(__builtin_amdgcn_readlane((uint32_t)st1, l));
+            } else {  // the entry share, or neither guess on the chain: chase from e
+                L.chase(e, el, cnt, ex, st);
+                cnt = uni(cnt);
+                ex = uni(ex);
+                st = (int32_t)uni((uint32_t)st);
+            }
+            if (lane == l) {
+                acc_entry = e;
+                acc_cnt = cnt;
+            }
+            total += cnt;
+            e = ex;
+            if (st != LSM_OK) {
+                status = st;
+                dead = true;
+            }
         }
-        if (lane == (l >> 1)) {
-            acc_e[l & 1] = e;
-            acc_c[l & 1] = cnt;
+        uint32_t tot;
+        const uint32_t pre = wave_excl_scan(acc_cnt, &tot);
+        if (acc_cnt) {
+            u32x4 *dst = a.scratch + q * kWalSegSlots + pre;
+            uint32_t p = acc_entry;
+            for (uint32_t i = 0; i < acc_cnt; i++) {
+                uint32_t kl = 0, vl = 0;
+                L.record(p, kl, vl);
+                const uint64_t ro = off + p;
+                dst[i] = u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), kl, vl};
+                p += 8 + kl + vl;
+            }
         }
-        e = ex;
-        if (st != LSM_OK) status = st;
+        if (lane == 0) a.seg[q] = WalSeg{gp, e, total, status};
     }
-    uint32_t tot;
-    const uint32_t pre = wave_excl_scan(acc_c[0] + acc_c[1], &tot);
-    total = tot;
-    // 8-byte scratch records (wal_pack): half the bytes of a descriptor, for
-    // the phase wal_compact_kernel may not keep
-    uint64_t *dst = wal_cscratch(a, q) + pre;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        uint32_t p = acc_e[i];
-        for (uint32_t r = 0; r < acc_c[i]; r++) {
-            uint32_t kl = 0, vl = 0;
-            L.record(p, kl, vl);
-            dst[r] = wal_pack(p - start, kl, vl);
-            p += 8 + kl + vl;
-        }
-        dst += acc_c[i];
-    }
-    if (lane == 0) a.seg[q] = WalSeg{gp, e, total, status};
 }
 
 __global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
@@ -2025,12 +1974,11 @@ __global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
                     nr = 0;
                     st = LSM_OK;
                     decode_range_any<LSM_GRAMMAR_KV, 8>(
-                        d, ring, off + e, len - e,
-                        (uint64_t)(wal_fscratch(a, (uint64_t)w * a.segs + s) - a.scratch),
+                        d, ring, off + e, len - e, ((uint64_t)w * a.segs + s) * 2 * kWalSegSlots,
                         kWalSegSlots, nr, st, stop, &endp);
                     ex = e + endp;
                 }
-                cnt = nr | (ph == 1 ? 0x80000000u : ph == 2 ? 0x40000000u : 0u);
+                cnt = nr | (ph == 1 ? 0x80000000u : 0u);
                 total += nr;
                 e = ex;
                 if (st != LSM_OK) {
@@ -2064,34 +2012,15 @@ __global__ __launch_bounds__(256) void wal_compact_kernel(WalArgs a) {
     const uint32_t s = blockIdx.x, w = blockIdx.y;
     const uint64_t q = (uint64_t)w * a.segs + s;
     const uint32_t pre = a.fin[2 * q], cf = a.fin[2 * q + 1];
-    const uint32_t cnt = cf & 0x3FFFFFFFu;
+    const uint32_t cnt = cf & 0x7FFFFFFFu;
     if (cnt == 0) return;
     uint64_t base, cap;
     wal_slots(a, w, base, cap);
     u32x4 *dst = reinterpret_cast<u32x4 *>(a.out.desc);
-    if (cf & 0x40000000u) {  // re-chased by the stitch: full descriptors
-        const u32x4 *src = wal_fscratch(a, q);
-        for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
-            if ((uint64_t)pre + j < cap)
-                __builtin_nontemporal_store(src[j], &dst[base + pre + j]);
-        return;
-    }
-    const uint64_t *src = wal_cscratch(a, 2 * q + (cf >> 31));
-    const uint64_t seg0 = a.wal_off[w] + (uint64_t)s * kWalSeg;
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-        if ((uint64_t)pre + j >= cap) continue;
-        const uint64_t x = src[j];
-        const uint64_t ro = seg0 + (x & 0x7FFF);
-        const uint32_t kl = (uint32_t)(x >> 15) & 0x1FFFFFu;
-        uint32_t vl = (uint32_t)(x >> 36);
-        if (vl == kWalVEsc) {  // a value of 2^28 bytes or more: its length from the log
-            const uint8_t *vp = a.wal + ro + 4 + kl;
-            vl = (uint32_t)vp[0] | (uint32_t)vp[1] << 8 | (uint32_t)vp[2] << 16 | (uint32_t)vp[3] << 24;
-        }
-        // nt: written once (A/B: 997 -> 1,017 GiB/s)
-        __builtin_nontemporal_store(u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), kl, vl},
-                                    &dst[base + pre + j]);
-    }
+    const u32x4 *src = a.scratch + (q * 2 + (cf >> 31)) * kWalSegSlots;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
+        if ((uint64_t)pre + j < cap)  // nt: written once (A/B: 997 -> 1,017 GiB/s)
+            __builtin_nontemporal_store(src[j], &dst[base + pre + j]);
 }
 
 }  // namespace
@@ -2355,7 +2284,7 @@ extern "C" int lsm_wal_replay(lsm_ctx *ctx, const uint8_t *d_wal, const uint64_t
     a.seg = reinterpret_cast<WalSeg *>(ws + n * 2 * kWalSegSlots * 16);
     a.fin = reinterpret_cast<uint32_t *>(ws + n * 2 * (kWalSegSlots * 16 + sizeof(WalSeg)));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(wal_seg_lanes_kernel, dim3(a.segs, nwal), dim3(kWalShares), 0, s, a);
+    hipLaunchKernelGGL(wal_seg_lanes_kernel, dim3(a.segs, nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_stitch_kernel, dim3(nwal), dim3(kWave), 0, s, a);
     hipLaunchKernelGGL(wal_compact_kernel, dim3(a.segs, nwal), dim3(256), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());

@@ -176,15 +176,38 @@ __global__ __launch_bounds__(kMergeThreads) void merge_stats_kernel(MergeIn m, u
         s[1] = v.kl < s[1] ? v.kl : s[1];
         s[2] |= v.kl;
         s[3] &= v.kl;
+        uint64_t ch[kFastChunks];
 #pragma unroll
         for (uint32_t d = 0; d < kFastChunks; d++) {
+            ch[d] = v.kl > 8 * d ? key_chunk(m.bytes + v.ko, v.kl, d) : 0;
             if (v.kl > 8 * d) {
-                const uint64_t c = key_chunk(m.bytes + v.ko, v.kl, d);
-                s[4 + 2 * d] |= c;
-                s[5 + 2 * d] &= c;
+                s[4 + 2 * d] |= ch[d];
+                s[5 + 2 * d] &= ch[d];
             }
         }
-        if (i > 0 && key_cmp(m.bytes, v, view(m, i - 1)) < 0) {  // a descent: a run starts at i
+        // the predecessor's first 32 bytes from the lane below (its key was
+        // loaded there; lane 0 loads it): the descent test compares chunks,
+        // and the whole keys only when those tie and a key is longer
+        uint64_t pc[kFastChunks];
+        uint32_t pkl = __shfl_up(v.kl, 1);
+#pragma unroll
+        for (uint32_t d = 0; d < kFastChunks; d++) pc[d] = __shfl_up(ch[d], 1);
+        if (lane_id() == 0 && i > 0) {
+            const View u = view(m, i - 1);
+            pkl = u.kl;
+#pragma unroll
+            for (uint32_t d = 0; d < kFastChunks; d++)
+                pc[d] = u.kl > 8 * d ? key_chunk(m.bytes + u.ko, u.kl, d) : 0;
+        }
+        int cmp = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < kFastChunks; d++)
+            if (cmp == 0 && ch[d] != pc[d]) cmp = ch[d] < pc[d] ? -1 : 1;
+        if (cmp == 0 && i > 0) {
+            if (v.kl <= 8 * kFastChunks && pkl <= 8 * kFastChunks) cmp = v.kl < pkl ? -1 : v.kl > pkl ? 1 : 0;
+            else cmp = key_cmp(m.bytes, v, view(m, i - 1));
+        }
+        if (i > 0 && cmp < 0) {  // a descent: a run starts at i
             atomicMin(&s_first, i);
             atomicMax(&s_last, i);
             const uint32_t at = atomicAdd(&s_cnt, 1u);
@@ -412,17 +435,24 @@ __device__ __forceinline__ bool is_tombstone(const uint8_t *b, const View &v) {
 // dropped at level 6); csize[j] = the pair's EstimateSize (16 + key + value,
 // kv.go:118-121), which merge_candidate_kernel keeps or zeroes in place (the
 // view is loaded here anyway: no second gather through perm)
+//
+// xinfo[j] = perm[j] | writable << 32 | min(EstimateSize, 2^24 - 1) << 40:
+// what merge_scan_apply needs of a file's extra (usually the pair right after
+// a candidate) in one load.
 __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, const uint32_t *perm,
                                                                     int level, uint8_t *flags,
-                                                                    uint32_t *csize) {
+                                                                    uint32_t *csize, uint64_t *xinfo) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j >= m.n) return;
-    const View v = view(m, perm[j]);
+    const uint32_t pj = perm[j];
+    const View v = view(m, pj);
     bool gs = j == 0 || v.kl == 0;
     if (!gs) gs = !keys_equal(m.bytes, v, view(m, perm[j - 1]));
     const bool wr = level < 6 || !is_tombstone(m.bytes, v);
     flags[j] = (uint8_t)((gs ? 1 : 0) | (wr ? 2 : 0));
-    csize[j] = 16 + v.kl + v.vl;
+    const uint64_t sz = 16 + (uint64_t)v.kl + v.vl;
+    csize[j] = (uint32_t)sz;
+    xinfo[j] = (uint64_t)pj | (uint64_t)(wr ? 1 : 0) << 32 | (sz < 0xFFFFFFull ? sz : 0xFFFFFFull) << 40;
 }
 
 // eq[j] = 1 when sorted position j holds the same key as j - 1 (plain key
@@ -514,8 +544,23 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scan_partials(SumPair *pa
     if (threadIdx.x == 0) sc[n] = carry;
 }
 
+// The sums per position, and per candidate c (the walk's plateau space, see
+// merge_walk_kernel): cand_pn[c] = the size sum after it, cand_pos[c] = its
+// position | 1 << 31 when the position after it continues its group, and for
+// such a candidate cand_ext[c]: the extra of the file that would start there
+// (the group's next writable pair, merge.go:67-72 after lastWrittenKey's
+// reset) as perm value | (its position - c's) << 32 | its EstimateSize << 40;
+// position delta 0: the group ends with no writable pair; 255: not resolved
+// within kExtScan positions, or a pair of 2^24 bytes or more (the walk's
+// general step).
+constexpr uint32_t kExtScan = 254;
+
 __global__ __launch_bounds__(kMergeThreads) void merge_scan_apply(const uint32_t *csize, uint32_t n,
-                                                                  const SumPair *part, SumPair *sc) {
+                                                                  const SumPair *part, SumPair *sc,
+                                                                  const uint8_t *flags, MergeIn m,
+                                                                  const uint32_t *perm, const uint64_t *xinfo,
+                                                                  uint64_t *cand_pn,
+                                                                  uint32_t *cand_pos, uint64_t *cand_ext) {
     uint32_t v[kScanPer];
     uint64_t s = 0, c = 0;
     const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
@@ -529,6 +574,35 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scan_apply(const uint32_t
     uint64_t ps = x.s + part[blockIdx.x].s, pc = x.c + part[blockIdx.x].c;
     for (uint32_t t = 0; t < kScanPer; t++) {
         if (i0 + t < n) sc[i0 + t] = SumPair{ps, pc};
+        if (v[t]) {
+            const uint64_t k = i0 + t;
+            const bool cont = k + 1 < n && !(flags[k + 1] & 1);
+            cand_pn[pc] = ps + v[t];
+            cand_pos[pc] = (uint32_t)k | (cont ? 0x80000000u : 0u);
+            if (cont) {
+                uint64_t X = 0xFFull << 32;
+                const uint64_t x1 = xinfo[k + 1];  // usually the extra itself
+                if ((x1 >> 32) & 1) {
+                    const uint64_t sz = x1 >> 40;
+                    if (sz < 0xFFFFFFull) X = (x1 & 0xFFFFFFFFull) | 1ull << 32 | sz << 40;
+                } else for (uint32_t d = 2; d <= kExtScan; d++) {
+                    const uint64_t q = k + d;
+                    const uint8_t f = q < n ? flags[q] : 1;
+                    if (f & 1) {  // the group ends with no writable pair
+                        X = 0;
+                        break;
+                    }
+                    if (f & 2) {
+                        const uint32_t wq = perm[q];
+                        const View w = view(m, wq);
+                        const uint64_t sz = 16 + (uint64_t)w.kl + w.vl;
+                        if (sz < (1ull << 24)) X = (uint64_t)wq | (uint64_t)d << 32 | sz << 40;
+                        break;
+                    }
+                }
+                cand_ext[pc] = X;
+            }
+        }
         ps += v[t];
         pc += v[t] != 0;
     }
@@ -547,6 +621,9 @@ struct WalkArgs {
     const uint32_t *perm;
     const uint8_t *flags;
     const SumPair *sc;  // n + 1
+    const uint64_t *cand_pn;   // per candidate: the size sum after it
+    const uint32_t *cand_pos;  // per candidate: its position | continues << 31
+    const uint64_t *cand_ext;  // per continuing candidate: the next file's extra (merge_scan_apply)
     uint64_t threshold;
     MergeFile *files;
     uint32_t *out;
@@ -558,114 +635,244 @@ struct WalkArgs {
 // lastWrittenKey is "" again and the group's next writable pair is written
 // (the file's "extra"); then come the candidates of later groups until the
 // size reaches the threshold.  The chain of files is sequential, so its cost
-// is the round trips it waits on.  One workgroup walks it:
-//  * prediction: each of its kWalkWins waves loads, in one round trip, the
-//    (S, C, flags) of a kWalkWin-position window around the predicted end of
-//    one of the next kWalkWins files (file j of the round ends near
-//    p + (j + 1) * span, span = the last file's positions) into LDS;
-//  * chain (wave 0, LDS only): a file that starts a group ends at the first
-//    position whose S reaches S(p) + threshold; found inside its window with
-//    the position before it below the target, it is exact, and the next file
-//    starts there with its S, C and flags from the same window;
-//  * a file whose end falls outside its window, or that continues a group,
-//    is walked by the whole workgroup (group end and extra by a parallel
-//    scan of the flags, the end by a 1,024-way search over S).
-// Round 3's one-wave walk (8 windows of 256 positions per round trip, loads
-// of one wave) took 160 us for 208 files.
-constexpr uint32_t kWalkThreads = 768;
-constexpr uint32_t kWalkWins = kWalkThreads / kWave;  // files predicted per round
-constexpr uint32_t kWalkWin = 512;                    // positions per window
+// is the round trips it waits on.  One workgroup walks it.
+//
+// Plateau space.  S(k), the candidate sizes before position k, is flat across
+// non-candidates, and a file ends at the first k > g with S(k) >= its target:
+// the position after a candidate.  With P[e] the size sum of the first e
+// candidates (cand_pn[e - 1]), a file whose first candidate is e0 writes its
+// extra (if any) and candidates e0 .. e - 1, e = the first plateau with
+// P[e] >= P[e0] + T - (the extra's size), and the next file starts at
+// cand_pos[e - 1] + 1 -- a group start unless that candidate's group goes on
+// (cand_pos bit 31; its extra is then in cand_ext[e - 1]).  Duplicates and
+// dropped tombstones take no plateau, so a file's plateau count is its pair
+// count and varies only with the pair sizes.
+//  * prediction: each round loads, in one round trip by the whole
+//    workgroup, a window of W = kWalkEntries / R plateaus around the
+//    predicted end of each of the next R files (file r of the round ends near
+//    e0 + (r + 1) * span, span = the mean pairs per file so far) into LDS;
+//  * succession (all threads, LDS only): every plateau of window r, taken as
+//    the start of file r + 1, gets that file's end in window r + 1 by a
+//    binary search -- exact when the plateau before it is in the window
+//    (below the target there) or is the file's own start;
+//  * chain (wave 0): file 0's end by ballots over window 0, then one LDS
+//    lookup per file;
+//  * a file whose end falls outside its window ends the round, and the next
+//    round predicts fewer files in wider windows (a round that resolves all
+//    its files doubles R); a continuation whose extra was not resolved by
+//    merge_scan_apply, a pair as large as the threshold, or an end outside a
+//    one-file window is walked by the whole workgroup (group end and extra
+//    by a parallel scan of the flags, the end by a 1,024-way search over S).
+// Round 3's one-wave walk (position windows, 8 files per round trip) took
+// 160 us for 208 files; a position-window form with 12 files per round,
+// 470 us (the duplicates' position drift missed its windows).
+constexpr uint32_t kWalkThreads = 1024;
+constexpr uint32_t kWalkEntries = 4 * kWalkThreads;  // window plateaus per round
+constexpr uint32_t kWalkMaxR = 32;                   // most files predicted per round
+constexpr uint16_t kSuccMiss = 0xFFFF, kSuccGeneral = 0xFFFE, kSuccStop = 0xFFFD,
+                   kSuccLast = 0xFFFC;
 
 struct WalkState {
-    uint32_t p, nf, span, stop;   // stop: 1 = walk done, 2 = general step next
-    uint64_t o, most;
+    uint32_t p, e, nf, span, R, stop;  // e = C(p); stop: 1 = walk done, 2 = general step next
+    uint64_t o, most, P;               // P = S(p)
 };
 
+// The file that starts right after plateau e (P = P[e], Q = cand_pos[e - 1],
+// X = cand_ext[e - 1]; first = the walk's first file, at 0): its first
+// position p, its extra (wpos / wperm, kNone if none) and its target, or the
+// code of a file the window search does not resolve.
+__device__ __forceinline__ uint16_t walk_file(uint64_t P, uint32_t Q, uint64_t X, bool first, uint32_t n,
+                                              uint64_t T, uint64_t tail_s, uint32_t &p, uint32_t &wpos,
+                                              uint32_t &wperm, uint64_t &tg) {
+    wpos = kNone;
+    wperm = 0;
+    uint64_t wsize = 0;
+    p = 0;
+    if (!first) {
+        p = (Q & 0x7FFFFFFFu) + 1;
+        if (p >= n) return kSuccStop;
+        if (Q >> 31) {  // continues a group
+            const uint32_t d = (uint32_t)(X >> 32) & 0xFFu;
+            if (d == 0xFFu) return kSuccGeneral;
+            if (d) {
+                wpos = (Q & 0x7FFFFFFFu) + d;
+                wperm = (uint32_t)X;
+                wsize = X >> 40;
+                if (wsize >= T) return kSuccGeneral;  // the extra alone fills the file
+            }
+        }
+    }
+    tg = P + T - wsize;
+    return tail_s < tg ? kSuccLast : 0;
+}
+
 __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
-    __shared__ uint64_t ws[kWalkWins][kWalkWin];
-    __shared__ uint64_t wc[kWalkWins][kWalkWin];
-    __shared__ uint8_t wf[kWalkWins][kWalkWin];
+    __shared__ uint64_t wp[kWalkEntries];   // P of each window plateau
+    __shared__ uint64_t wx[kWalkEntries];   // cand_ext of its last candidate
+    __shared__ uint32_t wq[kWalkEntries];   // cand_pos of its last candidate
+    __shared__ uint16_t sx[kWalkEntries];   // succession: the next file's end in the next window
     __shared__ WalkState st;
     __shared__ uint32_t s_min[2];
+    __shared__ uint32_t s_q0;
+    __shared__ uint64_t s_x0;
     const uint32_t n = a.m.n, t = threadIdx.x, lane = lane_id(), wave = t / kWave;
     const SumPair tail = a.sc[n];
     const uint64_t T = a.threshold;
-    if (t == 0) st = WalkState{0, 0, 0, n == 0 ? 1u : 0u, 0, 0};
+    const uint32_t ncand = (uint32_t)tail.c;
+    if (t == 0) {
+        // the first span: pairs per file at the mean candidate size
+        const double est = tail.s ? (double)T * (double)tail.c / (double)tail.s : 0.0;
+        const uint32_t span = est < 1.0 ? 1u : est > (double)ncand ? ncand : (uint32_t)est;
+        // the plateau path packs a flag into bit 31 of a position
+        const uint32_t stop = n == 0 ? 1u : n >= 0x80000000u ? 2u : 0u;
+        st = WalkState{0, 0, 0, span, kWalkMaxR, stop, 0, 0, 0};
+    }
     __syncthreads();
     for (;;) {
         WalkState S0 = st;
-        if (S0.stop == 1) break;
-        __syncthreads();
-        if (S0.span > 0 && S0.stop == 0) {
-            // prediction: window w around the predicted end of the round's file w
-            const uint64_t c = (uint64_t)S0.p + (uint64_t)(wave + 1) * S0.span;
-            const uint64_t b = c > S0.p + kWalkWin / 2 ? c - kWalkWin / 2 : S0.p + 1;
-#pragma unroll
-            for (uint32_t i = 0; i < kWalkWin / kWave; i++) {
-                const uint64_t k = b + kWave * i + lane;
-                const uint32_t kc = k < n ? (uint32_t)k : n;
-                const SumPair q = a.sc[kc];
-                ws[wave][kWave * i + lane] = q.s;
-                wc[wave][kWave * i + lane] = q.c;
-                wf[wave][kWave * i + lane] = k < n ? a.flags[kc] : (uint8_t)1;
+        // every pass writes a file or hands the next one to the general step,
+        // which writes one: more files than pairs cannot happen (fail-safe
+        // against overrunning files[])
+        if (S0.stop == 1 || S0.nf > n) break;
+        __syncthreads();  // st is rewritten below
+        if (S0.stop == 0 && S0.p != 0 && S0.e == 0) S0.stop = 2;  // no plateau before p
+        if (S0.stop == 0) {
+            const uint32_t R = S0.R, W = kWalkEntries / R;
+            auto base = [&](uint32_t r) -> uint64_t {  // the first plateau of window r
+                const uint64_t c = (uint64_t)S0.e + (uint64_t)(r + 1) * S0.span;
+                return c > (uint64_t)S0.e + 1 + W / 2 ? c - W / 2 : (uint64_t)S0.e + 1;
+            };
+            for (uint32_t x = t; x < kWalkEntries; x += kWalkThreads) {
+                const uint32_t r = x / W;
+                const uint64_t e = base(r) + (x - r * W);
+                uint64_t P = ~0ull, X = 0;
+                uint32_t Q = 0;
+                if (e <= ncand) {
+                    P = a.cand_pn[e - 1];
+                    Q = a.cand_pos[e - 1];
+                    X = a.cand_ext[e - 1];
+                }
+                wp[x] = P;
+                wq[x] = Q;
+                wx[x] = X;
+            }
+            if (t == 0 && S0.p) {  // the round's first file starts after plateau S0.e
+                s_q0 = a.cand_pos[S0.e - 1];
+                s_x0 = a.cand_ext[S0.e - 1];
+            }
+            __syncthreads();
+            // succession: plateau x of window r as the start of file r + 1
+            for (uint32_t x = t; x < kWalkEntries; x += kWalkThreads) {
+                const uint32_t r = x / W;
+                if (r + 1 >= R) break;
+                const uint64_t e = base(r) + (x - r * W);
+                uint16_t out = kSuccMiss;
+                if (e <= ncand) {
+                    uint32_t p, wpos, wperm;
+                    uint64_t tg;
+                    out = walk_file(wp[x], wq[x], wx[x], false, n, T, tail.s, p, wpos, wperm, tg);
+                    if (out == 0) {
+                        const uint32_t b1 = (r + 1) * W;
+                        uint32_t lo = 0, hi = W;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (wp[b1 + mid] < tg) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        out = (lo < W && (lo > 0 || base(r + 1) <= e + 1)) ? (uint16_t)lo : kSuccMiss;
+                    }
+                }
+                sx[x] = out;
             }
             __syncthreads();
             if (wave == 0) {
-                // the round's first file: its S, C and flags from global
-                uint32_t p = S0.p;
-                uint64_t Sp = uni64(a.sc[p].s), Cp = uni64(a.sc[p].c);
-                uint32_t fp = (uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? a.flags[p] : 0);
+                uint32_t nf = S0.nf, span = S0.span, Rn = R, stop = 0;
                 uint64_t o = S0.o, most = S0.most;
-                uint32_t nf = S0.nf, span = S0.span, stop = 2;
-                for (uint32_t j = 0; j < kWalkWins; j++) {
-                    if (p >= n) { stop = 1; break; }
-                    if (!(p == 0 || (fp & 1))) break;  // continues a group: general step
-                    const uint64_t tg = Sp + T;
-                    if (tail.s < tg) {  // the rest fits in this file (merge.go:125-128)
-                        const uint64_t nw = tail.c - Cp;
+                // the current start: after plateau e0 (P0, Q0, X0)
+                uint32_t e0 = S0.e, Q0 = S0.p ? s_q0 : 0;
+                uint64_t P0 = S0.P, X0 = S0.p ? s_x0 : 0;
+                uint32_t p, wpos, wperm;
+                uint64_t tg;
+                uint16_t code = walk_file(P0, Q0, X0, S0.p == 0, n, T, tail.s, p, wpos, wperm, tg);
+                if (p != S0.p) {  // not a plateau start (after an extra that filled a file)
+                    code = kSuccGeneral;
+                    p = S0.p;
+                }
+                if (code == 0) {  // file 0's end: the first window-0 plateau at the target
+                    code = kSuccMiss;
+                    for (uint32_t i0 = 0; i0 < W; i0 += kWave) {
+                        const uint64_t ge = __ballot(wp[i0 + lane] >= tg);
+                        if (!ge) continue;
+                        const uint32_t x = i0 + (uint32_t)__builtin_ctzll(ge);
+                        if (x > 0 || base(0) <= (uint64_t)e0 + 1) code = (uint16_t)x;
+                        break;
+                    }
+                }
+                const uint32_t e_first = e0, nf_first = nf;
+                for (uint32_t r = 0;; r++) {
+                    if (code == kSuccStop) {
+                        stop = 1;
+                        break;
+                    }
+                    if (code == kSuccLast) {  // the rest fits in this file (merge.go:125-128)
+                        const uint64_t nw = (wpos != kNone ? 1 : 0) + (tail.c - e0);
                         if (nw) {
-                            if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
+                            if (lane == 0) {
+                                a.files[nf] = MergeFile{p, wpos, o};
+                                if (wpos != kNone) a.out[o] = wperm;
+                            }
                             o += nw;
                             most = nw > most ? nw : most;
                             nf++;
                         }
-                        p = n;
                         stop = 1;
                         break;
                     }
-                    const uint64_t c = (uint64_t)S0.p + (uint64_t)(j + 1) * S0.span;
-                    const uint64_t b = c > S0.p + kWalkWin / 2 ? c - kWalkWin / 2 : S0.p + 1;
-                    int hit = -1;
-#pragma unroll
-                    for (uint32_t i = 0; i < kWalkWin / kWave; i++) {
-                        const uint64_t ge = __ballot(ws[j][kWave * i + lane] >= tg);
-                        if (!ge) continue;
-                        const uint32_t x = kWave * i + (uint32_t)__builtin_ctzll(ge);
-                        // exact when the position before it is in the window
-                        // (below the target there) or is p itself
-                        if (x > 0 || b <= (uint64_t)p + 1) hit = (int)x;
+                    if (code == kSuccGeneral) {
+                        stop = 2;
                         break;
                     }
-                    if (hit < 0) break;  // the end lies outside the window: general step
-                    const uint32_t k = (uint32_t)(b + (uint32_t)hit);
-                    const uint64_t Ck = wc[j][hit];
-                    const uint64_t nw = Ck - Cp;
-                    if (lane == 0) a.files[nf] = MergeFile{p, kNone, o};
+                    if (code == kSuccMiss) {  // outside the window: fewer files, wider windows
+                        Rn = 1;
+                        while (2 * Rn <= r) Rn *= 2;
+                        if (r == 0) stop = 2;  // nothing resolved: the general step
+                        break;
+                    }
+                    // file r ends after plateau e in window r
+                    const uint32_t x = r * W + code;
+                    const uint32_t e = (uint32_t)base(r) + code;
+                    const uint64_t nw = (wpos != kNone ? 1 : 0) + (e - e0);
+                    if (lane == 0) {
+                        a.files[nf] = MergeFile{p, wpos, o};
+                        if (wpos != kNone) a.out[o] = wperm;
+                    }
                     o += nw;
                     most = nw > most ? nw : most;
                     nf++;
-                    span = k - p;
-                    p = k;
-                    Sp = ws[j][hit];
-                    Cp = Ck;
-                    fp = wf[j][hit];
+                    e0 = e;
+                    P0 = wp[x];
+                    Q0 = wq[x];
+                    X0 = wx[x];
+                    if (r + 1 == R) {  // every file of the round resolved
+                        if (R < kWalkMaxR) Rn = 2 * R;
+                        p = (Q0 & 0x7FFFFFFFu) + 1;
+                        if (p >= n) stop = 1;
+                        break;
+                    }
+                    code = sx[x];
+                    if (code < kSuccLast) {
+                        walk_file(P0, Q0, X0, false, n, T, tail.s, p, wpos, wperm, tg);
+                    } else {
+                        p = (Q0 & 0x7FFFFFFFu) + 1;
+                        if (code == kSuccLast) walk_file(P0, Q0, X0, false, n, T, tail.s, p, wpos, wperm, tg);
+                    }
                 }
-                if (lane == 0) st = WalkState{p, nf, span, p >= n ? 1u : stop, o, most};
+                if (nf > nf_first && e0 > e_first) span = (e0 - e_first + (nf - nf_first) / 2) / (nf - nf_first);
+                if (span == 0) span = 1;
+                if (lane == 0) st = WalkState{p, e0, nf, span, Rn, stop, o, most, P0};
             }
             __syncthreads();
-            S0 = st;
-            if (S0.stop == 1) break;
-            __syncthreads();
+            continue;
         }
         // general step: the file starting at S0.p, by the whole workgroup
         const uint32_t p = S0.p;
@@ -703,7 +910,7 @@ __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
         } else {
             const uint64_t tg = Sg + (T - wsize);
             if (tail.s >= tg) {
-                // first k in [g + 1, n] with S(k) >= tg: 768-way search rounds
+                // first k in [g + 1, n] with S(k) >= tg: 1,024-way search rounds
                 uint32_t lo = g + 1, hi = n;
                 while (hi > lo) {
                     const uint32_t span = hi - lo;
@@ -726,8 +933,8 @@ __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
                 end = lo;  // the first position at or above the target; e = end - 1
             }
         }
-        const uint64_t Ce = end < n ? a.sc[end].c : tail.c;
-        const uint64_t nw = (w != kNone ? 1 : 0) + (end > g ? Ce - Cg : 0);
+        const SumPair Se = end < n ? a.sc[end] : tail;
+        const uint64_t nw = (w != kNone ? 1 : 0) + (end > g ? Se.c - Cg : 0);
         if (t == 0) {
             WalkState x = S0;
             if (nw == 0) {
@@ -738,9 +945,12 @@ __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
                 x.o += nw;
                 x.most = nw > x.most ? nw : x.most;
                 x.nf++;
-                x.span = end > g ? end - g : 0;  // 0: no prediction next round
+                if (end > g && Se.c > Cg) x.span = (uint32_t)(Se.c - Cg);
                 x.p = end;
-                x.stop = end >= n ? 1u : 0u;
+                x.e = (uint32_t)Se.c;
+                x.P = Se.s;
+                // the plateau path again, unless positions exceed its packing
+                x.stop = end >= n ? 1u : n >= 0x80000000u ? 2u : 0u;
             }
             st = x;
         }
@@ -1048,6 +1258,7 @@ struct MergeWs {
     MergeFile *files;
     uint64_t *stats;  // [0..1] counts, then the long-key OR/AND words
     uint64_t *part;   // kStatBlocks * kStatWords
+    uint64_t *xinfo;  // n: merge_flags_kernel's per-pair words for the walk's extras
     void *sort_tmp;
     size_t sort_bytes;
     size_t total;
@@ -1083,6 +1294,7 @@ MergeWs merge_ws_layout(uint8_t *base, uint32_t n) {
     w.files = reinterpret_cast<MergeFile *>(take(sizeof(MergeFile) * (nn + 2)));
     w.stats = reinterpret_cast<uint64_t *>(take(8 * (2 + 2 * (size_t)kMaxChunks)));
     w.part = reinterpret_cast<uint64_t *>(take(8 * (size_t)kStatBlocks * kStatWords));
+    w.xinfo = reinterpret_cast<uint64_t *>(take(8 * nn));
     w.sort_bytes = sort_tmp_bytes(n);
     w.sort_tmp = take(w.sort_bytes);
     w.total = at;
@@ -1366,7 +1578,7 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
 
     // 3. groups and candidates; 4. sums and the file walk; 5. emit
     hipLaunchKernelGGL(merge_flags_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m, perm,
-                       level, w.flags, w.csize);
+                       level, w.flags, w.csize, w.xinfo);
     hipLaunchKernelGGL(merge_candidate_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m,
                        w.flags, w.csize);
     const uint32_t ntiles = (N + kScanTile - 1) / kScanTile;
@@ -1374,9 +1586,12 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
                        w.scan_part);
     hipLaunchKernelGGL(merge_scan_partials, dim3(1), dim3(kMergeThreads), 0, s, w.scan_part, ntiles,
                        w.sc, N);
+    // the walk's plateau arrays in the sort's buffers, free from here on
+    uint64_t *cand_pn = w.keys[0], *cand_ext = w.keys[1];
+    uint32_t *cand_pos = w.perm[cur ^ 1];
     hipLaunchKernelGGL(merge_scan_apply, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
-                       w.scan_part, w.sc);
-    WalkArgs wa{m, perm, w.flags, w.sc, threshold, w.files, d_out, w.stats};
+                       w.scan_part, w.sc, w.flags, m, perm, w.xinfo, cand_pn, cand_pos, cand_ext);
+    WalkArgs wa{m, perm, w.flags, w.sc, cand_pn, cand_pos, cand_ext, threshold, w.files, d_out, w.stats};
     hipLaunchKernelGGL(merge_walk_kernel, dim3(1), dim3(kWalkThreads), 0, s, wa);
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
                        w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);

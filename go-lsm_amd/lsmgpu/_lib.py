@@ -151,6 +151,9 @@ ABI_VERSION = 4   # LSM_ABI_VERSION this binding is written against
 INPUT_SLACK = 32  # LSM_INPUT_SLACK: device inputs are padded by this much
 
 _lib = None
+# scripts/ab_lib.py clears this to load a diagnostic variant built from
+# patched sources; the product path always checks
+CHECK_BUILD_ID = True
 
 
 def load():
@@ -174,7 +177,7 @@ def load():
     # the library must be built from the sources beside it (build_id.py): a
     # stale prebuilt liblsm_gpu.so never stands in for the current tree
     pkg = os.path.dirname(_PKG_DIR)
-    if os.path.isdir(os.path.join(pkg, "csrc")):
+    if CHECK_BUILD_ID and os.path.isdir(os.path.join(pkg, "csrc")):
         import importlib.util
         spec = importlib.util.spec_from_file_location("_lsm_build_id", os.path.join(pkg, "build_id.py"))
         mod = importlib.util.module_from_spec(spec)
