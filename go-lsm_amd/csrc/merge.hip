@@ -114,6 +114,10 @@ __device__ __forceinline__ uint64_t wave_and64(uint64_t v) {
     for (int o = 32; o > 0; o >>= 1) v &= __shfl_xor(v, o);
     return v;
 }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+}
 __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t t = __shfl_xor(v, o);
@@ -761,115 +765,124 @@ __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
                 s_x0 = a.cand_ext[S0.e - 1];
             }
             __syncthreads();
-            // succession: plateau x of window r as the start of file r + 1
-            for (uint32_t x = t; x < kWalkEntries; x += kWalkThreads) {
-                const uint32_t r = x / W;
-                if (r + 1 >= R) break;
-                const uint64_t e = base(r) + (x - r * W);
-                uint16_t out = kSuccMiss;
-                if (e <= ncand) {
-                    uint32_t p, wpos, wperm;
-                    uint64_t tg;
-                    out = walk_file(wp[x], wq[x], wx[x], false, n, T, tail.s, p, wpos, wperm, tg);
-                    if (out == 0) {
-                        const uint32_t b1 = (r + 1) * W;
-                        uint32_t lo = 0, hi = W;
-                        while (lo < hi) {
-                            const uint32_t mid = (lo + hi) >> 1;
-                            if (wp[b1 + mid] < tg) lo = mid + 1;
-                            else hi = mid;
-                        }
-                        out = (lo < W && (lo > 0 || base(r + 1) <= e + 1)) ? (uint16_t)lo : kSuccMiss;
+            // succession: plateau x of window r as the start of file r + 1;
+            // a thread's plateaus search in lockstep (their LDS reads in
+            // flight together)
+            {
+                constexpr uint32_t PT = kWalkEntries / kWalkThreads;
+                uint64_t tg[PT];
+                uint32_t b1[PT], pos[PT];
+                uint16_t code[PT];
+#pragma unroll
+                for (uint32_t k = 0; k < PT; k++) {
+                    const uint32_t x = t + k * kWalkThreads, r = x / W;
+                    const uint64_t e = base(r) + (x - r * W);
+                    code[k] = kSuccMiss;
+                    tg[k] = ~0ull;
+                    if (r + 1 < R && e <= ncand) {
+                        uint32_t p, wpos, wperm;
+                        code[k] = walk_file(wp[x], wq[x], wx[x], false, n, T, tail.s, p, wpos, wperm, tg[k]);
                     }
+                    b1[k] = code[k] == 0 ? (r + 1) * W : 0;  // others search harmlessly
+                    pos[k] = 0;
                 }
-                sx[x] = out;
+                for (uint32_t s = W / 2; s > 0; s >>= 1) {
+#pragma unroll
+                    for (uint32_t k = 0; k < PT; k++)
+                        if (wp[b1[k] + pos[k] + s - 1] < tg[k]) pos[k] += s;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < PT; k++) {
+                    const uint32_t x = t + k * kWalkThreads, r = x / W;
+                    if (r + 1 >= R) continue;
+                    if (code[k] == 0) {
+                        const uint32_t lo = pos[k] + (wp[b1[k] + pos[k]] < tg[k] ? 1u : 0u);
+                        const uint64_t e = base(r) + (x - r * W);
+                        code[k] = (lo < W && (lo > 0 || base(r + 1) <= e + 1)) ? (uint16_t)lo : kSuccMiss;
+                    }
+                    sx[x] = code[k];
+                }
             }
             __syncthreads();
             if (wave == 0) {
-                uint32_t nf = S0.nf, span = S0.span, Rn = R, stop = 0;
-                uint64_t o = S0.o, most = S0.most;
-                // the current start: after plateau e0 (P0, Q0, X0)
-                uint32_t e0 = S0.e, Q0 = S0.p ? s_q0 : 0;
-                uint64_t P0 = S0.P, X0 = S0.p ? s_x0 : 0;
+                // the round's first file starts after plateau S0.e (the state)
+                const uint32_t Qs = S0.p ? s_q0 : 0;
+                const uint64_t Xs = S0.p ? s_x0 : 0;
                 uint32_t p, wpos, wperm;
                 uint64_t tg;
-                uint16_t code = walk_file(P0, Q0, X0, S0.p == 0, n, T, tail.s, p, wpos, wperm, tg);
-                if (p != S0.p) {  // not a plateau start (after an extra that filled a file)
-                    code = kSuccGeneral;
-                    p = S0.p;
-                }
+                uint16_t code = walk_file(S0.P, Qs, Xs, S0.p == 0, n, T, tail.s, p, wpos, wperm, tg);
+                if (p != S0.p) code = kSuccGeneral;  // not a plateau start (after an extra that filled a file)
                 if (code == 0) {  // file 0's end: the first window-0 plateau at the target
                     code = kSuccMiss;
                     for (uint32_t i0 = 0; i0 < W; i0 += kWave) {
                         const uint64_t ge = __ballot(wp[i0 + lane] >= tg);
                         if (!ge) continue;
                         const uint32_t x = i0 + (uint32_t)__builtin_ctzll(ge);
-                        if (x > 0 || base(0) <= (uint64_t)e0 + 1) code = (uint16_t)x;
+                        if (x > 0 || base(0) <= (uint64_t)S0.e + 1) code = (uint16_t)x;
                         break;
                     }
                 }
-                const uint32_t e_first = e0, nf_first = nf;
-                for (uint32_t r = 0;; r++) {
-                    if (code == kSuccStop) {
-                        stop = 1;
-                        break;
-                    }
-                    if (code == kSuccLast) {  // the rest fits in this file (merge.go:125-128)
-                        const uint64_t nw = (wpos != kNone ? 1 : 0) + (tail.c - e0);
-                        if (nw) {
-                            if (lane == 0) {
-                                a.files[nf] = MergeFile{p, wpos, o};
-                                if (wpos != kNone) a.out[o] = wperm;
-                            }
-                            o += nw;
-                            most = nw > most ? nw : most;
-                            nf++;
-                        }
-                        stop = 1;
-                        break;
-                    }
-                    if (code == kSuccGeneral) {
-                        stop = 2;
-                        break;
-                    }
-                    if (code == kSuccMiss) {  // outside the window: fewer files, wider windows
-                        Rn = 1;
-                        while (2 * Rn <= r) Rn *= 2;
-                        if (r == 0) stop = 2;  // nothing resolved: the general step
-                        break;
-                    }
-                    // file r ends after plateau e in window r
-                    const uint32_t x = r * W + code;
-                    const uint32_t e = (uint32_t)base(r) + code;
-                    const uint64_t nw = (wpos != kNone ? 1 : 0) + (e - e0);
-                    if (lane == 0) {
-                        a.files[nf] = MergeFile{p, wpos, o};
-                        if (wpos != kNone) a.out[o] = wperm;
-                    }
-                    o += nw;
-                    most = nw > most ? nw : most;
-                    nf++;
-                    e0 = e;
-                    P0 = wp[x];
-                    Q0 = wq[x];
-                    X0 = wx[x];
-                    if (r + 1 == R) {  // every file of the round resolved
-                        if (R < kWalkMaxR) Rn = 2 * R;
-                        p = (Q0 & 0x7FFFFFFFu) + 1;
-                        if (p >= n) stop = 1;
-                        break;
-                    }
-                    code = sx[x];
-                    if (code < kSuccLast) {
-                        walk_file(P0, Q0, X0, false, n, T, tail.s, p, wpos, wperm, tg);
-                    } else {
-                        p = (Q0 & 0x7FFFFFFFu) + 1;
-                        if (code == kSuccLast) walk_file(P0, Q0, X0, false, n, T, tail.s, p, wpos, wperm, tg);
-                    }
+                // chain: file r ends at plateau x_r of window r (lane r keeps
+                // it) while the files resolve; one LDS read per file
+                uint32_t nres = 0, my_x = 0;
+                while (code < kSuccLast) {
+                    if (lane == nres) my_x = code;
+                    nres++;
+                    if (nres == R) break;
+                    code = sx[(nres - 1) * W + code];
                 }
-                if (nf > nf_first && e0 > e_first) span = (e0 - e_first + (nf - nf_first) / 2) / (nf - nf_first);
+                // every lane r <= nres: file r's start (after file r - 1's
+                // end, or the state's) and, for r < nres, its end
+                const uint32_t px = __shfl_up(my_x, 1);
+                uint64_t Ps = S0.P, es = S0.e;
+                uint32_t Qr = Qs;
+                uint64_t Xr = Xs;
+                if (lane > 0 && lane <= nres) {
+                    const uint32_t y = (lane - 1) * W + px;
+                    Ps = wp[y];
+                    Qr = wq[y];
+                    Xr = wx[y];
+                    es = base(lane - 1) + px;
+                }
+                uint32_t pr = 0, wposr = kNone, wpermr = 0;
+                uint64_t tgr;
+                walk_file(Ps, Qr, Xr, lane == 0 && S0.p == 0, n, T, tail.s, pr, wposr, wpermr, tgr);
+                if (lane == 0) pr = S0.p;
+                uint64_t nw = 0;
+                if (lane < nres) {
+                    nw = (wposr != kNone ? 1 : 0) + (base(lane) + my_x - es);
+                } else if (lane == nres && nres < R && code == kSuccLast) {
+                    nw = (wposr != kNone ? 1 : 0) + (tail.c - es);  // the rest fits (merge.go:125-128)
+                }
+                uint64_t tot;
+                const uint64_t ox = S0.o + wave_excl_scan64(nw, &tot);
+                const uint64_t most = wave_max64(nw > S0.most ? nw : S0.most);
+                if (nw) {
+                    a.files[S0.nf + lane] = MergeFile{pr, wposr, ox};
+                    if (wposr != kNone) a.out[ox] = wpermr;
+                }
+                // the next state: the start of file nres
+                const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)pr, (int)nres);
+                const uint64_t ne = readlane64(es, nres), nP = readlane64(Ps, nres);
+                uint32_t stop = 0, Rn = R;
+                if (nres == R) {
+                    Rn = R < kWalkMaxR ? 2 * R : R;  // every file of the round resolved
+                    stop = np >= n ? 1u : 0u;
+                } else if (code == kSuccStop || code == kSuccLast) {
+                    stop = 1;
+                } else if (code == kSuccGeneral) {
+                    stop = 2;
+                } else {  // kSuccMiss: the end lies outside the window: fewer files, wider windows
+                    Rn = 1;
+                    while (2 * Rn <= nres) Rn *= 2;
+                    stop = nres == 0 ? 2u : 0u;  // nothing resolved: the general step
+                }
+                // files written: lanes 0 .. nres - 1, and lane nres for a last file
+                const uint32_t nfn = S0.nf + (uint32_t)__builtin_popcountll(__ballot(nw != 0));
+                uint32_t span = S0.span;
+                if (nres > 0 && ne > S0.e) span = (uint32_t)((ne - S0.e + nres / 2) / nres);
                 if (span == 0) span = 1;
-                if (lane == 0) st = WalkState{p, e0, nf, span, Rn, stop, o, most, P0};
+                if (lane == 0) st = WalkState{np, (uint32_t)ne, nfn, span, Rn, stop, S0.o + tot, most, nP};
             }
             __syncthreads();
             continue;
