@@ -628,6 +628,9 @@ struct WalkArgs {
     const uint64_t *cand_pn;   // per candidate: the size sum after it
     const uint32_t *cand_pos;  // per candidate: its position | continues << 31
     const uint64_t *cand_ext;  // per continuing candidate: the next file's extra (merge_scan_apply)
+    const uint8_t *abs_succ;   // merge_walk_abs_kernel's maps, window bases and head
+    const uint64_t *abs_bases;
+    const uint32_t *abs_head;
     uint64_t threshold;
     MergeFile *files;
     uint32_t *out;
@@ -710,11 +713,114 @@ __device__ __forceinline__ uint16_t walk_file(uint64_t P, uint32_t Q, uint64_t X
     return tail_s < tg ? kSuccLast : 0;
 }
 
+// ---- one-shot prediction of every file's end ------------------------------
+//
+// Before the rounds, merge_walk_abs_kernel predicts the end of every file of
+// the walk at once, from plateau 0: file f of a uniform stream ends near
+// plateau (f + 1) * span, span = (T + half a mean pair) / the mean pair (the
+// overshoot past T is half a pair on average), and the deviation only
+// accumulates the files' varying pair counts (a random walk: on the
+// compaction bench within +-55 plateaus over 208 files).  One workgroup per
+// window of kAbsW plateaus around each predicted end maps every plateau of
+// its window, taken as the end of file f, to file f + 1's end in the next
+// window (the same exact test as a round's succession), and the walk chains
+// the maps from file 0 in LDS.  The first miss (or a window limit) hands the
+// rest of the walk to the rounds.
+constexpr uint32_t kAbsW = 248;      // plateaus per window
+constexpr uint32_t kAbsThreads = 256;
+constexpr uint8_t kAbsLast = 252, kAbsStop = 253, kAbsGeneral = 254, kAbsMiss = 255;
+constexpr uint32_t kAbsMaxWin = 352;  // files predicted: 352 x 248 B of the walk's LDS
+
+struct AbsArgs {
+    const uint64_t *cand_pn;
+    const uint32_t *cand_pos;
+    const uint64_t *cand_ext;
+    const SumPair *sc;
+    uint32_t n;
+    uint64_t threshold;
+    uint8_t *succ;    // [kAbsMaxWin][kAbsW]
+    uint64_t *bases;  // [kAbsMaxWin][2]: window f's first plateau, and window f + 1's as block f used it
+    uint32_t *head;   // [0] = windows, [1] = file 0's end in window 0 (or a code)
+};
+
+__device__ __forceinline__ uint32_t abs_windows(const SumPair &tail, uint64_t T) {
+    if (tail.c == 0) return 0;
+    const uint64_t nf = tail.s / T + 2;
+    return nf < kAbsMaxWin ? (uint32_t)nf : kAbsMaxWin;
+}
+__device__ __forceinline__ uint64_t abs_base(const SumPair &tail, uint64_t T, uint32_t f) {
+    const double span = ((double)T + 0.5 * (double)tail.s / (double)tail.c) * (double)tail.c / (double)tail.s;
+    const uint64_t c = (uint64_t)((double)(f + 1) * span + 0.5);
+    return c > 1 + kAbsW / 2 ? c - kAbsW / 2 : 1;
+}
+
+__global__ __launch_bounds__(kAbsThreads) void merge_walk_abs_kernel(AbsArgs a) {
+    __shared__ uint64_t np[kAbsW];
+    __shared__ uint32_t s_first;
+    const uint32_t f = blockIdx.x, t = threadIdx.x;
+    const SumPair tail = a.sc[a.n];
+    const uint64_t T = a.threshold;
+    const uint32_t nwin = abs_windows(tail, T), ncand = (uint32_t)tail.c;
+    if (f == 0 && t == 0) a.head[0] = nwin;
+    if (f >= nwin) return;
+    const uint64_t b0 = abs_base(tail, T, f), b1 = abs_base(tail, T, f + 1);
+    if (t == 0) s_first = kAbsW;
+    uint64_t P = ~0ull, X = 0;
+    uint32_t Q = 0;
+    const uint64_t e = b0 + t;
+    if (t < kAbsW) {
+        const uint64_t e1 = b1 + t;
+        np[t] = e1 <= ncand ? a.cand_pn[e1 - 1] : ~0ull;
+        if (e <= ncand) {
+            P = a.cand_pn[e - 1];
+            Q = a.cand_pos[e - 1];
+            X = a.cand_ext[e - 1];
+        }
+    }
+    __syncthreads();
+    if (f == 0 && t < kAbsW && P >= T) atomicMin(&s_first, t);  // file 0 ends at P >= T
+    if (t < kAbsW) {
+        uint8_t out = kAbsMiss;
+        if (e <= ncand) {
+            uint32_t p, wpos, wperm;
+            uint64_t tg = ~0ull;
+            const uint16_t c = walk_file(P, Q, X, false, a.n, T, tail.s, p, wpos, wperm, tg);
+            if (c == kSuccLast) out = kAbsLast;
+            else if (c == kSuccStop) out = kAbsStop;
+            else if (c == kSuccGeneral) out = kAbsGeneral;
+            else {
+                uint32_t pos = 0;
+                for (uint32_t s = 128; s > 0; s >>= 1)
+                    if (pos + s <= kAbsW && np[pos + s - 1] < tg) pos += s;
+                // pos = the first window-(f + 1) plateau at the target, or kAbsW
+                if (pos < kAbsW && (pos > 0 || b1 <= e + 1)) out = (uint8_t)pos;
+            }
+        }
+        a.succ[(uint64_t)f * kAbsW + t] = out;
+    }
+    if (t == 0) {
+        a.bases[2 * f] = b0;
+        a.bases[2 * f + 1] = b1;
+    }
+    __syncthreads();
+    if (f == 0 && t == 0) {  // file 0 (from position 0, no extra): the target is T
+        const uint32_t x = s_first;
+        a.head[1] = tail.s < T ? kAbsLast : (x < kAbsW && (x > 0 || b0 <= 1)) ? x : kAbsMiss;
+    }
+}
+
 __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
-    __shared__ uint64_t wp[kWalkEntries];   // P of each window plateau
-    __shared__ uint64_t wx[kWalkEntries];   // cand_ext of its last candidate
-    __shared__ uint32_t wq[kWalkEntries];   // cand_pos of its last candidate
-    __shared__ uint16_t sx[kWalkEntries];   // succession: the next file's end in the next window
+    // the rounds' windows; phase 1's maps before them
+    __shared__ __attribute__((aligned(16))) uint8_t lds_raw[kWalkEntries * 22];
+    uint64_t *wp = reinterpret_cast<uint64_t *>(lds_raw);  // P of each window plateau
+    uint64_t *wx = wp + kWalkEntries;                       // cand_ext of its last candidate
+    uint32_t *wq = reinterpret_cast<uint32_t *>(wx + kWalkEntries);  // cand_pos of its last candidate
+    uint16_t *sx = reinterpret_cast<uint16_t *>(wq + kWalkEntries);  // succession: the next file's end
+    static_assert(kAbsMaxWin * kAbsW <= kWalkEntries * 22, "phase 1 maps fit the window buffers");
+    __shared__ uint64_t s_bases[2 * kAbsMaxWin];
+    __shared__ uint8_t s_chosen[kAbsMaxWin];
+    __shared__ uint64_t s_wsum[kWalkThreads / kWave], s_wmax[kWalkThreads / kWave];
+    __shared__ uint32_t s_nres, s_code;
     __shared__ WalkState st;
     __shared__ uint32_t s_min[2];
     __shared__ uint32_t s_q0;
@@ -732,6 +838,84 @@ __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
         st = WalkState{0, 0, 0, span, kWalkMaxR, stop, 0, 0, 0};
     }
     __syncthreads();
+    // phase 1: the one-shot prediction (merge_walk_abs_kernel's maps), chained
+    // from file 0 in LDS; the files it resolves are written in parallel
+    if (st.stop == 0 && a.abs_head[0] > 0) {
+        const uint32_t nwin = a.abs_head[0];
+        uint8_t *tab = lds_raw;
+        for (uint32_t i = t; i < nwin * kAbsW / 8; i += kWalkThreads)
+            reinterpret_cast<uint64_t *>(tab)[i] = reinterpret_cast<const uint64_t *>(a.abs_succ)[i];
+        for (uint32_t i = t; i < 2 * nwin; i += kWalkThreads) s_bases[i] = a.abs_bases[i];
+        const uint32_t x0 = a.abs_head[1];
+        __syncthreads();
+        if (t == 0) {
+            uint32_t x = x0, f = 0;
+            while (x < kAbsW) {  // file f ends at plateau base(f) + x
+                s_chosen[f++] = (uint8_t)x;
+                if (f == nwin || s_bases[2 * (f - 1) + 1] != s_bases[2 * f]) {
+                    x = kAbsMiss;  // no map past the last window (or not the window it was mapped into)
+                    break;
+                }
+                x = tab[(f - 1) * kAbsW + x];
+            }
+            s_nres = f;
+            s_code = x;
+        }
+        __syncthreads();
+        const uint32_t nres = s_nres, code = s_code;
+        // thread f: file f's start (after file f - 1's end) and, for f < nres, its end
+        uint64_t nw = 0, es = 0, Ps = 0;
+        uint32_t pf = 0, wposf = kNone, wpermf = 0;
+        if (t <= nres && t > 0) {
+            es = s_bases[2 * (t - 1)] + s_chosen[t - 1];
+            Ps = a.cand_pn[es - 1];
+            uint64_t tg;
+            walk_file(Ps, a.cand_pos[es - 1], a.cand_ext[es - 1], false, n, T, tail.s, pf, wposf, wpermf, tg);
+        }
+        if (t < nres) nw = (wposf != kNone ? 1 : 0) + (s_bases[2 * t] + s_chosen[t] - es);
+        else if (t == nres && code == kAbsLast) nw = (wposf != kNone ? 1 : 0) + (tail.c - es);  // the rest fits
+        uint64_t wt;
+        const uint64_t wex = wave_excl_scan64(nw, &wt);
+        const uint64_t wm = wave_max64(nw);
+        if (lane == 0) {
+            s_wsum[wave] = wt;
+            s_wmax[wave] = wm;
+        }
+        __syncthreads();
+        uint64_t pre = 0, tot = 0, most = 0;
+        for (uint32_t w = 0; w < kWalkThreads / kWave; w++) {
+            pre += w < wave ? s_wsum[w] : 0;
+            tot += s_wsum[w];
+            most = s_wmax[w] > most ? s_wmax[w] : most;
+        }
+        const uint64_t o = pre + wex;
+        if (nw) {
+            a.files[t] = MergeFile{pf, wposf, o};
+            if (wposf != kNone) a.out[o] = wpermf;
+        }
+        if (t == nres && nres > 0) {  // the rounds go on from file nres's start
+            WalkState x = st;
+            x.p = pf;
+            x.e = (uint32_t)es;
+            x.P = Ps;
+            x.nf = nres + (nw ? 1 : 0);
+            x.o = tot;
+            x.most = most;
+            x.span = (uint32_t)((es + nres / 2) / nres);
+            if (x.span == 0) x.span = 1;
+            x.stop = code == kAbsLast || code == kAbsStop ? 1u : code == kAbsGeneral ? 2u : 0u;
+            if (x.p >= n) x.stop = 1;
+            st = x;
+        } else if (t == 0 && nres == 0 && code == kAbsLast) {  // one file holds everything
+            WalkState x = st;
+            x.nf = nw ? 1 : 0;
+            x.o = tot;
+            x.most = most;
+            x.stop = 1;
+            st = x;
+        }
+        __syncthreads();
+    }
     for (;;) {
         WalkState S0 = st;
         // every pass writes a file or hands the next one to the general step,
@@ -1272,6 +1456,9 @@ struct MergeWs {
     uint64_t *stats;  // [0..1] counts, then the long-key OR/AND words
     uint64_t *part;   // kStatBlocks * kStatWords
     uint64_t *xinfo;  // n: merge_flags_kernel's per-pair words for the walk's extras
+    uint8_t *abs_succ;    // the walk's one-shot prediction (merge_walk_abs_kernel)
+    uint64_t *abs_bases;
+    uint32_t *abs_head;
     void *sort_tmp;
     size_t sort_bytes;
     size_t total;
@@ -1308,6 +1495,9 @@ MergeWs merge_ws_layout(uint8_t *base, uint32_t n) {
     w.stats = reinterpret_cast<uint64_t *>(take(8 * (2 + 2 * (size_t)kMaxChunks)));
     w.part = reinterpret_cast<uint64_t *>(take(8 * (size_t)kStatBlocks * kStatWords));
     w.xinfo = reinterpret_cast<uint64_t *>(take(8 * nn));
+    w.abs_succ = take((size_t)kAbsMaxWin * kAbsW);
+    w.abs_bases = reinterpret_cast<uint64_t *>(take(16 * (size_t)kAbsMaxWin));
+    w.abs_head = reinterpret_cast<uint32_t *>(take(8));
     w.sort_bytes = sort_tmp_bytes(n);
     w.sort_tmp = take(w.sort_bytes);
     w.total = at;
@@ -1604,7 +1794,10 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     uint32_t *cand_pos = w.perm[cur ^ 1];
     hipLaunchKernelGGL(merge_scan_apply, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
                        w.scan_part, w.sc, w.flags, m, perm, w.xinfo, cand_pn, cand_pos, cand_ext);
-    WalkArgs wa{m, perm, w.flags, w.sc, cand_pn, cand_pos, cand_ext, threshold, w.files, d_out, w.stats};
+    const AbsArgs aa{cand_pn, cand_pos, cand_ext, w.sc, N, threshold, w.abs_succ, w.abs_bases, w.abs_head};
+    hipLaunchKernelGGL(merge_walk_abs_kernel, dim3(kAbsMaxWin), dim3(kAbsThreads), 0, s, aa);
+    WalkArgs wa{m, perm, w.flags, w.sc, cand_pn, cand_pos, cand_ext, w.abs_succ, w.abs_bases, w.abs_head,
+                threshold, w.files, d_out, w.stats};
     hipLaunchKernelGGL(merge_walk_kernel, dim3(1), dim3(kWalkThreads), 0, s, wa);
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
                        w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);
