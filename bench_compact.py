@@ -83,6 +83,7 @@ def bench_compact(args, world, rank, local):
     mg = lsmgpu.alloc_merge(ctx, n)
     stream = torch.cuda.current_stream()
     ev_names = ("decode", "join", "merge", "gather", "build")
+    keep = {}  # the gather's and the build's buffers, allocated by the first step
 
     def step(evs=None):
         def mark(i):
@@ -97,10 +98,11 @@ def bench_compact(args, world, rank, local):
         mark(3)
         # keys packed; values read in place by the build (no second copy)
         batch = lsmgpu.gather_kvs(ctx, img, kd, vd, mg.out, mg.nout, key_bytes, None,
-                                  stream=stream)
+                                  stream=stream, reuse=keep.get("batch"))
         mark(4)
         sb = lsmgpu.prepare_sst_device(ctx, batch, mg.file_start, mg.nfiles, mg.max_recs,
-                                       val_bytes=val_bytes, stream=stream)
+                                       val_bytes=val_bytes, stream=stream, reuse=keep.get("sb"))
+        keep["batch"], keep["sb"] = batch, sb
         lsmgpu.build_sst_views_into(ctx, batch, sb, img, kd, vd, mg.out, stream=stream)
         mark(5)
         return sb, batch

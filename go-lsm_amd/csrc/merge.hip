@@ -533,19 +533,27 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scan_tiles(const uint32_t
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
+// one pass over the tile sums (see plan_scan_partials): a contiguous stretch
+// per thread, one block scan of the stretch sums
 __global__ __launch_bounds__(kMergeThreads) void merge_scan_partials(SumPair *part, uint32_t ntiles,
                                                                      SumPair *sc, uint32_t n) {
-    SumPair carry{0, 0};
-    for (uint32_t t0 = 0; t0 < ntiles; t0 += kMergeThreads) {
-        const uint32_t t = t0 + threadIdx.x;
-        const SumPair v = t < ntiles ? part[t] : SumPair{0, 0};
-        SumPair tot;
-        const SumPair x = block_excl_scan2(v.s, v.c, &tot);
-        if (t < ntiles) part[t] = SumPair{carry.s + x.s, carry.c + x.c};
-        carry.s += tot.s;
-        carry.c += tot.c;
+    const uint32_t per = (ntiles + kMergeThreads - 1) / kMergeThreads, b = threadIdx.x * per;
+    const uint32_t e = b + per < ntiles ? b + per : ntiles;
+    uint64_t s = 0, c = 0;
+    for (uint32_t i = b; i < e; i++) {
+        const SumPair v = part[i];
+        s += v.s;
+        c += v.c;
     }
-    if (threadIdx.x == 0) sc[n] = carry;
+    SumPair tot;
+    SumPair pre = block_excl_scan2(s, c, &tot);
+    for (uint32_t i = b; i < e; i++) {
+        const SumPair v = part[i];
+        part[i] = pre;
+        pre.s += v.s;
+        pre.c += v.c;
+    }
+    if (threadIdx.x == 0) sc[n] = tot;
 }
 
 // The sums per position, and per candidate c (the walk's plateau space, see

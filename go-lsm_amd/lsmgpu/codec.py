@@ -721,30 +721,40 @@ def goheap_pop_order(ctx_or_lib, rank: np.ndarray) -> np.ndarray:
 
 def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
                val_desc: Optional[torch.Tensor], idx: torch.Tensor, nout: int,
-               key_bytes: int, val_bytes: int, stream=None) -> RecordBatch:
+               key_bytes: int, val_bytes: int, stream=None,
+               reuse: Optional[RecordBatch] = None) -> RecordBatch:
     """The selected pairs as a device CSR batch (lsm_build_sst's input);
     key_bytes / val_bytes bound the selected bytes.  koff_host / voff_host
-    are left None (use sst_layout for the image sizes)."""
+    are left None (use sst_layout for the image sizes).  reuse: an earlier
+    result whose buffers are large enough is written again (a compaction
+    loop allocates once)."""
     dev = ctx.torch_device
-    keys = torch.empty(pad16(max(key_bytes, 1)), dtype=torch.uint8, device=dev)
-    vals = (torch.empty(pad16(max(val_bytes, 1)), dtype=torch.uint8, device=dev)
-            if val_bytes is not None else None)  # None: keys only (build_sst_views_into)
-    koff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
-    voff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
-    ws = torch.empty(int(ctx.lib.lsm_gather_kvs_workspace_bytes(nout)), dtype=torch.uint8,
-                     device=dev)
+    kb, vb = pad16(max(key_bytes, 1)), (pad16(max(val_bytes, 1)) if val_bytes is not None else None)
+    wsb = int(ctx.lib.lsm_gather_kvs_workspace_bytes(nout))
+    if (reuse is not None and reuse.koff.numel() >= nout + 1 and reuse.keys.numel() >= kb and
+            (vb is None) == (reuse.vals is None) and (vb is None or reuse.vals.numel() >= vb) and
+            getattr(reuse, "_ws", None) is not None and reuse._ws.numel() >= wsb):
+        keys, vals, koff, voff, ws = reuse.keys, reuse.vals, reuse.koff, reuse.voff, reuse._ws
+    else:
+        keys = torch.empty(kb, dtype=torch.uint8, device=dev)
+        vals = torch.empty(vb, dtype=torch.uint8, device=dev) if vb is not None else None
+        koff = torch.empty(nout + 1, dtype=torch.int64, device=dev)  # vals None: keys only
+        voff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     _lib.check(ctx.lib.lsm_gather_kvs(
         ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), _ptr(idx), nout, _ptr(keys),
         _ptr(koff), _ptr(vals), _ptr(voff), _ptr(ws), ws.numel(), _stream_handle(stream)),
         "lsm_gather_kvs")
-    return RecordBatch(keys=keys, koff=koff, vals=vals, voff=voff, n=nout, koff_host=None,
-                       voff_host=None)
+    out = RecordBatch(keys=keys, koff=koff, vals=vals, voff=voff, n=nout, koff_host=None,
+                      voff_host=None)
+    out._ws = ws
+    return out
 
 
 def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Tensor, nfile: int,
                        max_recs: int, val_bytes: Optional[int] = None,
                        m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K,
-                       align: int = 16, stream=None) -> "SstBuild":
+                       align: int = 16, stream=None, reuse: Optional["SstBuild"] = None) -> "SstBuild":
     """prepare_sst for a device-resident batch (a merge's output): the layout
     by lsm_sst_layout on the device, nothing read back.  max_recs = the merge's
     most pairs per file (Merge.max_recs); the image buffer is sized from the
@@ -758,16 +768,24 @@ def prepare_sst_device(ctx: Context, batch: RecordBatch, d_file_start: torch.Ten
     fbytes = int(ctx.lib.lsm_filter_block_size(m))
     bound = (nfile * (fbytes + 40 + align - 1) + 16 * batch.n + 3 * int(batch.keys.numel()) +
              int(val_bytes))
-    d_size = torch.empty(max(nfile, 1), dtype=torch.int64, device=dev)
-    d_off = torch.empty(nfile + 1, dtype=torch.int64, device=dev)
+    if reuse is not None and reuse.nfile == nfile:
+        d_size, d_off = reuse.d_file_size, reuse.d_file_off
+    else:
+        d_size = torch.empty(max(nfile, 1), dtype=torch.int64, device=dev)
+        d_off = torch.empty(nfile + 1, dtype=torch.int64, device=dev)
     _lib.check(ctx.lib.lsm_sst_layout(
         ctx.handle, _ptr(batch.koff), _ptr(batch.voff), _ptr(d_file_start), nfile, m, align,
         _ptr(d_size), _ptr(d_off), _stream_handle(stream)), "lsm_sst_layout")
     ws_bytes = int(ctx.lib.lsm_build_sst_workspace_bytes(nfile, max_recs, m, k))
-    return SstBuild(  # every image byte is written by lsm_build_sst: no fill
-        out=torch.empty(pad16(bound), dtype=torch.uint8, device=dev),
-        footer=torch.zeros(max(nfile, 1) * 4, dtype=torch.int64, device=dev),
-        workspace=torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
+    if (reuse is not None and reuse.out.numel() >= pad16(bound) and reuse.footer.numel() >= nfile * 4
+            and reuse.workspace.numel() >= ws_bytes):  # reuse: an earlier build's buffers
+        out, footer, workspace = reuse.out, reuse.footer, reuse.workspace
+    else:  # every image byte and every footer word is written by the build: no fill
+        out = torch.empty(pad16(bound), dtype=torch.uint8, device=dev)
+        footer = torch.empty(max(nfile, 1) * 4, dtype=torch.int64, device=dev)
+        workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    return SstBuild(
+        out=out, footer=footer, workspace=workspace,
         d_file_start=d_file_start[:nfile + 1], d_file_off=d_off, d_file_size=d_size,
         max_recs=max_recs, m=m, k=k, nfile=nfile,
         stream=stream if stream is not None else torch.cuda.current_stream(dev))
