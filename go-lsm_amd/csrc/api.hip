@@ -30,6 +30,7 @@ extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(&c->host_rb, kHostReadback, hipHostMallocDefault);
     if (e != hipSuccess) {
         lsm_ctx_destroy(c);
         return -(1000 + (int)e);
@@ -44,6 +45,7 @@ extern "C" int lsm_ctx_destroy(lsm_ctx *ctx) {
         if (ctx->join) (void)hipEventDestroy(ctx->join);
         if (ctx->fork) (void)hipEventDestroy(ctx->fork);
         if (ctx->side) (void)hipStreamDestroy(ctx->side);
+        if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
     }
     free(ctx);
     return 0;

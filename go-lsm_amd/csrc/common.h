@@ -16,12 +16,17 @@
 // its CU count, and a side stream with fork / join events for a call that
 // runs two independent kernels at once (lsm_build_sst: the VALU-bound filters
 // beside the HBM-bound regions, co-resident on the CUs).
+// It also owns a small pinned host buffer for the merge's read-backs (its key
+// statistics and counts): a copy into pageable memory goes through a staging
+// handshake that left 25-55 us idle gaps around each read-back.
 struct lsm_ctx {
     int device;
     int num_cus;
     hipStream_t side;
     hipEvent_t fork, join;
+    void *host_rb;  // kHostReadback bytes of pinned host memory
 };
+constexpr size_t kHostReadback = 256 * 1024;
 
 namespace lsm {
 

@@ -914,22 +914,45 @@ __global__ __launch_bounds__(kScanThreads) void plan_tile_sums(int mode, const u
     if (threadIdx.x == 0) partial[blockIdx.x] = tot;
 }
 
-// one pass over the tile sums: each thread a contiguous stretch of them (all
-// its loads in flight), one block scan of the stretch sums (a loop of block
-// scans over 256-tile chunks took 16 us for 6,400 tiles: a round trip each)
-__global__ __launch_bounds__(kScanThreads) void plan_scan_partials(uint64_t *partial,
+// one pass over the tile sums by 1,024 threads: each a contiguous stretch of
+// them (its loads in flight together), one block scan of the stretch sums (a
+// loop of 256-thread block scans over 256-tile chunks took 16 us for 6,400
+// tiles: a round trip per chunk)
+constexpr uint32_t kPartThreads = 1024;
+
+__global__ __launch_bounds__(kPartThreads) void plan_scan_partials(uint64_t *partial,
                                                                    uint32_t ntiles, uint64_t *out,
                                                                    uint32_t n) {
-    const uint32_t per = (ntiles + kScanThreads - 1) / kScanThreads, b = threadIdx.x * per;
+    __shared__ uint64_t wsum[kPartThreads / kWave];
+    const uint32_t per = (ntiles + kPartThreads - 1) / kPartThreads, b = threadIdx.x * per;
     const uint32_t e = b + per < ntiles ? b + per : ntiles;
     uint64_t s = 0;
-    for (uint32_t i = b; i < e; i++) s += partial[i];
-    uint64_t tot;
-    uint64_t pre = block_excl_scan(s, &tot);
-    for (uint32_t i = b; i < e; i++) {
-        const uint64_t v = partial[i];
-        partial[i] = pre;
-        pre += v;
+    for (uint32_t i0 = b; i0 < e; i0 += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) v[k] = i0 + k < e ? partial[i0 + k] : 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) s += v[k];
+    }
+    uint64_t wt;
+    const uint64_t wx = wave_excl_scan64(s, &wt);
+    const uint32_t w = threadIdx.x / kWave;
+    if (lane_id() == 0) wsum[w] = wt;
+    __syncthreads();
+    uint64_t pre = wx, tot = 0;
+    for (uint32_t i = 0; i < kPartThreads / kWave; i++) {
+        pre += i < w ? wsum[i] : 0;
+        tot += wsum[i];
+    }
+    for (uint32_t i0 = b; i0 < e; i0 += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) v[k] = i0 + k < e ? partial[i0 + k] : 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            if (i0 + k < e) partial[i0 + k] = pre;
+            pre += v[k];
+        }
     }
     if (threadIdx.x == 0) out[n] = tot;
 }
@@ -965,7 +988,7 @@ int plan_scan(int mode, const uint32_t *d_len, uint32_t n, uint64_t *d_out, void
     }
     hipLaunchKernelGGL(plan_tile_sums, dim3(ntiles), dim3(kScanThreads), 0, s, mode, d_len, n,
                        partial);
-    hipLaunchKernelGGL(plan_scan_partials, dim3(1), dim3(kScanThreads), 0, s, partial, ntiles,
+    hipLaunchKernelGGL(plan_scan_partials, dim3(1), dim3(kPartThreads), 0, s, partial, ntiles,
                        d_out, n);
     hipLaunchKernelGGL(plan_tile_apply, dim3(ntiles), dim3(kScanThreads), 0, s, mode, d_len, n,
                        partial, d_out);

@@ -533,25 +533,53 @@ __global__ __launch_bounds__(kMergeThreads) void merge_scan_tiles(const uint32_t
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-// one pass over the tile sums (see plan_scan_partials): a contiguous stretch
-// per thread, one block scan of the stretch sums
-__global__ __launch_bounds__(kMergeThreads) void merge_scan_partials(SumPair *part, uint32_t ntiles,
-                                                                     SumPair *sc, uint32_t n) {
-    const uint32_t per = (ntiles + kMergeThreads - 1) / kMergeThreads, b = threadIdx.x * per;
+// one pass over the tile sums by 1,024 threads (see plan_scan_partials): a
+// contiguous stretch per thread, one block scan of the stretch sums
+constexpr uint32_t kPartThreads = 1024;
+
+__global__ __launch_bounds__(kPartThreads) void merge_scan_partials(SumPair *part, uint32_t ntiles,
+                                                                    SumPair *sc, uint32_t n) {
+    __shared__ uint64_t ws_[kPartThreads / kWave], wc_[kPartThreads / kWave];
+    const uint32_t per = (ntiles + kPartThreads - 1) / kPartThreads, b = threadIdx.x * per;
     const uint32_t e = b + per < ntiles ? b + per : ntiles;
     uint64_t s = 0, c = 0;
-    for (uint32_t i = b; i < e; i++) {
-        const SumPair v = part[i];
-        s += v.s;
-        c += v.c;
+    for (uint32_t i0 = b; i0 < e; i0 += 8) {  // 8 loads in flight
+        SumPair v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) v[k] = i0 + k < e ? part[i0 + k] : SumPair{0, 0};
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            s += v[k].s;
+            c += v[k].c;
+        }
     }
-    SumPair tot;
-    SumPair pre = block_excl_scan2(s, c, &tot);
-    for (uint32_t i = b; i < e; i++) {
-        const SumPair v = part[i];
-        part[i] = pre;
-        pre.s += v.s;
-        pre.c += v.c;
+    uint64_t ts, tc;
+    const uint64_t xs = wave_excl_scan64(s, &ts), xc = wave_excl_scan64(c, &tc);
+    const uint32_t w = threadIdx.x / kWave;
+    if (lane_id() == 0) {
+        ws_[w] = ts;
+        wc_[w] = tc;
+    }
+    __syncthreads();
+    SumPair pre{xs, xc}, tot{0, 0};
+    for (uint32_t i = 0; i < kPartThreads / kWave; i++) {
+        if (i < w) {
+            pre.s += ws_[i];
+            pre.c += wc_[i];
+        }
+        tot.s += ws_[i];
+        tot.c += wc_[i];
+    }
+    for (uint32_t i0 = b; i0 < e; i0 += 8) {
+        SumPair v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) v[k] = i0 + k < e ? part[i0 + k] : SumPair{0, 0};
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            if (i0 + k < e) part[i0 + k] = pre;
+            pre.s += v[k].s;
+            pre.c += v[k].c;
+        }
     }
     if (threadIdx.x == 0) sc[n] = tot;
 }
@@ -1644,8 +1672,9 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     //    tiles, per-tile partials reduced here
     const uint32_t chunk = (N + sb - 1) / sb;
     hipLaunchKernelGGL(merge_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, chunk, w.part);
-    std::vector<uint64_t> part((size_t)sb * kStatWords);
-    LSM_HIP_CHECK(hipMemcpyAsync(part.data(), w.part, part.size() * 8, hipMemcpyDeviceToHost, s));
+    static_assert((size_t)kStatBlocks * kStatWords * 8 + 64 <= kHostReadback, "read-back buffer");
+    const uint64_t *part = static_cast<const uint64_t *>(ctx->host_rb);  // pinned
+    LSM_HIP_CHECK(hipMemcpyAsync(ctx->host_rb, w.part, (size_t)sb * kStatWords * 8, hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
     uint64_t st[kStatCore];
     for (uint32_t t = 0; t < kStatCore; t++) st[t] = part[t];
@@ -1795,7 +1824,7 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     const uint32_t ntiles = (N + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(merge_scan_tiles, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
                        w.scan_part);
-    hipLaunchKernelGGL(merge_scan_partials, dim3(1), dim3(kMergeThreads), 0, s, w.scan_part, ntiles,
+    hipLaunchKernelGGL(merge_scan_partials, dim3(1), dim3(kPartThreads), 0, s, w.scan_part, ntiles,
                        w.sc, N);
     // the walk's plateau arrays in the sort's buffers, free from here on
     uint64_t *cand_pn = w.keys[0], *cand_ext = w.keys[1];
@@ -1810,8 +1839,8 @@ extern "C" int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes,
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
                        w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);
     LSM_HIP_CHECK(hipGetLastError());
-    uint64_t c3[3];
-    LSM_HIP_CHECK(hipMemcpyAsync(c3, w.stats, sizeof c3, hipMemcpyDeviceToHost, s));
+    uint64_t *c3 = static_cast<uint64_t *>(ctx->host_rb);  // pinned
+    LSM_HIP_CHECK(hipMemcpyAsync(c3, w.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
     for (int i = 0; i < 3; i++) h_counts[i] = c3[i];
     return 0;
