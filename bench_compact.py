@@ -84,6 +84,11 @@ def bench_compact(args, world, rank, local):
     stream = torch.cuda.current_stream()
     ev_names = ("decode", "join", "merge", "gather", "build")
     keep = {}  # the gather's and the build's buffers, allocated by the first step
+    # the merge's counts stay on the device (lsm_merge_kvs_async): the gather
+    # runs on the device count while the host reads it (pinned, one event)
+    d_counts = torch.zeros(3, dtype=torch.int64, device=ctx.torch_device)
+    h_counts = torch.zeros(3, dtype=torch.int64, pin_memory=True)
+    counted = torch.cuda.Event()
 
     def step(evs=None):
         def mark(i):
@@ -94,11 +99,16 @@ def bench_compact(args, world, rank, local):
         mark(1)
         lsmgpu.sst_pairs_into(ctx, r, kd, vd, prefix, stream=stream)
         mark(2)
-        lsmgpu.merge_kvs_into(ctx, img, kd, vd, mg, level=1, stream=stream)
+        lsmgpu.merge_kvs_into(ctx, img, kd, vd, mg, level=1, stream=stream, d_counts=d_counts)
+        h_counts.copy_(d_counts, non_blocking=True)
+        counted.record(stream)
         mark(3)
         # keys packed; values read in place by the build (no second copy)
-        batch = lsmgpu.gather_kvs(ctx, img, kd, vd, mg.out, mg.nout, key_bytes, None,
-                                  stream=stream, reuse=keep.get("batch"))
+        batch = lsmgpu.gather_kvs(ctx, img, kd, vd, mg.out, n, key_bytes, None,
+                                  stream=stream, reuse=keep.get("batch"), d_nout=d_counts)
+        counted.synchronize()  # while the gather runs
+        mg.nout, mg.nfiles, mg.max_recs = (int(x) for x in h_counts.tolist())
+        batch.n = mg.nout
         mark(4)
         sb = lsmgpu.prepare_sst_device(ctx, batch, mg.file_start, mg.nfiles, mg.max_recs,
                                        val_bytes=val_bytes, stream=stream, reuse=keep.get("sb"))

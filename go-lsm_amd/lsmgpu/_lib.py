@@ -116,11 +116,19 @@ SIGNATURES = {
                                          ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_int, ctypes.c_void_p, c_u64p, c_u64p,
                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_merge_kvs_async": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64,
+                                           ctypes.c_int, ctypes.c_void_p, c_u64p, c_u64p,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "lsm_goheap_pop_order_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "lsm_gather_kvs_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint64]),
     "lsm_gather_kvs": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_uint64, c_u8p, c_u64p, c_u8p,
                                       c_u64p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_gather_kvs_dev": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, c_u64p, ctypes.c_uint64, c_u8p, c_u64p,
+                                          c_u8p, c_u64p, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.c_void_p]),
     "lsm_sst_image_sizes": (ctypes.c_int, [ctypes.c_void_p, c_u64p, c_u64p, c_u64p,
                                            ctypes.c_uint32, ctypes.c_uint64, c_u64p,
                                            ctypes.c_void_p]),
@@ -147,7 +155,7 @@ SIGNATURES = {
     "lsm_stream_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 4   # LSM_ABI_VERSION this binding is written against
+ABI_VERSION = 5   # LSM_ABI_VERSION this binding is written against
 INPUT_SLACK = 32  # LSM_INPUT_SLACK: device inputs are padded by this much
 
 _lib = None

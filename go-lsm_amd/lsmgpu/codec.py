@@ -689,10 +689,19 @@ TIE_INPUT, TIE_GOHEAP = 0, 1  # enum lsm_tie
 
 def merge_kvs_into(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
                    val_desc: Optional[torch.Tensor], r: Merge, level: int = 1,
-                   threshold: int = MAX_SSTABLE_SIZE, stream=None, tie: int = TIE_INPUT) -> Merge:
+                   threshold: int = MAX_SSTABLE_SIZE, stream=None, tie: int = TIE_INPUT,
+                   d_counts: Optional[torch.Tensor] = None) -> Merge:
     """CompactAndMergeKVs (merge.go:42-94) over pairs given as descriptors
     (key: IDX/KV descriptor, value: V descriptor or None for KV records).
-    tie=TIE_GOHEAP: equal keys in container/heap's pop order (exact)."""
+    tie=TIE_GOHEAP: equal keys in container/heap's pop order (exact).
+    d_counts (device int64[3]): lsm_merge_kvs_async -- the counts are left
+    there, not read back (r.nout / nfiles / max_recs are not set)."""
+    if d_counts is not None:
+        _lib.check(ctx.lib.lsm_merge_kvs_async(
+            ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), r.n, level, threshold, tie,
+            _ptr(r.out), _ptr(r.file_start), _ptr(d_counts), _ptr(r.workspace),
+            r.workspace.numel(), _stream_handle(stream)), "lsm_merge_kvs_async")
+        return r
     counts = np.zeros(3, np.uint64)
     _lib.check(ctx.lib.lsm_merge_kvs_tie(
         ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), r.n, level, threshold, tie,
@@ -722,7 +731,7 @@ def goheap_pop_order(ctx_or_lib, rank: np.ndarray) -> np.ndarray:
 def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
                val_desc: Optional[torch.Tensor], idx: torch.Tensor, nout: int,
                key_bytes: int, val_bytes: int, stream=None,
-               reuse: Optional[RecordBatch] = None) -> RecordBatch:
+               reuse: Optional[RecordBatch] = None, d_nout: Optional[torch.Tensor] = None) -> RecordBatch:
     """The selected pairs as a device CSR batch (lsm_build_sst's input);
     key_bytes / val_bytes bound the selected bytes.  koff_host / voff_host
     are left None (use sst_layout for the image sizes).  reuse: an earlier
@@ -741,10 +750,16 @@ def gather_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
         koff = torch.empty(nout + 1, dtype=torch.int64, device=dev)  # vals None: keys only
         voff = torch.empty(nout + 1, dtype=torch.int64, device=dev)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    _lib.check(ctx.lib.lsm_gather_kvs(
-        ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), _ptr(idx), nout, _ptr(keys),
-        _ptr(koff), _ptr(vals), _ptr(voff), _ptr(ws), ws.numel(), _stream_handle(stream)),
-        "lsm_gather_kvs")
+    if d_nout is not None:  # lsm_gather_kvs_dev: the count on the device, nout its bound
+        _lib.check(ctx.lib.lsm_gather_kvs_dev(
+            ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), _ptr(idx), _ptr(d_nout), nout,
+            _ptr(keys), _ptr(koff), _ptr(vals), _ptr(voff), _ptr(ws), ws.numel(),
+            _stream_handle(stream)), "lsm_gather_kvs_dev")
+    else:
+        _lib.check(ctx.lib.lsm_gather_kvs(
+            ctx.handle, _ptr(d_bytes), _ptr(key_desc), _ptr(val_desc), _ptr(idx), nout, _ptr(keys),
+            _ptr(koff), _ptr(vals), _ptr(voff), _ptr(ws), ws.numel(), _stream_handle(stream)),
+            "lsm_gather_kvs")
     out = RecordBatch(keys=keys, koff=koff, vals=vals, voff=voff, n=nout, koff_host=None,
                       voff_host=None)
     out._ws = ws

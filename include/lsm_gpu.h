@@ -33,8 +33,10 @@ extern "C" {
 /* v3: the input slack grew from 16 to 32 bytes (a binding built for v2 pads
  * too little); lsm_input_slack() reports it at run time.
  * v4: lsm_merge_kvs_tie writes 3 h_counts entries; lsm_merge_kvs keeps the
- * v2 / v3 contract of exactly 2 ({nout, nfiles}). */
-#define LSM_ABI_VERSION 4
+ * v2 / v3 contract of exactly 2 ({nout, nfiles}).
+ * v5: lsm_merge_kvs_async and lsm_gather_kvs_dev (the merge's counts stay on
+ * the device; the gather reads its pair count there). */
+#define LSM_ABI_VERSION 5
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
 /* Record grammars (all fixed-width little-endian). */
@@ -429,6 +431,16 @@ int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_ke
                   const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
                   uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts, void *d_ws,
                   size_t ws_bytes, void *stream);
+/* lsm_merge_kvs_tie without its closing read-back (ABI 5): the counts {nout,
+ * nfiles, the most pairs in one file} go to d_counts (device, 3 entries) and
+ * the call returns with the file walk and the emit still queued.  The
+ * key-statistics read-back that picks the radix passes stays (and, for
+ * LSM_TIE_GOHEAP, the host replay).  A compaction reads d_counts while its
+ * gather (lsm_gather_kvs_dev) runs: the stream does not idle for the read. */
+int lsm_merge_kvs_async(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                        const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
+                        int tie, uint32_t *d_out, uint64_t *d_file_start, uint64_t *d_counts,
+                        void *d_ws, size_t ws_bytes, void *stream);
 
 /* The selected pairs d_idx[0 .. nout) as a CSR record batch -- the input of
  * lsm_build_sst: keys packed into d_keys with d_koff[0 .. nout], values into
@@ -440,6 +452,14 @@ int lsm_gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_k
                    const lsm_rec_desc *d_val_desc, const uint32_t *d_idx, uint64_t nout,
                    uint8_t *d_keys, uint64_t *d_koff, uint8_t *d_vals, uint64_t *d_voff,
                    void *d_ws, size_t ws_bytes, void *stream);
+/* lsm_gather_kvs with the pair count on the device (ABI 5): nout = *d_nout
+ * (lsm_merge_kvs_async's d_counts[0]), at most nout_max, which sizes the
+ * launches, the workspace (lsm_gather_kvs_workspace_bytes(nout_max)) and
+ * d_koff / d_voff (nout_max + 1 entries).  Asynchronous. */
+int lsm_gather_kvs_dev(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
+                       const lsm_rec_desc *d_val_desc, const uint32_t *d_idx, const uint64_t *d_nout,
+                       uint64_t nout_max, uint8_t *d_keys, uint64_t *d_koff, uint8_t *d_vals,
+                       uint64_t *d_voff, void *d_ws, size_t ws_bytes, void *stream);
 
 /* The positional join of decoded files in file order -- loadLevelData's
  * allPairs (compaction.go:173-193) over GetKeyValuePairs (sstable.go:248-268):

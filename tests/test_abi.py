@@ -31,7 +31,7 @@ def test_header_functions_exported():
 
 
 def test_abi_version():
-    assert _lib.load().lsm_abi_version() == 4
+    assert _lib.load().lsm_abi_version() == 5
     assert _lib.load().lsm_input_slack() == 32
 
 

@@ -418,3 +418,42 @@ def test_merge_path_one_long_run(ctx, tie, shape):
     for level in (1, 6):
         for thr in (MiB2, 4000, 257):
             run(ctx, pairs, level, thr, seed=level, tie=tie)
+
+
+@pytest.mark.parametrize("tie", TIES)
+def test_async_merge_and_device_count_gather(ctx, tie):
+    """lsm_merge_kvs_async (counts left on the device) + lsm_gather_kvs_dev
+    (the gather on that device count, launched on a bound) equal the
+    read-back forms: the same written pairs, file starts and counts, and the
+    same packed keys, values and offsets."""
+    rng = random.Random(31 + tie)
+    pairs = random_pairs(rng, 6000, b"abc\x00", 9)
+    buf, kd, vd, kpos, vpos = lay_out(pairs, False, random.Random(5))
+    dev = ctx.torch_device
+    d_buf = lsmgpu.to_device_bytes(buf, dev)
+    d_kd = torch.from_numpy(kd.view(np.int32).reshape(-1, 4).copy()).to(dev)
+    d_vd = torch.from_numpy(vd.view(np.int32).reshape(-1, 4).copy()).to(dev)
+    n = len(pairs)
+    for level, threshold in ((1, 900), (6, 4000), (1, MiB2)):
+        want = lsmgpu.merge_kvs(ctx, d_buf, d_kd, d_vd, level=level, threshold=threshold, tie=tie)
+        got = lsmgpu.alloc_merge(ctx, n)
+        d_counts = torch.full((3,), -1, dtype=torch.int64, device=dev)
+        lsmgpu.merge_kvs_into(ctx, d_buf, d_kd, d_vd, got, level=level, threshold=threshold,
+                              tie=tie, d_counts=d_counts)
+        torch.cuda.synchronize()
+        cnt = d_counts.cpu().tolist()
+        assert cnt == [want.nout, want.nfiles, want.max_recs], (level, threshold)
+        assert torch.equal(got.out[:want.nout], want.out[:want.nout])
+        assert torch.equal(got.file_start[:want.nfiles + 1], want.file_start[:want.nfiles + 1])
+        kb = buf.size + 64  # the input's bytes bound the selected keys and values
+        for vb in (None, buf.size + 64):
+            a = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, want.out, want.nout, kb, vb)
+            b = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, got.out, n, kb, vb, d_nout=d_counts)
+            torch.cuda.synchronize()
+            m = want.nout
+            assert torch.equal(a.koff[:m + 1], b.koff[:m + 1]) and torch.equal(a.voff[:m + 1], b.voff[:m + 1])
+            kbytes = int(a.koff[m])
+            assert torch.equal(a.keys[:kbytes], b.keys[:kbytes])
+            if vb is not None:
+                vbytes = int(a.voff[m])
+                assert torch.equal(a.vals[:vbytes], b.vals[:vbytes])
