@@ -2988,6 +2988,32 @@ extern "C" size_t lsm_level_may_contain_workspace_bytes(uint32_t nfile, uint64_t
     return total;
 }
 
+// The search over an index whose table array is `files` (lsm_level_index_build
+// output, or the workspace's own copy built just before).
+static int level_search(hipStream_t s, const uint8_t *d_img, const McFile *files, uint32_t nfile,
+                        const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
+                        int32_t *d_table, uint8_t *d_may, LvWs w) {
+    w.files = const_cast<McFile *>(files);
+    if (nfile > kLvMaxFiles || nkeys > 0xFFFFFFFFull) {
+        const uint64_t g = (nkeys + 255) / 256;
+        hipLaunchKernelGGL(lv_probe_kernel, dim3(g < 4096 ? (uint32_t)g : 4096u), dim3(256), 0, s,
+                           d_img, nfile, d_keys, d_koff, nkeys, w, d_table, d_may);
+    } else {
+        // passes of up to 2M probes (the test kernel's segment table)
+        const uint64_t pass = (uint64_t)kLvMaxWgs * kLvProbes;
+        for (uint64_t k0 = 0; k0 < nkeys; k0 += pass) {
+            const uint64_t n = nkeys - k0 < pass ? nkeys - k0 : pass;
+            const uint32_t nwg = (uint32_t)((n + kLvProbes - 1) / kLvProbes);
+            hipLaunchKernelGGL(lv_classify_kernel, dim3(nwg), dim3(kLvThreads), 0, s, d_img, nfile,
+                               d_keys, d_koff, k0, k0 + n, w, nwg, d_table, d_may);
+            hipLaunchKernelGGL(lv_test_kernel, dim3(nfile), dim3(kLvThreads), kMcLdsBytes, s, d_img,
+                               nfile, nwg, w, k0, d_may);
+        }
+    }
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 extern "C" int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
                                      const lsm_sst_meta *d_meta, uint32_t nfile,
                                      const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
@@ -3008,24 +3034,47 @@ extern "C" int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const u
     if (ws_bytes < need) return LSM_ESPACE;
     hipLaunchKernelGGL(lv_prep_kernel, dim3((nfile + 255) / 256), dim3(256), 0, s, d_img, d_file_off,
                        d_meta, nfile, w);
-    if (nfile > kLvMaxFiles || nkeys > 0xFFFFFFFFull) {
-        const uint64_t g = (nkeys + 255) / 256;
-        hipLaunchKernelGGL(lv_probe_kernel, dim3(g < 4096 ? (uint32_t)g : 4096u), dim3(256), 0, s,
-                           d_img, nfile, d_keys, d_koff, nkeys, w, d_table, d_may);
-    } else {
-        // passes of up to 2M probes (the test kernel's segment table)
-        const uint64_t pass = (uint64_t)kLvMaxWgs * kLvProbes;
-        for (uint64_t k0 = 0; k0 < nkeys; k0 += pass) {
-            const uint64_t n = nkeys - k0 < pass ? nkeys - k0 : pass;
-            const uint32_t nwg = (uint32_t)((n + kLvProbes - 1) / kLvProbes);
-            hipLaunchKernelGGL(lv_classify_kernel, dim3(nwg), dim3(kLvThreads), 0, s, d_img, nfile,
-                               d_keys, d_koff, k0, k0 + n, w, nwg, d_table, d_may);
-            hipLaunchKernelGGL(lv_test_kernel, dim3(nfile), dim3(kLvThreads), kMcLdsBytes, s, d_img,
-                               nfile, nwg, w, k0, d_may);
-        }
-    }
+    return level_search(s, d_img, w.files, nfile, d_keys, d_koff, nkeys, d_table, d_may, w);
+}
+
+extern "C" size_t lsm_level_index_bytes(uint32_t nfile) {
+    return sizeof(McFile) * (size_t)(nfile ? nfile : 1);
+}
+
+extern "C" int lsm_level_index_build(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                                     const lsm_sst_meta *d_meta, uint32_t nfile, void *d_index,
+                                     void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nfile == 0) return 0;
+    if (!d_img || !d_file_off || !d_meta || !d_index) return LSM_EINVAL;
+    LvWs w{};
+    w.files = static_cast<McFile *>(d_index);
+    hipLaunchKernelGGL(lv_prep_kernel, dim3((nfile + 255) / 256), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_img, d_file_off, d_meta, nfile, w);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+extern "C" int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img, const void *d_index,
+                                             uint32_t nfile, const uint8_t *d_keys,
+                                             const uint64_t *d_koff, uint64_t nkeys, int32_t *d_table,
+                                             uint8_t *d_may, void *d_workspace, size_t ws_bytes,
+                                             void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nkeys == 0) return 0;
+    if (!d_keys || !d_koff || !d_table || !d_may) return LSM_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (nfile == 0) {
+        LSM_HIP_CHECK(hipMemsetAsync(d_table, 0xFF, 4 * nkeys, s));
+        LSM_HIP_CHECK(hipMemsetAsync(d_may, 0, nkeys, s));
+        return 0;
+    }
+    if (!d_img || !d_index || !d_workspace) return LSM_EINVAL;
+    size_t need = 0;
+    const LvWs w = lv_ws_layout(static_cast<uint8_t *>(d_workspace), nfile, nkeys, &need);
+    if (ws_bytes < need) return LSM_ESPACE;
+    return level_search(s, d_img, static_cast<const McFile *>(d_index), nfile, d_keys, d_koff, nkeys,
+                        d_table, d_may, w);
 }
 
 extern "C" int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,

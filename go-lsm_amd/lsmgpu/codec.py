@@ -454,14 +454,35 @@ def level_may_contain_workspace(ctx: Context, nfile: int, nkeys: int) -> torch.T
     return torch.empty(max(n, 16), dtype=torch.uint8, device=ctx.torch_device)
 
 
+def level_index(ctx: Context, d_img: torch.Tensor, r: SstDecode, stream=None) -> torch.Tensor:
+    """lsm_level_index_build: the level's sparse index (Manager.sparseIndexes),
+    parsed once from the decoded tables' headers; valid with this d_img."""
+    idx = torch.empty(max(int(ctx.lib.lsm_level_index_bytes(r.nfile)), 16), dtype=torch.uint8,
+                      device=ctx.torch_device)
+    if r.nfile:
+        _lib.check(ctx.lib.lsm_level_index_build(
+            ctx.handle, _ptr(d_img), _ptr(r.d_file_off), _ptr(r.meta), r.nfile, _ptr(idx),
+            _stream_handle(stream)), "lsm_level_index_build")
+    return idx
+
+
 def level_may_contain_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
                            table: torch.Tensor, may: torch.Tensor,
-                           ws: Optional[torch.Tensor] = None, stream=None) -> None:
+                           ws: Optional[torch.Tensor] = None, stream=None,
+                           index: Optional[torch.Tensor] = None) -> None:
     """lsm_level_may_contain: searchFromLevelWithSparseIndex's candidate table
     (int32 per key, -1 for an empty level) and its MayContain (uint8 per key)
-    for a level >= 1 whose tables were decoded into r in sparse-index order."""
+    for a level >= 1 whose tables were decoded into r in sparse-index order.
+    index (level_index): lsm_level_may_contain_indexed, the headers not parsed
+    again."""
     if ws is None:
         ws = level_may_contain_workspace(ctx, r.nfile, batch.n)
+    if index is not None:
+        _lib.check(ctx.lib.lsm_level_may_contain_indexed(
+            ctx.handle, _ptr(d_img) if r.nfile else None, _ptr(index) if r.nfile else None,
+            r.nfile, _ptr(batch.keys), _ptr(batch.koff), batch.n, _ptr(table), _ptr(may), _ptr(ws),
+            ws.numel(), _stream_handle(stream)), "lsm_level_may_contain_indexed")
+        return
     _lib.check(ctx.lib.lsm_level_may_contain(
         ctx.handle, _ptr(d_img) if r.nfile else None, _ptr(r.d_file_off) if r.nfile else None,
         _ptr(r.meta) if r.nfile else None, r.nfile, _ptr(batch.keys), _ptr(batch.koff), batch.n,

@@ -35,7 +35,8 @@ extern "C" {
  * v4: lsm_merge_kvs_tie writes 3 h_counts entries; lsm_merge_kvs keeps the
  * v2 / v3 contract of exactly 2 ({nout, nfiles}).
  * v5: lsm_merge_kvs_async and lsm_gather_kvs_dev (the merge's counts stay on
- * the device; the gather reads its pair count there). */
+ * the device; the gather reads its pair count there); the level sparse index
+ * (lsm_level_index_build, lsm_level_may_contain_indexed). */
 #define LSM_ABI_VERSION 5
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
@@ -295,6 +296,20 @@ int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_
                           const lsm_sst_meta *d_meta, uint32_t nfile, const uint8_t *d_keys,
                           const uint64_t *d_koff, uint64_t nkeys, int32_t *d_table,
                           uint8_t *d_may, void *d_workspace, size_t ws_bytes, void *stream);
+/* The level's sparse index (ABI 5) -- Manager's sparseIndexes[level-1]
+ * (manager.go:183-187): each table's MinKey / MaxKey prefixes and filter shape,
+ * parsed from the images once and kept while the level is unchanged, as the
+ * Manager keeps its loaded SSTables.  d_index: lsm_level_index_bytes(nfile)
+ * bytes; it refers to offsets inside d_img, so the searches pass the same
+ * d_img.  lsm_level_may_contain_indexed = lsm_level_may_contain without
+ * parsing the headers again (same outputs, same workspace). */
+size_t lsm_level_index_bytes(uint32_t nfile);
+int lsm_level_index_build(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                          const lsm_sst_meta *d_meta, uint32_t nfile, void *d_index, void *stream);
+int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img, const void *d_index,
+                                  uint32_t nfile, const uint8_t *d_keys, const uint64_t *d_koff,
+                                  uint64_t nkeys, int32_t *d_table, uint8_t *d_may,
+                                  void *d_workspace, size_t ws_bytes, void *stream);
 
 /* ---- encode ---------------------------------------------------------------- */
 

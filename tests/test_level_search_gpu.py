@@ -59,7 +59,15 @@ def check(ctx, rng, images, probes):
     d_img = lsmgpu.to_device_bytes(buf, ctx.torch_device)
     r = lsmgpu.decode_sst(ctx, d_img, offs, np.array([im.size for im in images], np.uint64))
     table, may = lsmgpu.level_may_contain(ctx, d_img, r, batch)
+    # the same search over the level's sparse index built beforehand
+    # (lsm_level_index_build + lsm_level_may_contain_indexed)
+    index = lsmgpu.level_index(ctx, d_img, r)
+    t2 = torch.full_like(table, -7)
+    m2 = torch.full_like(may, 7)
+    if batch.n:
+        lsmgpu.level_may_contain_into(ctx, d_img, r, batch, t2, m2, index=index)
     torch.cuda.synchronize()
+    assert torch.equal(t2, table) and torch.equal(m2, may), "indexed search differs"
     table, may = table.cpu().numpy(), may.cpu().numpy()
     metas = [ora.sst_decode(im)[1] for im in images]
     wt, wm = ora.level_may_contain(buf, offs, metas, kb, ko, 0, len(probes))
