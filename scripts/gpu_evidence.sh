@@ -41,6 +41,7 @@ K[mixed]=sched_hist_kernel,sched_scatter_kernel,decode_v2_kernel; A[mixed]=decod
 K[sstdec]=sst_index_kernel,sst_index_fixup_kernel,sst_data_verify_kernel,sst_data_fixup_kernel; A[sstdec]=sst_index_fixup_kernel; W[sstdec]=sstdec:208
 K[probe]=mc_prep_kernel,mc_classify_kernel,mc_scatter_kernel,mc_test_kernel,may_contain_kernel; A[probe]=mc_prep_kernel; W[probe]=probe:208:1048576
 K[wal]=wal_seg_lanes_kernel,wal_stitch_kernel,wal_compact_kernel; A[wal]=wal_stitch_kernel; W[wal]=wal:64:desc
+K[level]=lv_classify_kernel,lv_test_kernel; A[level]=lv_classify_kernel; W[level]=level:208:1048576
 for cfg in ${PMCM:-sst sstdec probe wal}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmcm_${cfg}_$c 180 rocprofv3 --pmc $c --output-format csv -d $OUT/pmcm_${TAG}_${cfg}_$c -o run \
@@ -51,7 +52,7 @@ for cfg in ${PMCM:-sst sstdec probe wal}; do
 done
 fi
 if [ "$PHASE" = all ] || [ "$PHASE" = 3 ]; then
-for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal probe compact e2e}; do
+for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal probe level compact e2e}; do
   case $line in
     cfg4) args="--global-blocks 1000000 --no-cpu-baseline" ;;
     arena) args="--arena" ;;
@@ -62,7 +63,7 @@ for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal 
     || { tail -20 $OUT/bench_${TAG}_$line.err; exit 1; }
   cut -c1-200 $OUT/bench_${TAG}_$line.json
 done
-for p in ${PROF:-decode4k arena decode64k mixed sst sstdec probe wal compact}; do
+for p in ${PROF:-decode4k arena decode64k mixed sst sstdec probe level wal compact}; do
   case $p in arena) args="--arena" ;; *) args="--config $p" ;; esac
   step prof_$p 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_$p -o run \
     -- python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline --no-cold > $OUT/prof_${TAG}_$p.log 2>&1 || exit 1
