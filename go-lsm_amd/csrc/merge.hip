@@ -450,31 +450,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, c
     if (j >= m.n) return;
     const uint32_t pj = perm[j];
     const View v = view(m, pj);
-    // the predecessor's key length, offset and first 32 bytes from the lane
-    // below (lane 0 loads them): the whole keys are compared only when those
-    // tie and the keys are longer
-    uint64_t ch[kFastChunks], pc[kFastChunks];
-#pragma unroll
-    for (uint32_t d = 0; d < kFastChunks; d++) ch[d] = v.kl > 8 * d ? key_chunk(m.bytes + v.ko, v.kl, d) : 0;
-    uint32_t pkl = __shfl_up(v.kl, 1);
-    uint64_t pko = __shfl_up(v.ko, 1);
-#pragma unroll
-    for (uint32_t d = 0; d < kFastChunks; d++) pc[d] = __shfl_up(ch[d], 1);
-    if (lane_id() == 0 && j > 0) {
-        const View u = view(m, perm[j - 1]);
-        pkl = u.kl;
-        pko = u.ko;
-#pragma unroll
-        for (uint32_t d = 0; d < kFastChunks; d++) pc[d] = u.kl > 8 * d ? key_chunk(m.bytes + u.ko, u.kl, d) : 0;
-    }
-    bool gs = j == 0 || v.kl == 0 || v.kl != pkl;
-#pragma unroll
-    for (uint32_t d = 0; d < kFastChunks; d++) gs = gs || ch[d] != pc[d];
-    if (!gs && v.kl > 8 * kFastChunks) {
-        View u = v;
-        u.ko = pko;
-        gs = !keys_equal(m.bytes, v, u);
-    }
+    bool gs = j == 0 || v.kl == 0;
+    if (!gs) gs = !keys_equal(m.bytes, v, view(m, perm[j - 1]));
     const bool wr = level < 6 || !is_tombstone(m.bytes, v);
     flags[j] = (uint8_t)((gs ? 1 : 0) | (wr ? 2 : 0));
     const uint64_t sz = 16 + (uint64_t)v.kl + v.vl;
@@ -1258,9 +1235,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_emit_kernel(
 // length, value length) -- tile sums (the lengths kept), the tile sums'
 // scan (merge_scan_partials), then each slot's offsets -- where two scans
 // of separately gathered lengths took 88 us for 3.3M pairs.
-constexpr uint32_t kGatherPer = 8;  // pairs per thread: 8 view gathers in flight
-constexpr uint32_t kGatherTile = kMergeThreads * kGatherPer;
-
 // the gather's pair count: the host's, or lsm_gather_kvs_dev's device count
 __device__ __forceinline__ uint32_t gather_count(uint32_t nout, const uint64_t *d_nout) {
     return d_nout ? (uint32_t)*d_nout : nout;
@@ -1272,18 +1246,14 @@ __global__ __launch_bounds__(kMergeThreads) void gather_scan_tiles(MergeIn m, co
                                                                    SumPair *part) {
     const uint32_t nout = gather_count(nmax, d_nout);
     uint64_t s = 0, c = 0;
-    const uint64_t i0 = (uint64_t)blockIdx.x * kGatherTile + threadIdx.x * kGatherPer;
-    View v[kGatherPer];
-#pragma unroll
-    for (uint32_t t = 0; t < kGatherPer; t++)
-        if (i0 + t < nout) v[t] = view(m, idx[i0 + t]);
-#pragma unroll
-    for (uint32_t t = 0; t < kGatherPer; t++) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t t = 0; t < kScanPer; t++) {
         if (i0 + t < nout) {
-            klen[i0 + t] = v[t].kl;
-            vlen[i0 + t] = v[t].vl;
-            s += v[t].kl;
-            c += v[t].vl;
+            const View v = view(m, idx[i0 + t]);
+            klen[i0 + t] = v.kl;
+            vlen[i0 + t] = v.vl;
+            s += v.kl;
+            c += v.vl;
         }
     }
     SumPair tot;
@@ -1298,10 +1268,10 @@ __global__ __launch_bounds__(kMergeThreads) void gather_scan_apply(const uint32_
                                                                    const SumPair *total, uint64_t *koff,
                                                                    uint64_t *voff) {
     const uint32_t nout = gather_count(nmax, d_nout);
-    uint32_t kl[kGatherPer], vl[kGatherPer];
+    uint32_t kl[kScanPer], vl[kScanPer];
     uint64_t s = 0, c = 0;
-    const uint64_t i0 = (uint64_t)blockIdx.x * kGatherTile + threadIdx.x * kGatherPer;
-    for (uint32_t t = 0; t < kGatherPer; t++) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t t = 0; t < kScanPer; t++) {
         kl[t] = i0 + t < nout ? klen[i0 + t] : 0;
         vl[t] = i0 + t < nout ? vlen[i0 + t] : 0;
         s += kl[t];
@@ -1310,7 +1280,7 @@ __global__ __launch_bounds__(kMergeThreads) void gather_scan_apply(const uint32_
     SumPair tot;
     const SumPair x = block_excl_scan2(s, c, &tot);
     uint64_t ps = x.s + part[blockIdx.x].s, pc = x.c + part[blockIdx.x].c;
-    for (uint32_t t = 0; t < kGatherPer; t++) {
+    for (uint32_t t = 0; t < kScanPer; t++) {
         if (i0 + t < nout) {
             koff[i0 + t] = ps;
             voff[i0 + t] = pc;
@@ -1989,7 +1959,7 @@ static int gather_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *
     uint32_t *kl = static_cast<uint32_t *>(d_ws);
     uint32_t *vl = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d_ws) + part);
     SumPair *tparts = reinterpret_cast<SumPair *>(static_cast<uint8_t *>(d_ws) + 2 * part);
-    const uint32_t ntiles = (uint32_t)((nn + kGatherTile - 1) / kGatherTile);
+    const uint32_t ntiles = (uint32_t)((nn + kScanTile - 1) / kScanTile);
     SumPair *total = tparts + ntiles;
     const MergeIn m{d_bytes, d_key_desc, d_val_desc, N};
     if (N == 0) {  // (a device count is then 0 as well)
