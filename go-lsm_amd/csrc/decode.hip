@@ -1132,17 +1132,20 @@ __global__ __launch_bounds__(kSchedThreads) void sched_scatter_kernel(const uint
 //      hypothesis "every index entry has the first entry's key length" on
 //      the whole index region at once.  Entry i verified <=> its key length
 //      field holds K0, so the serial chase visits exactly these entries.
-//   2. sst_index_fixup_kernel: one wave chases the index from the first
-//      entry the hypothesis failed on (decode_range_v2, exact semantics).
-//   3. sst_data_verify_kernel: the values are located by the index offsets
+//   Steps 2-4 run in sst_tail_kernel, one 256-thread workgroup per file
+//   (three launches of a wave per file each took ~4.8 us: 14.6 -> 4.8 us):
+//   2. wave 0 chases the index from the first entry the hypothesis failed
+//      on (decode_range_v2, exact semantics).
+//   3. only when it did fail: the values are located by the index offsets
 //      (SSTable.EncodeTo writes value i at Indexes[i].Offset,
 //      sstable.go:164-169); value i is verified when it starts where value
 //      i-1 ended (value 0 at DataHandle.Offset) and ends where value i+1
 //      starts (the last one at the end of the region).  The verified values
-//      are exactly the serial chase's.
-//   4. sst_data_fixup_kernel: one wave chases the data region from the first
-//      unverified value, then applies GetKeyValuePairs' count rules and
-//      writes the per-file lsm_sst_meta.
+//      are exactly the serial chase's.  (Under the hypothesis
+//      sst_index_kernel checked them already.)
+//   4. wave 0 chases the data region from the first unverified value, then
+//      applies GetKeyValuePairs' count rules and writes the per-file
+//      lsm_sst_meta.
 // A well-formed file costs two parallel passes; a corrupted one falls back
 // to the exact chase only from the first entry that cannot be vouched for.
 
@@ -1172,7 +1175,6 @@ struct SstWork {
     uint32_t k0, spec_cnt;     // index stride hypothesis: key length, entries to test
     uint32_t idx_overrun;      // IndexHandle.Size runs past the end of the file
     uint32_t data_neg;         // DataHandle.Offset < 0: the seek fails
-    uint32_t spec_ok;          // the stride hypothesis held for the whole index (fixup)
 };
 
 // SSTable.DecodeFrom's framing (sstable.go:87-128) as the oracle restates it
@@ -1266,10 +1268,10 @@ __global__ __launch_bounds__(256) void sst_index_kernel(SstArgs a) {
     if (W.m.stage != 0) return;
     // Entry i at io + i S (the stride hypothesis: every key has the first
     // key's length), and in the same pass value i, located by the entry's
-    // offset and checked against the next entry's (sst_data_verify_kernel's
+    // offset and checked against the next entry's (sst_tail_kernel's step 3
     // rule).  The value checks stand only if the hypothesis holds for the
-    // whole index; sst_index_fixup_kernel decides, and otherwise
-    // sst_data_verify_kernel checks the values again from the final offsets.
+    // whole index; sst_tail_kernel decides, and otherwise checks the values
+    // again from the final offsets.
     const uint64_t S = 12ull + W.k0;
     const uint64_t doff = (uint64_t)W.m.data_off, dl = W.dl;
     const bool whole = (uint64_t)W.spec_cnt * S == W.il && !W.idx_overrun;
@@ -1317,90 +1319,96 @@ __global__ __launch_bounds__(256) void sst_index_kernel(SstArgs a) {
     }
 }
 
-__global__ __launch_bounds__(64) void sst_index_fixup_kernel(SstArgs a) {
+// Steps 2-4 for one file in one workgroup (wave 0 chases, the workgroup
+// verifies): a file whose index held the stride hypothesis had its values
+// verified by sst_index_kernel and takes one pass of wave 0.
+__global__ __launch_bounds__(256) void sst_tail_kernel(SstArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
-    const uint32_t f = blockIdx.x;
+    __shared__ uint32_t s_nidx, s_hyp, s_fail;
+    __shared__ int32_t s_stage, s_status;
+    const uint32_t f = blockIdx.x, t = threadIdx.x;
     SstWork &W = a.work[f];
-    if (uni((uint32_t)W.m.stage) != 0) return;
-    const uint32_t spec = uni(W.spec_cnt);
-    const uint32_t fl = uni(a.fail[3 * f]);
-    const uint32_t i0 = fl < spec ? fl : spec;
-    const uint64_t S = 12ull + uni(W.k0), il = uni64(W.il);
-    const bool overrun = uni(W.idx_overrun) != 0;
-    uint32_t nidx;
-    int32_t st = LSM_OK;
-    const bool hyp = i0 == spec && (uint64_t)spec * S == il && !overrun;
-    if (hyp) {
-        nidx = spec;
-    } else {
-        DecodeArgs d = {};
-        d.in = a.img;
-        d.desc = a.idx_desc;
-        d.idx_value = a.idx_value;
-        const uint64_t start = (uint64_t)i0 * S, cap = uni64(W.cap);
-        uint32_t nr = 0;
-        decode_range_any<LSM_GRAMMAR_IDX, 8>(
-            d, ring, uni64(a.file_off[f]) + uni64(W.io) + start, (uint32_t)(il - start),
-            uni64(W.base) + i0, (uint32_t)(cap - i0 < 0xFFFFFFFFull ? cap - i0 : 0xFFFFFFFFull), nr, st);
-        nidx = i0 + nr;
-        if (overrun && st == LSM_OK) st = LSM_ST_IDX_OVERRUN;  // index.go:73-91 reads past EOF
-    }
-    if (lane_id() == 0) {
-        W.m.nidx = nidx;
-        W.spec_ok = hyp;  // the values were checked with the index (sst_index_kernel)
-        if (hyp) a.fail[3 * f + 1] = a.fail[3 * f + 2];
-        if (st != LSM_OK) {
-            W.m.stage = LSM_SST_INDEX;
-            W.m.status = st;
+    const int32_t stage0 = (int32_t)uni((uint32_t)W.m.stage);
+    if (t < kWave) {
+        // 2. the index
+        uint32_t nidx = 0;
+        bool hyp = false;
+        int32_t st = LSM_OK;
+        if (stage0 == 0) {
+            const uint32_t spec = uni(W.spec_cnt);
+            const uint32_t fl = uni(a.fail[3 * f]);
+            const uint32_t i0 = fl < spec ? fl : spec;
+            const uint64_t S = 12ull + uni(W.k0), il = uni64(W.il);
+            const bool overrun = uni(W.idx_overrun) != 0;
+            hyp = i0 == spec && (uint64_t)spec * S == il && !overrun;
+            if (hyp) {
+                nidx = spec;
+            } else {
+                DecodeArgs d = {};
+                d.in = a.img;
+                d.desc = a.idx_desc;
+                d.idx_value = a.idx_value;
+                const uint64_t start = (uint64_t)i0 * S, cap = uni64(W.cap);
+                uint32_t nr = 0;
+                decode_range_any<LSM_GRAMMAR_IDX, 8>(
+                    d, ring, uni64(a.file_off[f]) + uni64(W.io) + start, (uint32_t)(il - start),
+                    uni64(W.base) + i0, (uint32_t)(cap - i0 < 0xFFFFFFFFull ? cap - i0 : 0xFFFFFFFFull), nr, st);
+                nidx = i0 + nr;
+                if (overrun && st == LSM_OK) st = LSM_ST_IDX_OVERRUN;  // index.go:73-91 reads past EOF
+            }
+        }
+        if (t == 0) {
+            // the index's outcome stays on chip (no re-read of W's fields
+            // through the vector cache after a store to them)
+            s_stage = st != LSM_OK ? (int32_t)LSM_SST_INDEX : stage0;
+            s_status = st != LSM_OK ? st : (int32_t)W.m.status;
+            s_nidx = nidx;
+            s_hyp = (stage0 == 0 && st == LSM_OK && !hyp && !uni(W.data_neg)) ? 1u : 0u;
+            s_fail = hyp ? a.fail[3 * f + 2] : 0xFFFFFFFFu;
         }
     }
-}
-
-__global__ __launch_bounds__(256) void sst_data_verify_kernel(SstArgs a) {
-    __shared__ SstWork W;
-    const uint32_t f = blockIdx.y;
-    if (threadIdx.x == 0) W = a.work[f];
     __syncthreads();
-    if (W.m.stage != 0 || W.data_neg || W.spec_ok) return;
-    const uint64_t foff = a.file_off[f];
-    ImgReader R;
-    R.init(a.img, foff, a.file_len[f]);
-    const uint64_t doff = (uint64_t)W.m.data_off, dl = W.dl;
-    const uint32_t nidx = W.m.nidx;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nidx;
-         i += gridDim.x * blockDim.x) {
-        const uint64_t pos = (uint64_t)a.idx_value[W.base + i] - doff;  // value i, region-relative
-        bool bad = dl < 4 || pos > dl - 4 || (i == 0 && pos != 0);
-        if (!bad) {
-            const uint32_t v = R.u32(W.dof + pos);
-            const uint64_t e = pos + 4 + v;  // where value i ends
-            const uint64_t next = i + 1 < nidx ? (uint64_t)a.idx_value[W.base + i + 1] - doff : dl;
-            bad = e > dl || e != next;
-            const uint64_t ro = foff + W.dof + pos;
-            u32x4 d;
-            d.x = (uint32_t)ro;
-            d.y = (uint32_t)(ro >> 32);
-            d.z = 0;
-            d.w = v;
-            __builtin_nontemporal_store(d, &a.data_desc[W.base + i]);
+    // 3. the values from the final offsets when the index did not hold the
+    //    hypothesis (by the whole workgroup)
+    if (s_hyp) {
+        const uint64_t foff = a.file_off[f];
+        ImgReader R;
+        R.init(a.img, foff, a.file_len[f]);
+        const uint64_t doff = (uint64_t)W.m.data_off, dl = W.dl, base = W.base, dof = W.dof;
+        const uint32_t nidx = s_nidx;
+        uint32_t mine = 0xFFFFFFFFu;
+        for (uint32_t i = t; i < nidx; i += blockDim.x) {
+            const uint64_t pos = (uint64_t)a.idx_value[base + i] - doff;  // value i, region-relative
+            bool bad = dl < 4 || pos > dl - 4 || (i == 0 && pos != 0);
+            if (!bad) {
+                const uint32_t v = R.u32(dof + pos);
+                const uint64_t e = pos + 4 + v;  // where value i ends
+                const uint64_t next = i + 1 < nidx ? (uint64_t)a.idx_value[base + i + 1] - doff : dl;
+                bad = e > dl || e != next;
+                const uint64_t ro = foff + dof + pos;
+                u32x4 d;
+                d.x = (uint32_t)ro;
+                d.y = (uint32_t)(ro >> 32);
+                d.z = 0;
+                d.w = v;
+                __builtin_nontemporal_store(d, &a.data_desc[base + i]);
+            }
+            if (bad && i < mine) mine = i;
         }
-        if (bad) atomicMin(&a.fail[3 * f + 1], i);
+        if (mine != 0xFFFFFFFFu) atomicMin(&s_fail, mine);
+        __syncthreads();
     }
-}
-
-__global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[8 * kChunk / 4 + 4];
-    const uint32_t f = blockIdx.x;
-    SstWork &W = a.work[f];
-    int32_t stage = (int32_t)uni((uint32_t)W.m.stage);
-    int32_t status = (int32_t)uni((uint32_t)W.m.status);
-    const uint32_t nidx = uni(W.m.nidx);
+    if (t >= kWave) return;
+    // 4. the data region and the file's meta
+    int32_t stage = s_stage;
+    int32_t status = s_status;
+    const uint32_t nidx = s_nidx;
     uint32_t ndata = 0;
     if (stage == LSM_SST_OK) {
         if (uni(W.data_neg)) {
             stage = LSM_SST_DATA;  // seek to a negative offset
         } else {
-            const uint32_t fl = uni(a.fail[3 * f + 1]);
+            const uint32_t fl = uni(s_fail);
             const uint32_t f0 = nidx == 0 ? 0u : (fl < nidx ? fl : nidx);
             int32_t st = LSM_OK;
             if (nidx > 0 && f0 == nidx) {
@@ -1428,8 +1436,9 @@ __global__ __launch_bounds__(64) void sst_data_fixup_kernel(SstArgs a) {
             }
         }
     }
-    if (lane_id() == 0) {
+    if (t == 0) {
         lsm_sst_meta m = W.m;
+        m.nidx = nidx;
         m.stage = stage;
         m.status = status;
         m.ndata = ndata;
@@ -2356,9 +2365,7 @@ extern "C" int lsm_decode_sst(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t
     if (g > 64) g = 64;
     if (g == 0) g = 1;
     hipLaunchKernelGGL(sst_index_kernel, dim3(g, nfile), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(sst_index_fixup_kernel, dim3(nfile), dim3(kWave), 0, s, a);
-    hipLaunchKernelGGL(sst_data_verify_kernel, dim3(g, nfile), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(sst_data_fixup_kernel, dim3(nfile), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL(sst_tail_kernel, dim3(nfile), dim3(256), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }
