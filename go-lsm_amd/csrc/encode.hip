@@ -2843,6 +2843,14 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
 
 
     hipStream_t rs = forked ? ctx->side : s;  // the regions' stream
+    // With views the V region is a copy independent of the IDX region and of
+    // the filter: it runs on the side stream beside them (joined below).
+    const bool vfork = views && chunks && !forked;
+    if (vfork) {
+        LSM_HIP_CHECK(hipEventRecord(ctx->fork, s));
+        LSM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->fork, 0));
+    }
+    hipStream_t vs = vfork ? ctx->side : rs;  // the V region's stream
     // Past the fork every error still joins: kernels already queued on the
     // side stream must be ordered before the caller's stream (which may free
     // the outputs once the call returns an error).
@@ -2860,10 +2868,10 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
             // V descriptors: the records are copied whole (runs); KV
             // descriptors: each record assembled from its value view
             if (views->vd)
-                hipLaunchKernelGGL(sst_vregion_runs_kernel, dim3(nfile, chunks), dim3(256), 0, rs, a,
+                hipLaunchKernelGGL(sst_vregion_runs_kernel, dim3(nfile, chunks), dim3(256), 0, vs, a,
                                    *views);
             else
-                hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, rs,
+                hipLaunchKernelGGL(sst_vregion_views_kernel, dim3(nfile, chunks), dim3(256), 0, vs,
                                    a, *views);
             LSM_TRY(hipGetLastError());
         }
@@ -2889,7 +2897,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
                            (size_t)(osb / 8), s, bo, a);
         LSM_TRY(hipGetLastError());
     }
-    if (forked) {  // join (also after an error): the caller's stream waits for the regions
+    if (forked || vfork) {  // join (also after an error): the caller's stream waits for the side
         LSM_TRY(hipEventRecord(ctx->join, ctx->side));
         LSM_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     }
