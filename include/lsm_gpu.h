@@ -8,7 +8,10 @@
  * allocation and no host synchronisation (hipGraph-capturable) -- except
  * lsm_merge_kvs, which synchronizes `stream` (its radix passes are chosen
  * from key statistics read back to the host); the caller owns every buffer
- * and the library keeps no pointer after the call returns.
+ * and the library keeps no pointer after the call returns.  lsm_build_sst
+ * and lsm_build_sst_views may run part of their launches on the context's
+ * side stream, forked from `stream` by an event and joined back into it
+ * before they return (so a context serves one caller thread at a time).
  *
  * Device input buffers (blocks, images, logs, key and value arenas) must be
  * readable up to LSM_INPUT_SLACK bytes past the next multiple of 16 bytes
