@@ -72,13 +72,15 @@ struct MergeIn {
     uint32_t n;
 };
 
+// plain loads: the stats, flags, rank and gather passes read the same
+// descriptors again (nt loads: compaction 1.027 -> 1.018 ms without them, A/B)
 __device__ __forceinline__ View view(const MergeIn &m, uint32_t i) {
-    const u32x4 k = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(m.kd) + i);
+    const u32x4 k = reinterpret_cast<const u32x4 *>(m.kd)[i];
     View v;
     v.ko = ((uint64_t)k.y << 32 | k.x) + 4;
     v.kl = k.z;
     if (m.vd) {
-        const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(m.vd) + i);
+        const u32x4 d = reinterpret_cast<const u32x4 *>(m.vd)[i];
         v.vo = ((uint64_t)d.y << 32 | d.x) + 4;
         v.vl = d.w;
     } else {
