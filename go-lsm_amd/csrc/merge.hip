@@ -1203,10 +1203,12 @@ __global__ __launch_bounds__(kWalkThreads) void merge_walk_kernel(WalkArgs a) {
 // the candidates before it in the file
 __global__ __launch_bounds__(kMergeThreads) void merge_emit_kernel(
     const uint32_t *perm, const SumPair *sc, const uint32_t *csize, const MergeFile *files,
-    const uint64_t *counts, uint32_t n, uint32_t *out, uint64_t *file_start) {
+    const uint64_t *counts, uint32_t n, uint32_t *out, uint64_t *file_start, uint64_t *counts_out) {
     __shared__ uint32_t s_lo;
     const uint32_t j0 = blockIdx.x * kMergeThreads, j = j0 + threadIdx.x;
     const uint32_t nf = (uint32_t)counts[1];
+    // the async form's device counts (no copy launch after this one)
+    if (counts_out && j < 3) counts_out[j] = counts[j];
     if (j <= nf && file_start) file_start[j] = files[j].o;
     // the file of the workgroup's first position: one search per workgroup;
     // a position's file is then at most a few files further (a file spans
@@ -1894,12 +1896,9 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
                 threshold, w.files, d_out, w.stats};
     hipLaunchKernelGGL(merge_walk_kernel, dim3(1), dim3(kWalkThreads), 0, s, wa);
     hipLaunchKernelGGL(merge_emit_kernel, dim3(grid_for(n + 1)), dim3(kMergeThreads), 0, s, perm,
-                       w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start);
+                       w.sc, w.csize, w.files, w.stats, N, d_out, d_file_start, d_counts);
     LSM_HIP_CHECK(hipGetLastError());
-    if (d_counts) {  // the async form: the counts stay on the device
-        LSM_HIP_CHECK(hipMemcpyAsync(d_counts, w.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-        return 0;
-    }
+    if (d_counts) return 0;  // the async form: the counts stay on the device (written by the emit)
     uint64_t *c3 = static_cast<uint64_t *>(ctx->host_rb);  // pinned
     LSM_HIP_CHECK(hipMemcpyAsync(c3, w.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
