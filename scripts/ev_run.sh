@@ -1,2 +1,2 @@
-TAG=r04y PHASE=2 PMC1="" PMCM="sstdec" bash scripts/gpu_evidence.sh || exit 1
-TAG=r04y PHASE=3 PROF="sstdec compact decode4k" bash scripts/gpu_evidence.sh || exit 1
+TAG=r04w PHASE=1 bash scripts/gpu_evidence.sh || exit 1
+TAG=r04w PHASE=3 LINES="decode4k compact sstdec" PROF="compact" bash scripts/gpu_evidence.sh || exit 1
