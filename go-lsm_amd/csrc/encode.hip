@@ -968,7 +968,7 @@ constexpr uint32_t kSstChunkRecs = kSstWaves * kWave;  // records per workgroup
 // issued.  A chunk whose images do not fit the buffer takes the one-region
 // encoders.
 constexpr uint32_t kRegWaves = 2;         // waves per workgroup
-constexpr uint32_t kRegWaveChunks = 4;    // 64-record chunks per wave
+constexpr uint32_t kRegWaveChunks = 2;    // 64-record chunks per wave (4: config 3 0.2573 ms, 2: 0.2500, 8: 0.2650; A/B)
 constexpr uint32_t kRegBufDwords = 2432;  // both images of a chunk (9.5 KiB)
 constexpr uint32_t kRegSpanRecs = kRegWaves * kRegWaveChunks * kWave;  // records per workgroup
 constexpr uint32_t kRegMaxImage = 32 * kGatherMaskWords;  // dwords one mask covers
