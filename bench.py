@@ -47,7 +47,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
                     choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal",
-                             "probe", "level", "compact"])
+                             "probe", "level", "get", "compact"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU (weak scaling)")
     ap.add_argument("--global-blocks", type=int, default=None,
                     help="fixed global batch dealt round-robin over the ranks (strong "
@@ -69,6 +69,9 @@ def parse(argv=None):
                     help="host-resident blocks: pinned H2D -> decode -> compact -> D2H "
                          "(the PCIe-inclusive rate recorded in DESIGN.md; not the headline)")
     ap.add_argument("--chunk", type=int, default=8192, help="blocks per e2e pipeline chunk")
+    ap.add_argument("--tie", default="input", choices=["input", "goheap"],
+                    help="--config compact: equal keys in input order (LSM_TIE_INPUT) or in "
+                         "container/heap's pop order, the reference's exact output (LSM_TIE_GOHEAP)")
     return ap.parse_args(argv)
 
 
@@ -772,8 +775,9 @@ def main(argv=None):
     elif args.config == "probe":
         from bench_sstdec import bench_may_contain  # batched MayContain (§8(f) f3)
         out, data = bench_may_contain(args, world, rank, local)
-    elif args.config == "level":
-        from bench_sstdec import bench_level_search  # level search, reference shape (§8(f) f3)
+    elif args.config in ("level", "get"):
+        # level search, reference shape (§8(f) f3); get: + Seek + value
+        from bench_sstdec import bench_level_search
         out, data = bench_level_search(args, world, rank, local)
     elif args.config == "compact":
         from bench_compact import bench_compact  # L0 -> L1 compaction (§8(f) f1 + f2)
@@ -792,7 +796,7 @@ def main(argv=None):
         elif args.config == "probe":
             from bench_sstdec import cpu_baseline_may_contain
             out["cpu_baseline"] = cpu_baseline_may_contain(args, data)
-        elif args.config == "level":
+        elif args.config in ("level", "get"):
             from bench_sstdec import cpu_baseline_level_search
             out["cpu_baseline"] = cpu_baseline_level_search(args, data)
         elif args.config == "compact":

@@ -29,13 +29,17 @@ L0_FILES = 8
 L0_RECS = 15_888  # records of a 2 MiB memtable flush (README's 2.2 MB file)
 
 
+def level0_ids(n1, first, rank, nfiles=L0_FILES, per=L0_RECS):
+    """The key ids of the L0 flushes, newest file first."""
+    rng = np.random.default_rng(synth.SEED + 77 + rank)
+    return [np.unique(rng.integers(first, first + n1, per)) for _ in range(nfiles)]
+
+
 def level0_runs(n1, first, rank, nfiles=L0_FILES, per=L0_RECS):
     """L0 flushes: sorted unique update keys inside level 1's key range;
     newest file first (go-lsm lists level-0 files newest first)."""
-    rng = np.random.default_rng(synth.SEED + 77 + rank)
     runs = []
-    for f in range(nfiles):
-        ids = np.unique(rng.integers(first, first + n1, per))
+    for f, ids in enumerate(level0_ids(n1, first, rank, nfiles, per)):
         keys = synth.keys_for(ids).reshape(-1)
         vals = synth.value_bytes(ids + (f + 1) * 10 ** 9, synth.VAL_LEN).reshape(len(ids), -1)
         vlen = np.full(len(ids), synth.VAL_LEN, np.int64)
@@ -81,6 +85,10 @@ def bench_compact(args, world, rank, local):
     key_bytes = int(meta["idx_size"].astype(np.int64).sum())   # bounds the selected keys
     val_bytes = int(meta["data_size"].astype(np.int64).sum())  # and values
     mg = lsmgpu.alloc_merge(ctx, n)
+    # LSM_TIE_INPUT: equal keys in input order (merge.go:41's contract, all on
+    # the device); LSM_TIE_GOHEAP: container/heap's own pop order, the
+    # reference's exact output (the heap's history replayed on one host thread)
+    tie = lsmgpu.TIE_GOHEAP if getattr(args, "tie", "input") == "goheap" else lsmgpu.TIE_INPUT
     stream = torch.cuda.current_stream()
     ev_names = ("decode", "join", "merge", "gather", "build")
     keep = {}  # the gather's and the build's buffers, allocated by the first step
@@ -90,7 +98,7 @@ def bench_compact(args, world, rank, local):
     h_counts = torch.zeros(3, dtype=torch.int64, pin_memory=True)
     counted = torch.cuda.Event()
 
-    def step(evs=None):
+    def step(evs=None, tie=tie):
         def mark(i):
             if evs is not None:
                 evs[i].record(stream)
@@ -99,7 +107,7 @@ def bench_compact(args, world, rank, local):
         mark(1)
         lsmgpu.sst_pairs_into(ctx, r, kd, vd, prefix, stream=stream)
         mark(2)
-        lsmgpu.merge_kvs_into(ctx, img, kd, vd, mg, level=1, stream=stream, d_counts=d_counts)
+        lsmgpu.merge_kvs_into(ctx, img, kd, vd, mg, level=1, stream=stream, d_counts=d_counts, tie=tie)
         h_counts.copy_(d_counts, non_blocking=True)
         counted.record(stream)
         mark(3)
@@ -130,6 +138,32 @@ def bench_compact(args, world, rank, local):
     torch.cuda.synchronize()
     stage_ms = {nm: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in evs]))
                 for i, nm in enumerate(ev_names)}
+    goheap = None
+    if tie == lsmgpu.TIE_GOHEAP:
+        # what the exact tie order costs: the host replay alone on this
+        # input's key ranks (the L0 and L1 key ids are their dense ranks),
+        # and the merge stage against the input-order merge of the same run
+        ids = np.concatenate(level0_ids(n1, first, rank) + [np.arange(first, first + n1)])
+        ranks = (ids - first).astype(np.uint32)
+        assert ranks.size == n
+        rep = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            lsmgpu.goheap_pop_order(ctx, ranks)
+            rep.append(time.perf_counter() - t0)
+        evi = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(3)]
+        for s_ in range(3):
+            step(evi[s_], tie=lsmgpu.TIE_INPUT)
+        torch.cuda.synchronize()
+        merge_in = float(np.mean([e[2].elapsed_time(e[3]) for e in evi]))
+        goheap = {"replay_host_ms": round(min(rep) * 1e3, 2),
+                  "replay_host_ms_mean": round(float(np.mean(rep)) * 1e3, 2),
+                  "merge_stage_ms": round(stage_ms["merge"], 3),
+                  "merge_stage_input_order_ms": round(merge_in, 4),
+                  "chain_ms": round(elapsed * 1e3 / steps, 3),
+                  "note": "merge stage = device sort + equal-key flags + read-back of the sorted "
+                          "order + host ranks and container/heap replay (one thread) + the order "
+                          "back + the device group / flush / emit passes"}
     in_bytes = float(file_size.astype(np.float64).sum())
     total = sum_over_ranks(world, in_bytes)
     # the build stage (lsm_sst_layout + lsm_build_sst_views) moves the most
@@ -155,6 +189,9 @@ def bench_compact(args, world, rank, local):
                    "files_in": nf_in, "files_out": mg.nfiles, "pairs_in": n, "pairs_out": mg.nout,
                    "input_bytes_per_gpu": int(in_bytes),
                    "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+                   "tie": ("goheap: container/heap's pop order for equal keys (the reference's "
+                           "exact output)" if goheap else
+                           "input: equal keys in input order (merge.go:41's contract)"),
                    "parallelism": f"dp{world} (one compaction per rank, no collective)"},
         # the whole chain: an ideal compaction reads every input image byte
         # once and writes every output image byte once; everything between
@@ -175,6 +212,8 @@ def bench_compact(args, world, rank, local):
                                      "achieved": round(b_ach, 1),
                                      "frac": round(b_ach / HBM_PEAK_GBS, 4)}},
     }
+    if goheap:
+        out["goheap"] = goheap
     return out, (img.cpu().numpy(), file_off, file_size)
 
 
@@ -203,7 +242,9 @@ def cpu_baseline_compact(args, data):
     buf = np.concatenate(bufs)
     kpos, klen = np.concatenate(kpos), np.concatenate(klen)
     vpos, vlen = np.concatenate(vpos), np.concatenate(vlen)
-    out, starts = ora.merge_kvs(buf, kpos, klen, vpos, vlen, 1, lsmgpu.MAX_SSTABLE_SIZE)
+    goheap = getattr(args, "tie", "input") == "goheap"
+    out, starts = ora.merge_kvs(buf, kpos, klen, vpos, vlen, 1, lsmgpu.MAX_SSTABLE_SIZE,
+                                ora.TIE_GOHEAP if goheap else ora.TIE_INPUT)
     keys = np.concatenate([buf[int(kpos[i]):int(kpos[i]) + int(klen[i])] for i in out])
     vals = np.concatenate([buf[int(vpos[i]):int(vpos[i]) + int(vlen[i])] for i in out])
     koff = np.concatenate([[0], np.cumsum(klen[out].astype(np.uint64))]).astype(np.uint64)
@@ -215,4 +256,4 @@ def cpu_baseline_compact(args, data):
     return {"value": round(in_bytes / t / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{len(files)} input files ({int(in_bytes)} B, {len(kpos)} pairs) -> "
                       f"{len(starts) - 1} files by the C restatement in {t:.1f} s (1 thread, "
-                      f"Python-driven gathers)"}
+                      f"Python-driven gathers; {'container/heap' if goheap else 'input-order'} ties)"}

@@ -280,10 +280,18 @@ def bench_level_search(args, world, rank, local):
     # the level's sparse index, built when the level changes (Manager keeps
     # sparseIndexes per level, manager.go:183-187), not per search batch
     index = lsmgpu.level_index(ctx, sb.out, r, stream=stream)
+    # --config get: the whole batched Get of one level (searchFromTable,
+    # manager.go:209-223): past the may bit, Iterator.Seek over the table's
+    # decoded index and the value read by its offset (lsm_level_get)
+    get = args.config == "get"
+    result = torch.empty(nprobe, dtype=torch.int32, device=dev)
+    value = torch.empty((nprobe, 4), dtype=torch.int32, device=dev)
 
     def step():
         lsmgpu.level_may_contain_into(ctx, sb.out, r, probes, table, may, ws=ws, stream=stream,
                                       index=index)
+        if get:
+            lsmgpu.level_get_into(ctx, sb.out, r, probes, table, may, result, value, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -298,14 +306,34 @@ def bench_level_search(args, world, rank, local):
     assert np.array_equal(t_h[is_held], want_t), "candidate table"
     assert (m_h[is_held] == 1).all(), "false negative"
     assert (t_h[~is_held] == nf - 1).all() and (m_h[~is_held] == 0).all(), "absent keys"
+    if get:
+        # every held key found, its view the value's own bytes in its image;
+        # every absent key absent
+        res, val = result.cpu().numpy(), value.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+        assert (res[is_held] == lsmgpu.GET_FOUND).all(), "held key not found"
+        assert (res[~is_held] == lsmgpu.GET_ABSENT).all(), "absent key found"
+        assert (val["val_len"][is_held] == synth.VAL_LEN).all() and (val["key_len"] == 0).all()
+        fo = sb.file_off.astype(np.int64)
+        st = starts.astype(np.int64)
+        # header (two 16-byte keys) | filter block (32 + 8 words) | data region
+        data_off = 8 + 2 * synth.KEY_LEN + 32 + 8 * ((lsmgpu.DEFAULT_BLOOM_M + 63) // 64)
+        want_off = fo[want_t] + data_off + (rec - st[want_t]) * (4 + synth.VAL_LEN)
+        assert np.array_equal(val["rec_off"][is_held].astype(np.int64), want_off), "value view"
     total = sum_over_ranks(world, float(nprobe))
     fbits = r.meta_numpy()["filter_nbits"].astype(np.float64)
     # algorithmic bytes per launch: 5 B out per probe (table + may), the probe
-    # keys and offsets read once, every stored filter word read once
+    # keys and offsets read once, every stored filter word read once; with
+    # the Get also 20 B out per probe (result + value view) and, per probe
+    # that passes MayContain, its index entry (4 + key + 8 B) and the value's
+    # length prefix (4 B) read once
     alg = 5.0 * nprobe + pk.size + 8.0 * (nprobe + 1) + float((8 * np.ceil(fbits / 64)).sum())
-    traffic, tsrc = traffic_from_profile(f"level:{nf}:{nprobe}")
+    if get:
+        npass = float(m_h.sum())
+        alg += 20.0 * nprobe + npass * (4 + synth.KEY_LEN + 8 + 4)
+    traffic, tsrc = traffic_from_profile(f"{'get' if get else 'level'}:{nf}:{nprobe}")
     out = {
-        "metric": "M keys/s searched in one level (candidate table + SSTable.MayContain)",
+        "metric": ("M keys/s looked up in one level (candidate table + MayContain + Seek + value)"
+                   if get else "M keys/s searched in one level (candidate table + SSTable.MayContain)"),
         "value": round(total * args.steps / elapsed / 1e6, 2),
         "unit": "M keys/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -314,13 +342,17 @@ def bench_level_search(args, world, rank, local):
         "data": "synthetic: the 208 config-3 images as one level; probes half held, half above "
                 "every range",
         "verified": "every held probe: candidate = its table, may = 1; every absent probe: "
-                    "the last table, may = 0",
+                    "the last table, may = 0" + ("; every held probe found with its value's view, "
+                                                 "every absent probe absent" if get else ""),
         "config": {"workload": f"{nprobe} keys x one level of {nf} .sst files per GPU "
-                               "(searchFromLevelWithSparseIndex -> MayContain, bloom m=1.6M k=16)",
+                               "(searchFromLevelWithSparseIndex -> MayContain" +
+                               (" -> Iterator.Seek -> GetValueByOffset" if get else "") +
+                               ", bloom m=1.6M k=16)",
                    "files_per_gpu": nf, "probes_per_gpu": nprobe,
                    "parallelism": f"dp{world} (probe batches per rank, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "lsm_level_may_contain_indexed (all launches; the level's "
-                               "sparse index built once, outside the step)",
+                               "sparse index built once, outside the step)" +
+                               (" + lsm_level_get" if get else ""),
                      "kernel_ms": round(kern_ms, 5),
                      "kernel_ms_median": round(float(np.median(times)), 5),
                      "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1),
@@ -328,7 +360,7 @@ def bench_level_search(args, world, rank, local):
                      "frac": round(alg / (kern_ms * 1e-3) / 1e9 / 8000.0, 4),
                      "traffic": traffic, "traffic_source": tsrc, "alg_bytes_per_launch": int(alg)},
     }
-    return out, (sb.out.cpu().numpy(), sb.file_off, r.meta_numpy(), pk, nprobe)
+    return out, (sb.out.cpu().numpy(), sb.file_off, r.meta_numpy(), pk, nprobe, sb.file_size, get)
 
 
 def cpu_baseline_level_search(args, data):
@@ -338,15 +370,24 @@ def cpu_baseline_level_search(args, data):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as ora
     from bench import host_cpu, timed_threads
-    img, file_off, meta, pk, nprobe = data
+    img, file_off, meta, pk, nprobe, file_size, get = data
     cpu = host_cpu()
     nf = len(file_off)
     metas = (ora.SstMeta * nf).from_buffer_copy(np.ascontiguousarray(meta).tobytes())
     pko = np.arange(nprobe + 1, dtype=np.uint64) * np.uint64(16)
     chunk = 16384
+    gidx = None
+    if get:  # the tables' index blocks, decoded once (SSTable.DecodeFrom at Recover)
+        dec = [ora.sst_decode(img[int(file_off[f]):int(file_off[f]) + int(file_size[f])])
+               for f in range(nf)]
+        gidx = ora.level_get_index([d[2] for d in dec], [d[3] for d in dec])
 
     def one(c):
-        ora.level_may_contain(img, file_off, metas, pk, pko, c, min(nprobe, c + chunk))
+        c1 = min(nprobe, c + chunk)
+        t, m = ora.level_may_contain(img, file_off, metas, pk, pko, c, c1)
+        if get:
+            ora.level_get(img, file_off, file_size, metas, None, None, pk, pko, c, c1, t, m,
+                          index=gidx)
 
     t1, done = 0.0, 0
     while (t1 < args.cpu_seconds / 3 or done == 0) and done < nprobe:

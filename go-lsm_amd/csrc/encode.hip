@@ -852,48 +852,55 @@ __global__ __launch_bounds__(1024) void bloom_file_kernel(BloomFileArgs a) {
 // 208 CUs with LDS to spare for only a few region waves.  For two-slice
 // filters with k <= 16 the build is split: the region writer (which gathers
 // every key into LDS for the index region anyway) hashes each key once and
-// leaves per key the residues mod m of the four location classes and of the
-// two class steps (location(j) = h[j%2] + j*h[2 + ((j + j%2) % 4)/2],
+// leaves per key the residues mod m of the four location classes' bases and
+// of the class step of classes 0 and 3 (location(j) = h[j%2] + j*h[2 + ((j + j%2) % 4)/2],
 // bloom.go:133-136: class c = j%4 is an arithmetic progression) plus the carry
-// bit of each 64-bit step, 24 bytes; bloom_or_kernel then rebuilds the k
+// bit of each 64-bit step and the two carries that rebuild the other class
+// step from the class bases: 16 bytes; bloom_or_kernel then rebuilds the k
 // locations of every key of its filter from them (additions only) and ORs
 // those of its slice into LDS.
-constexpr uint32_t kHashRecDwords = 6;
+//
+// Record (m <= 2^21: a two-slice filter is at most 2 * 819,200 bits), dword c
+// of 4: bits 0-20 the residue of class c's base, bits 21-23 the carries of
+// its three steps, bits 24-31 byte c of X = res(4 h2) | a << 21 | b << 22,
+// where T = 2 h3 mod 2^64, a = carry of h0 + T (class 2's base) and b = the
+// top bit of T: res(T) = res(base2) - res(base0) + a (2^64 mod m), and
+// res(4 h3) = 2 res(T) - b (2^64 mod m), all mod m.  (24 bytes per key, the
+// round-4 record, were read twice and written once: 1.28x the algorithmic
+// traffic of config 3.)
+constexpr uint32_t kHashRecDwords = 4;
+constexpr uint32_t kHashRecBits = 21;  // residue bits: m <= 2^21
 constexpr uint32_t kOrSlices = 2;  // bloom_or_kernel workgroups per filter
 constexpr uint32_t kSplitMaxK = 16;  // three carries per class fit the record
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// The 24-byte hash record of a key from its sum256 digest: the residues mod m
-// of the four location classes and of the two class steps, carry bits of the
-// 64-bit steps in the residues' spare top bits (m <= 2^30).
+// The 16-byte hash record of a key from its sum256 digest (layout above).
 __device__ __forceinline__ void store_hash_rec(const uint64_t h[4], uint32_t m, uint32_t rl,
                                                uint32_t rh, uint32_t *rec) {
-    uint64_t loc[4] = {h[0], h[1] + h[3], h[0] + (h[3] << 1), h[1] + h[2] + (h[2] << 1)};
+    const uint64_t T = h[3] << 1;
+    const uint64_t loc[4] = {h[0], h[1] + h[3], h[0] + T, h[1] + h[2] + (h[2] << 1)};
     const uint64_t st2 = h[2] << 2, st3 = h[3] << 2;
-    uint32_t r[6];
-    uint32_t cy = 0;  // bit 3c + n - 1: the step to location 4n + c carries
+    uint32_t r[4];
 #pragma unroll
     for (uint32_t c = 0; c < 4; c++) {
-        r[c] = mod_small(loc[c], m, rl, rh);
+        uint32_t cy = 0;  // bit n: the step to location 4(n + 1) + c carries
         const uint64_t st = (c == 0 || c == 3) ? st2 : st3;
         uint64_t l = loc[c];
 #pragma unroll
         for (uint32_t n = 0; n < 3; n++) {
             uint64_t nl;
-            cy |= (uint32_t)__builtin_add_overflow(l, st, &nl) << (3 * c + n);
+            cy |= (uint32_t)__builtin_add_overflow(l, st, &nl) << n;
             l = nl;
         }
+        r[c] = mod_small(loc[c], m, rl, rh) | cy << kHashRecBits;
     }
-    r[4] = mod_small(st2, m, rl, rh);
-    r[5] = mod_small(st3, m, rl, rh);
-    // residues are < m <= 2^30: two carry bits ride in the top of each dword
+    const uint32_t a = loc[2] < h[0];  // h0 + T wrapped
+    const uint32_t x = mod_small(st2, m, rl, rh) | a << 21 | (uint32_t)(T >> 63) << 22;
 #pragma unroll
-    for (uint32_t d = 0; d < 6; d++) r[d] |= ((cy >> (2 * d)) & 3u) << 30;
-    gptr_t<uint32_t> o = gbl(rec);
-    *(gptr_t<u32x4>)o = u32x4{r[0], r[1], r[2], r[3]};
-    *(gptr_t<u32x2>)(o + 4) = u32x2{r[4], r[5]};
+    for (uint32_t c = 0; c < 3; c++) r[c] |= ((x >> (8 * c)) & 0xFFu) << 24;
+    *(gptr_t<u32x4>)gbl(rec) = u32x4{r[0], r[1], r[2], r[3]};
 }
 
 struct BloomOrArgs {
@@ -968,7 +975,7 @@ constexpr uint32_t kSstChunkRecs = kSstWaves * kWave;  // records per workgroup
 // issued.  A chunk whose images do not fit the buffer takes the one-region
 // encoders.
 constexpr uint32_t kRegWaves = 2;         // waves per workgroup
-constexpr uint32_t kRegWaveChunks = 2;    // 64-record chunks per wave (4: config 3 0.2573 ms, 2: 0.2500, 8: 0.2650; A/B)
+constexpr uint32_t kRegWaveChunks = 1;    // 64-record chunks per wave (4: config 3 0.2573 ms, 2: 0.2500, 8: 0.2650; 1: 0.2488 vs 0.2531, round 5; A/B)
 constexpr uint32_t kRegBufDwords = 2432;  // both images of a chunk (9.5 KiB)
 constexpr uint32_t kRegSpanRecs = kRegWaves * kRegWaveChunks * kWave;  // records per workgroup
 constexpr uint32_t kRegMaxImage = 32 * kGatherMaskWords;  // dwords one mask covers
@@ -1053,19 +1060,38 @@ __device__ __forceinline__ void region_issue(const RegionPlan &R, uint32_t *buf,
     const rsrc_t rs = make_rsrc(sbase + (R.Sc - R.ph), uni((R.sbytes + R.ph + 3) & ~3u));
     if (R.ulen != ~0u) {
         // records of one size S: the record of image dword D (first byte
-        // x0 = 4D - ph) is min(cnt - 1, floor(x0 / S)) -- no mask, no scan.
-        // floor((x + 1/2) * rcp(S)) is exact for x < 2^16 (the quotient is at
-        // least 1/(2S) from an integer)
+        // x0 = 4D - ph) is floor(x0 / S) (< cnt inside the image; dwords past
+        // it are never read back).  floor((x + 1/2) * rcp(S)) is exact for
+        // x < 2^16 (the quotient is at least 1/(2S) from an integer); it
+        // seeds the first two rounds, and each later round (x0 + 256) steps
+        // the record by q = floor(256 / S) or q + 1 and the source offset
+        // with it: a remainder test instead of the float division per round.
         const uint32_t S = pre + R.ulen;
         const float inv = __builtin_amdgcn_rcpf((float)S), hinv = 0.5f * inv;
-        for (uint32_t i = 0; i * kWave < R.nD; i++) {
-            const int32_t x0 = 256 * (int32_t)i + 4 * (int32_t)lane - (int32_t)R.ph;
-            const uint32_t xq = x0 < 0 ? 0u : (uint32_t)x0;
+        const int32_t x00 = 4 * (int32_t)lane - (int32_t)R.ph;
+        {
+            const uint32_t xq = x00 < 0 ? 0u : (uint32_t)x00;
             const uint32_t r = min((uint32_t)__builtin_fmaf((float)xq, inv, hinv), R.cnt - 1);
-            const uint32_t voff = (uint32_t)(x0 - (int32_t)(pre * r) - 4 + (int32_t)R.ph);
+            const uint32_t voff = (uint32_t)(x00 - (int32_t)(pre * r) - 4 + (int32_t)R.ph);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)&buf[R.base + R.OD], 4, voff, 0, 0, 2);
+        }
+        if (R.nD <= kWave) return;
+        const uint32_t x1 = (uint32_t)(x00 + 256);  // > 0
+        uint32_t r = (uint32_t)__builtin_fmaf((float)x1, inv, hinv);
+        int32_t rem = (int32_t)(x1 - r * S);  // in [0, S)
+        uint32_t voff = x1 - pre * r - 4 + R.ph;
+        const uint32_t q = 256 / S;
+        const int32_t dq = 256 - (int32_t)(q * S);      // in [0, S)
+        const uint32_t dv = 256 - pre * q;              // source step when the record steps by q
+        for (uint32_t i = 1; i * kWave < R.nD; i++) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, (__attribute__((address_space(3))) void *)&buf[R.base + R.OD + i * kWave], 4,
                 voff, 0, 0, 2);
+            rem += dq;
+            const bool c = rem >= (int32_t)S;
+            rem = c ? rem - (int32_t)S : rem;
+            voff += c ? dv - pre : dv;
         }
         return;
     }
@@ -1104,11 +1130,23 @@ __device__ __forceinline__ void region_finish(const RegionPlan &R, uint32_t *buf
     const uint32_t lane = lane_id();
     uint8_t *ob = reinterpret_cast<uint8_t *>(buf + R.base + R.OD) + R.ph;
     if (lane < R.cnt) {
+        // dword stores where the field is dword-aligned in LDS (fixed-size
+        // records of a multiple of 4 bytes: every record), bytes otherwise
+        const uint32_t A = R.ph + R.P;
+        if ((A & 3) == 0) *reinterpret_cast<uint32_t *>(ob + R.P) = R.len;
+        else {
 #pragma unroll
-        for (uint32_t b = 0; b < 4; b++) ob[R.P + b] = (uint8_t)(R.len >> (8 * b));
+            for (uint32_t b = 0; b < 4; b++) ob[R.P + b] = (uint8_t)(R.len >> (8 * b));
+        }
         if (G == LSM_GRAMMAR_IDX) {
+            if (((A + R.len) & 3) == 0) {
+                uint32_t *o = reinterpret_cast<uint32_t *>(ob + R.P + 4 + R.len);
+                o[0] = (uint32_t)R.xo;
+                o[1] = (uint32_t)(R.xo >> 32);
+            } else {
 #pragma unroll
-            for (uint32_t b = 0; b < 8; b++) ob[R.P + 4 + R.len + b] = (uint8_t)(R.xo >> (8 * b));
+                for (uint32_t b = 0; b < 8; b++) ob[R.P + 4 + R.len + b] = (uint8_t)(R.xo >> (8 * b));
+            }
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1123,12 +1161,14 @@ __device__ __forceinline__ void region_finish(const RegionPlan &R, uint32_t *buf
         if (u0 >= 0 && u0 + 16 <= tot) {
             const uint32_t q = q0 + 4 * e;
             const u32x4 v = *reinterpret_cast<const u32x4 *>(&img[q]);
-            const uint32_t v4 = img[q + 4];
-            u32x4 o;
-            o.x = funnel(v.x, v.y, R.sh);
-            o.y = funnel(v.y, v.z, R.sh);
-            o.z = funnel(v.z, v.w, R.sh);
-            o.w = funnel(v.w, v4, R.sh);
+            u32x4 o = v;
+            if (R.sh) {  // wave-uniform: source and image share their dword phase otherwise
+                const uint32_t v4 = img[q + 4];
+                o.x = funnel(v.x, v.y, R.sh);
+                o.y = funnel(v.y, v.z, R.sh);
+                o.z = funnel(v.z, v.w, R.sh);
+                o.w = funnel(v.w, v4, R.sh);
+            }
             __builtin_nontemporal_store(o, &dA[e]);
         } else {
             gptr_t<uint8_t> db = (gptr_t<uint8_t>)(dA + e);
@@ -1567,32 +1607,59 @@ __global__ __launch_bounds__(64) void sst_meta_kernel(SstArgs a) { sst_meta_body
 //    loses 2^64: its residue less 2^64 mod m), by bitfield insert.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-template <uint32_t K>
-__device__ __forceinline__ void or_key_locations(const u32x4 x, const u32x2 y, uint32_t k, uint32_t m,
-                                                 uint32_t c64, uint32_t base) {
-    const uint32_t raw[6] = {x.x, x.y, x.z, x.w, y.x, y.y};
+// A hash record (store_hash_rec) unpacked: the residues of the four class
+// bases (location c of class c) and each class's three steps, the carried
+// ones already less 2^64 mod m: location 4(n + 1) + c = r[c] + st[c][n] mod m.
+struct HashRecSteps {
     uint32_t r[4];
+    uint32_t st[4][3];
+};
+
+__device__ __forceinline__ HashRecSteps unpack_hash_rec(const u32x4 x, uint32_t m, uint32_t c64) {
+    constexpr uint32_t kRes = (1u << kHashRecBits) - 1;
+    const uint32_t raw[4] = {x.x, x.y, x.z, x.w};
+    HashRecSteps H;
 #pragma unroll
-    for (uint32_t c = 0; c < 4; c++) r[c] = raw[c] & 0x3FFFFFFFu;
-    const uint32_t d2 = raw[4] & 0x3FFFFFFFu, d3 = raw[5] & 0x3FFFFFFFu;
+    for (uint32_t c = 0; c < 4; c++) H.r[c] = raw[c] & kRes;
+    // X = res(4 h2) | a << 21 | b << 22 from the top bytes of dwords 0-2
+    const uint32_t X = __builtin_amdgcn_perm(raw[1], raw[0], 0x0c0c0703u) |
+                       (raw[2] >> 24) << 16;
+    const uint32_t d2 = X & kRes;
+    // res(T) = res(base2) - res(base0) + a c64, res(4 h3) = 2 res(T) - b c64 (mod m)
+    uint32_t rt = H.r[2] - H.r[0];
+    rt = min(rt, rt + m);
+    rt = (X >> 21) & 1 ? rt + c64 : rt;
+    rt = min(rt, rt - m);
+    uint32_t d3 = rt << 1;
+    d3 = min(d3, d3 - m);
+    d3 = (X >> 22) & 1 ? d3 - c64 : d3;
+    d3 = min(d3, d3 + m);
+    // the steps less 2^64 mod m, for a step whose 64-bit add wraps
     const uint32_t t2 = d2 - c64, t3 = d3 - c64;
     const uint32_t w2 = min(t2, t2 + m), w3 = min(t3, t3 + m);
-    uint32_t st[4][3];
 #pragma unroll
     for (uint32_t c = 0; c < 4; c++) {
         const bool a2 = c == 0 || c == 3;
 #pragma unroll
         for (uint32_t n = 0; n < 3; n++) {
-            // all-ones where the step from location 4n + c carries (carry bit
-            // 3c + n = bit 30 + b of dword q), then one bitfield insert (the
-            // compiler's and / compare / cndmask form is three VALU)
-            const uint32_t bit = 3 * c + n, q = bit >> 1, b = bit & 1;
-            const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)raw[q], 30 + b, 1);
+            // all-ones where the step from location 4n + c carries (bit
+            // 21 + n of dword c), then one bitfield insert (the compiler's
+            // and / compare / cndmask form is three VALU)
+            const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)raw[c], kHashRecBits + n, 1);
             uint32_t v;
             __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(v) : "v"(msk), "v"(a2 ? w2 : w3), "v"(a2 ? d2 : d3));
-            st[c][n] = v;
+            H.st[c][n] = v;
         }
     }
+    return H;
+}
+
+template <uint32_t K, bool Masked>
+__device__ __forceinline__ void or_key_locations(const u32x4 x, uint32_t k, uint32_t m, uint32_t c64,
+                                                 uint32_t base, uint32_t lo, uint32_t span) {
+    HashRecSteps H = unpack_hash_rec(x, m, c64);
+    uint32_t *r = H.r;
+    auto &st = H.st;
 #pragma unroll
     for (uint32_t j = 0; j < kSplitMaxK; j++) {
         const uint32_t c = j & 3, n = j >> 2;  // compile-time: r[] stays in registers
@@ -1603,8 +1670,9 @@ __device__ __forceinline__ void or_key_locations(const u32x4 x, const u32x2 y, u
         // (shift + shift-add: the compiler's shift / and / add form is three)
         uint32_t a;
         __asm__("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(p >> 5), "v"(base));
-        __hip_atomic_fetch_or((lds_u32 *)(size_t)a, 1u << (p & 31), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!Masked || p - lo < span)
+            __hip_atomic_fetch_or((lds_u32 *)(size_t)a, 1u << (p & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         if (n < 3) {
             const uint32_t t = p + st[c][n];
             r[c] = min(t, t - m);
@@ -1615,29 +1683,25 @@ __device__ __forceinline__ void or_key_locations(const u32x4 x, const u32x2 y, u
 // Filter blockIdx.x, slice blockIdx.y: every key's k locations rebuilt from
 // its record, the slice's bits ORed in LDS, then stored big-endian into the
 // image; the first slice's workgroup also writes the file's framing.
-template <uint32_t K>
+template <uint32_t K, bool Masked>
 __device__ __forceinline__ void bloom_or_body(const BloomOrArgs &a, uint64_t s, uint64_t e,
-                                              uint32_t base) {
+                                              uint32_t base, uint32_t lo, uint32_t span) {
     const uint32_t m = a.m, c64 = a.c64;
     const uint64_t k0 = uni64(a.file_start[0]);
     // the file's records through one buffer resource: the record offset is
-    // a 32-bit register stepping by 24 KiB per round, and the loads two
+    // a 32-bit register stepping by 16 KiB per round, and the loads two
     // rounds ahead past the last key return zeros (never used)
-    const rsrc_t rs = make_rsrc(a.rec + kHashRecDwords * (s - k0), (uint32_t)(24 * (e - s)));
-    uint32_t vo = 24 * threadIdx.x;
-    constexpr uint32_t kStep = 24 * 1024;
+    constexpr uint32_t kRec = 4 * kHashRecDwords;
+    const rsrc_t rs = make_rsrc(a.rec + kHashRecDwords * (s - k0), (uint32_t)(kRec * (e - s)));
+    uint32_t vo = kRec * threadIdx.x;
+    constexpr uint32_t kStep = kRec * 1024;
     u32x4 xa = ld_b128(rs, vo), xb = ld_b128(rs, vo + kStep);
-    u32x2 ya = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + 16, 0, 0);
-    u32x2 yb = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + kStep + 16, 0, 0);
     for (uint64_t i = s + threadIdx.x; i < e; i += 1024) {
         const u32x4 x = xa;
-        const u32x2 y = ya;
         xa = xb;
-        ya = yb;
         vo += kStep;
         xb = ld_b128(rs, vo + kStep);
-        yb = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + kStep + 16, 0, 0);
-        or_key_locations<K>(x, y, a.k, m, c64, base);
+        or_key_locations<K, Masked>(x, a.k, m, c64, base, lo, span);
     }
 }
 
@@ -1652,10 +1716,22 @@ __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs s
     __syncthreads();
     const uint64_t s = uni64(a.file_start[f]), e = uni64(a.file_start[f + 1]);
     // lo is a multiple of 64: the slice's bit p sits in LDS word (p - lo) >> 5,
-    // bit p & 31; base = -lo / 8 bytes, plus the array's own LDS address
-    const uint32_t base = (uint32_t)(size_t)(lds_u32 *)lds_bits - lo / 8;
-    if (a.k == kSplitMaxK) bloom_or_body<kSplitMaxK>(a, s, e, base);
-    else bloom_or_body<0>(a, s, e, base);
+    // bit p & 31; base = -lo / 8 bytes, plus the array's own LDS address.
+    // The unmasked ORs rely on lds_bits being the workgroup's only LDS, at
+    // address 0: a location below the slice then wraps below zero and one
+    // above it lies past the allocation, and the LDS drops both.  This
+    // kernel and everything it calls (sst_meta_body, store_filter_slice)
+    // declare no static __shared__ (tests/test_source_invariants.py); should
+    // the array ever not start at 0, the slice test is made per location
+    // instead (a wave-uniform choice, never taken in this build).
+    const uint32_t lds0 = (uint32_t)(size_t)(lds_u32 *)lds_bits;
+    const uint32_t base = lds0 - lo / 8, span = hi - lo;
+    if (lds0 == 0) {
+        if (a.k == kSplitMaxK) bloom_or_body<kSplitMaxK, false>(a, s, e, base, lo, span);
+        else bloom_or_body<0, false>(a, s, e, base, lo, span);
+    } else {
+        bloom_or_body<0, true>(a, s, e, base, lo, span);
+    }
     __syncthreads();
     const uint64_t hdr = sst_header_bytes(a.koff, s, e);
     store_filter_slice(WgGroup{}, lds_bits, lo / 64, hi == a.m ? a.nwords : (uint64_t)(hi + 63) / 64,
@@ -2293,8 +2369,19 @@ struct LvWs {
     uint32_t *grid;   // [nfile][nwg]: the table's first slot in the workgroup
     uint32_t *cnt;    // [nfile][nwg]: the table's probes in the workgroup
     uint32_t *ids;    // [nwg * 2048] probe of each slot
-    uint64_t *hash;   // [nwg * 2048 * 4] its sum256
+    u32x4 *rec;       // [nwg * 2048] its 16-byte hash record (lv_compact tables),
+                      // else h0, h1 of its sum256
+    u32x4 *ext;       // [nwg * 2048] h2, h3 (tables that are not lv_compact)
 };
+
+// A table whose filter takes the 16-byte hash record of the encode path
+// (store_hash_rec: m <= 2^21, k <= 16; go-lsm's 1.6 Mbit, k = 16): classify
+// stores the record for the table's m, and the test rebuilds the locations
+// from it by additions -- 16 bytes per probe through the workspace instead
+// of the 32-byte sum256, and no modulo in the test.
+__device__ __forceinline__ bool lv_compact(const McFile &F) {
+    return F.m != 0 && F.m <= (1ull << kHashRecBits) && F.k <= kSplitMaxK;
+}
 
 LvWs lv_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
     LvWs w{};
@@ -2311,7 +2398,8 @@ LvWs lv_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) 
     w.grid = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
     w.cnt = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
     w.ids = reinterpret_cast<uint32_t *>(take(4 * (nwg ? nwg : 1) * kLvProbes));
-    w.hash = reinterpret_cast<uint64_t *>(take(32 * (nwg ? nwg : 1) * kLvProbes));
+    w.rec = reinterpret_cast<u32x4 *>(take(16 * (nwg ? nwg : 1) * kLvProbes));
+    w.ext = reinterpret_cast<u32x4 *>(take(16 * (nwg ? nwg : 1) * kLvProbes));
     if (total) *total = at;
     return w;
 }
@@ -2466,8 +2554,14 @@ __global__ __launch_bounds__(kLvThreads) void lv_classify_kernel(const uint8_t *
         const uint64_t i = k_begin + (uint64_t)blockIdx.x * kLvProbes + p * kLvThreads + t;
         const uint64_t slot = (uint64_t)blockIdx.x * kLvProbes + lh[cand[p]] + rank[p];
         w.ids[slot] = (uint32_t)(i - k_begin);
-        *(gptr_t<u64x2>)(gbl(w.hash) + 4 * slot) = u64x2{hh[p][0], hh[p][1]};
-        *(gptr_t<u64x2>)(gbl(w.hash) + 4 * slot + 2) = u64x2{hh[p][2], hh[p][3]};
+        const McFile &F = w.files[cand[p]];
+        if (lv_compact(F)) {
+            store_hash_rec(hh[p], (uint32_t)F.m, (uint32_t)F.mr, (uint32_t)(F.mr >> 32),
+                           reinterpret_cast<uint32_t *>(w.rec + slot));
+        } else {
+            *(gptr_t<u64x2>)gbl(w.rec + slot) = u64x2{hh[p][0], hh[p][1]};
+            *(gptr_t<u64x2>)gbl(w.ext + slot) = u64x2{hh[p][2], hh[p][3]};
+        }
     }
 }
 
@@ -2525,6 +2619,33 @@ __device__ __forceinline__ uint32_t filter_test(const McFile &F, const uint64_t 
     return r;
 }
 
+// filter_test from a probe's hash record (lv_compact tables): the k <= 16
+// locations by additions (unpack_hash_rec), each bit read as filter_test does.
+__device__ __forceinline__ uint32_t filter_test_rec(const McFile &F, const HashRecSteps &H0,
+                                                    uint32_t m, const uint8_t *lb, uint64_t in_lds,
+                                                    const uint8_t *src) {
+    uint32_t r[4] = {H0.r[0], H0.r[1], H0.r[2], H0.r[3]};
+    uint32_t bits = 1;
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t c = j & 3, n = j >> 2;
+        if (j >= F.k) break;
+        const uint32_t p = r[c];
+        if (p >= F.nbits) {
+            bits = 0;  // bitset.Test is false past its length
+        } else {
+            const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+            const uint32_t byte = q < in_lds ? lb[q] : gbl(src)[q];
+            bits &= byte >> (p & 7);
+        }
+        if (n < 3) {
+            const uint32_t t = p + H0.st[c][n];
+            r[c] = min(t, t - m);
+        }
+    }
+    return bits & 1;
+}
+
 __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
                                                              uint32_t nwg, LvWs w, uint64_t k_begin,
                                                              uint8_t *may) {
@@ -2558,12 +2679,17 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
         }
         return (uint64_t)a * kLvProbes + w.grid[(uint64_t)f * nwg + a] + (q - sb[a]);
     };
+    const bool compact = lv_compact(F);
+    const uint32_t m32 = (uint32_t)F.m;
+    // 2^64 mod m for the record's carried steps
+    const uint32_t c64 = compact ? (mod_small(~0ull, m32, (uint32_t)F.mr, (uint32_t)(F.mr >> 32)) + 1) % m32 : 0u;
     uint32_t q = t, id = 0;
-    uint64_t h[4] = {0, 0, 0, 0};
+    u32x4 x = {0, 0, 0, 0}, y = {0, 0, 0, 0};
     if (q < total) {  // the first probe's hash in flight during the fill
         const uint64_t sl = slot_of(q);
         id = w.ids[sl];
-        for (int j = 0; j < 4; j++) h[j] = w.hash[4 * sl + j];
+        x = w.rec[sl];
+        if (!compact) y = w.ext[sl];
     }
     const uint8_t *src = img + F.words_at;
     uint32_t delta;
@@ -2574,16 +2700,26 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
     while (q < total) {
         const uint32_t qn = q + kLvThreads;
         uint32_t idn = 0;
-        uint64_t hn[4] = {0, 0, 0, 0};
+        u32x4 xn = {0, 0, 0, 0}, yn = {0, 0, 0, 0};
         if (qn < total) {
             const uint64_t sl = slot_of(qn);
             idn = w.ids[sl];
-            for (int j = 0; j < 4; j++) hn[j] = w.hash[4 * sl + j];
+            xn = w.rec[sl];
+            if (!compact) yn = w.ext[sl];
         }
-        may[k_begin + id] = (uint8_t)filter_test(F, h, lb, in_lds, src);
+        uint32_t r;
+        if (compact) {
+            r = filter_test_rec(F, unpack_hash_rec(x, m32, c64), m32, lb, in_lds, src);
+        } else {
+            const uint64_t h[4] = {(uint64_t)x.y << 32 | x.x, (uint64_t)x.w << 32 | x.z,
+                                   (uint64_t)y.y << 32 | y.x, (uint64_t)y.w << 32 | y.z};
+            r = filter_test(F, h, lb, in_lds, src);
+        }
+        may[k_begin + id] = (uint8_t)r;
         q = qn;
         id = idn;
-        for (int j = 0; j < 4; j++) h[j] = hn[j];
+        x = xn;
+        y = yn;
     }
 }
 
@@ -2617,6 +2753,104 @@ __global__ __launch_bounds__(256) void lv_probe_kernel(const uint8_t *img, uint3
         }
         may[i] = r;
     }
+}
+
+// ---- batched Get past MayContain: Iterator.Seek + GetValueByOffset ---------
+//
+// searchFromTable (sstable/manager.go:209-223) after its MayContain: Seek
+// (sstable/block/index.go:157-181: left, right := 0, n; mid := left +
+// (right-left)/2; Indexes[mid].Key < target -> left = mid + 1, else right =
+// mid; valid only if Indexes[left].Key == target) over the table's decoded
+// IndexBlock, then Iterator.Value -> GetValueByOffset (sstable.go:271-296:
+// Seek to the entry's offset, Value.DecodeFrom, kv.go:181-200).  One thread
+// per probe; the bisection compares 16-byte big-endian prefixes loaded from
+// the index entries in the image (the bytes past them only on a prefix tie).
+struct GetArgs {
+    const uint8_t *img;
+    const uint64_t *file_off, *file_len;
+    const lsm_sst_meta *meta;
+    uint32_t nfile;
+    const uint64_t *rec_base;
+    const lsm_rec_desc *idx_desc;
+    const int64_t *idx_value;
+    const uint8_t *keys;
+    const uint64_t *koff;
+    uint64_t nkeys;
+    const int32_t *table;
+    const uint8_t *may;
+    int32_t *result;
+    lsm_rec_desc *value;
+};
+
+// key bytes [p, p + len) as four big-endian words, zero padded past len
+// (reads 16 bytes at p: the input slack covers a key that ends a buffer)
+__device__ __forceinline__ void key_prefix(const uint8_t *p, uint64_t len, uint32_t kw[4]) {
+    uint64_t f0 = ldg_u64_unaligned(p), f1 = ldg_u64_unaligned(p + 8);
+    if (len < 8) { f0 &= len ? (~0ull >> (64 - 8 * len)) : 0; f1 = 0; }
+    else if (len < 16) f1 &= len > 8 ? (~0ull >> (128 - 8 * len)) : 0;
+    kw[0] = __builtin_bswap32((uint32_t)f0);
+    kw[1] = __builtin_bswap32((uint32_t)(f0 >> 32));
+    kw[2] = __builtin_bswap32((uint32_t)f1);
+    kw[3] = __builtin_bswap32((uint32_t)(f1 >> 32));
+}
+
+__global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.nkeys) return;
+    int32_t res = LSM_GET_ABSENT;
+    lsm_rec_desc v{0, 0, 0};
+    const int32_t t = a.table[i];
+    if (a.may[i] && t >= 0 && (uint32_t)t < a.nfile) {
+        const lsm_sst_meta &M = a.meta[t];
+        const uint64_t fo = a.file_off[t], fl = a.file_len[t];
+        const uint64_t base = a.rec_base ? a.rec_base[t] : fo / 4;
+        const uint32_t n = M.nidx;
+        const uint64_t k0 = a.koff[i], kl = a.koff[i + 1] - k0;
+        const uint8_t *kp = a.keys + k0;
+        uint32_t kw[4];
+        key_prefix(kp, kl, kw);
+        uint32_t left = 0, right = n;
+        while (left < right) {
+            const uint32_t mid = left + (right - left) / 2;
+            const lsm_rec_desc d = a.idx_desc[base + mid];
+            const uint8_t *ep = a.img + d.rec_off + 4;
+            uint32_t ew[4];
+            key_prefix(ep, d.key_len, ew);
+            const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
+            if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
+            else right = mid;
+        }
+        bool hit = false;
+        if (left < n) {
+            const lsm_rec_desc d = a.idx_desc[base + left];
+            const uint8_t *ep = a.img + d.rec_off + 4;
+            hit = d.key_len == kl && go_cmp(ep, d.key_len, kp, kl) == 0;
+        }
+        if (hit) {
+            const int64_t off = a.idx_value[base + left];
+            if (off < 0) {
+                res = LSM_GET_SEEK_FAILED;  // file.Seek to a negative offset
+            } else {
+                // Value.DecodeFrom from the file at off: u32 length, cap, bytes
+                const uint64_t rem = (uint64_t)off < fl ? fl - (uint64_t)off : 0;
+                if (rem < 4) {
+                    res = LSM_GET_VALUE_LENGTH;
+                } else {
+                    const uint8_t *vp = a.img + fo + (uint64_t)off;
+                    const uint32_t vl = (uint32_t)vp[0] | (uint32_t)vp[1] << 8 | (uint32_t)vp[2] << 16 |
+                                        (uint32_t)vp[3] << 24;
+                    if (vl > (1u << 30)) res = LSM_GET_VALUE_TOO_LONG;
+                    else if (rem - 4 < vl) res = LSM_GET_VALUE_SHORT;
+                    else {
+                        res = LSM_GET_FOUND;
+                        v = lsm_rec_desc{fo + (uint64_t)off, 0, vl};
+                    }
+                }
+            }
+        }
+    }
+    a.result[i] = res;
+    a.value[i] = v;
 }
 
 template <int G>
@@ -2730,7 +2964,7 @@ static bool hash_once_bloom(uint64_t m) { return m <= (1ull << 30) && bloom_slic
 // bloom_or_kernel; a file's hash records are addressed by one 32-bit buffer
 // offset, so at most 2^27 records per file)
 static bool split_bloom(uint64_t m, uint32_t k, uint64_t max_file_records) {
-    return hash_once_bloom(m) && bloom_slices(m) == 2 && k <= kSplitMaxK &&
+    return hash_once_bloom(m) && bloom_slices(m) == 2 && m <= (1ull << kHashRecBits) && k <= kSplitMaxK &&
            max_file_records <= (1ull << 27);
 }
 
@@ -3083,6 +3317,41 @@ extern "C" int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img,
     if (ws_bytes < need) return LSM_ESPACE;
     return level_search(s, d_img, static_cast<const McFile *>(d_index), nfile, d_keys, d_koff, nkeys,
                         d_table, d_may, w);
+}
+
+extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                             const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
+                             const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
+                             const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
+                             uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may,
+                             int32_t *d_result, lsm_rec_desc *d_value, void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nkeys == 0) return 0;
+    if (!d_keys || !d_koff || !d_table || !d_may || !d_result || !d_value) return LSM_EINVAL;
+    if (nfile && (!d_img || !d_file_off || !d_file_len || !d_meta || !d_idx_desc || !d_idx_value))
+        return LSM_EINVAL;
+    GetArgs a;
+    a.img = d_img;
+    a.file_off = d_file_off;
+    a.file_len = d_file_len;
+    a.meta = d_meta;
+    a.nfile = nfile;
+    a.rec_base = d_rec_base;
+    a.idx_desc = d_idx_desc;
+    a.idx_value = d_idx_value;
+    a.keys = d_keys;
+    a.koff = d_koff;
+    a.nkeys = nkeys;
+    a.table = d_table;
+    a.may = d_may;
+    a.result = d_result;
+    a.value = d_value;
+    const uint64_t grid = (nkeys + 255) / 256;
+    if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
+    hipLaunchKernelGGL(level_get_kernel, dim3((uint32_t)grid), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 extern "C" int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,

@@ -1239,9 +1239,13 @@ __global__ __launch_bounds__(kMergeThreads) void merge_emit_kernel(
 // length, value length) -- tile sums (the lengths kept), the tile sums'
 // scan (merge_scan_partials), then each slot's offsets -- where two scans
 // of separately gathered lengths took 88 us for 3.3M pairs.
-// the gather's pair count: the host's, or lsm_gather_kvs_dev's device count
-__device__ __forceinline__ uint32_t gather_count(uint32_t nout, const uint64_t *d_nout) {
-    return d_nout ? (uint32_t)*d_nout : nout;
+// the gather's pair count: the host's, or lsm_gather_kvs_dev's device count,
+// capped at the bound the grid and the klen / vlen / koff / voff arrays are
+// sized from (a count above it is a caller error; the gather stays in bounds)
+__device__ __forceinline__ uint32_t gather_count(uint32_t nmax, const uint64_t *d_nout) {
+    if (!d_nout) return nmax;
+    const uint64_t n = *d_nout;
+    return n < nmax ? (uint32_t)n : nmax;
 }
 
 __global__ __launch_bounds__(kMergeThreads) void gather_scan_tiles(MergeIn m, const uint32_t *idx,

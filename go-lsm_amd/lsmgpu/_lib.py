@@ -115,6 +115,10 @@ SIGNATURES = {
                                                      ctypes.c_uint64, ctypes.c_void_p, c_u8p,
                                                      ctypes.c_void_p, ctypes.c_size_t,
                                                      ctypes.c_void_p]),
+    "lsm_level_get": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u64p, ctypes.c_void_p,
+                                     ctypes.c_uint32, c_u64p, ctypes.c_void_p, ctypes.c_void_p,
+                                     c_u8p, c_u64p, ctypes.c_uint64, ctypes.c_void_p, c_u8p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lsm_merge_kvs_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint64]),
     "lsm_merge_kvs": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
@@ -163,7 +167,7 @@ SIGNATURES = {
     "lsm_stream_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 5   # LSM_ABI_VERSION this binding is written against
+ABI_VERSION = 6   # LSM_ABI_VERSION this binding is written against
 INPUT_SLACK = 32  # LSM_INPUT_SLACK: device inputs are padded by this much
 
 _lib = None

@@ -39,8 +39,9 @@ extern "C" {
  * v2 / v3 contract of exactly 2 ({nout, nfiles}).
  * v5: lsm_merge_kvs_async and lsm_gather_kvs_dev (the merge's counts stay on
  * the device; the gather reads its pair count there); the level sparse index
- * (lsm_level_index_build, lsm_level_may_contain_indexed). */
-#define LSM_ABI_VERSION 5
+ * (lsm_level_index_build, lsm_level_may_contain_indexed).
+ * v6: lsm_level_get (the batched Get past MayContain: Seek + the value). */
+#define LSM_ABI_VERSION 6
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
 /* Record grammars (all fixed-width little-endian). */
@@ -314,6 +315,35 @@ int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img, const void
                                   uint64_t nkeys, int32_t *d_table, uint8_t *d_may,
                                   void *d_workspace, size_t ws_bytes, void *stream);
 
+/* Batched searchFromTable past its MayContain (sstable/manager.go:209-223):
+ * for key i with d_may[i] = 1 (lsm_level_may_contain's answer for table
+ * d_table[i]), Iterator.Seek over that table's IndexBlock (sstable/block/
+ * index.go:157-181: Go's bisection for the first entry whose key >= the
+ * target, valid only on an exact match) and Iterator.Value ->
+ * GetValueByOffset (sstable.go:271-296: Value.DecodeFrom, kv.go:181-200, at
+ * the entry's offset in the file).  The index is lsm_decode_sst's output for
+ * the same images (d_meta, d_idx_desc, d_idx_value, with the same
+ * d_rec_base or offset placement); file f is d_img[file_off[f] ..
+ * + file_len[f]).  d_result[i] is a lsm_get_result; on LSM_GET_FOUND
+ * d_value[i] is a view of the value {rec_off = offset in d_img of its u32
+ * length prefix, key_len = 0, val_len}; otherwise d_value[i] is zero.  The
+ * Seek runs over the nidx entries the decode kept (a table whose index did
+ * not decode is one the Manager would not have loaded, manager.go:226-275). */
+enum lsm_get_result {
+    LSM_GET_ABSENT = 0,         /* (nil, nil): not MayContain, or no entry equals the key        */
+    LSM_GET_FOUND = 1,          /* the value, d_value[i]                                          */
+    LSM_GET_SEEK_FAILED = 2,    /* negative offset: sstable.go:284-287 "seek to offset failed"  */
+    LSM_GET_VALUE_LENGTH = 3,   /* < 4 bytes left: kv.go:183-186 "decode value length"          */
+    LSM_GET_VALUE_TOO_LONG = 4, /* kv.go:188-190 "invalid value length: %d" (> 1<<30)           */
+    LSM_GET_VALUE_SHORT = 5,    /* kv.go:192-196 "decode value"                                  */
+};
+int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                  const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
+                  const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
+                  const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
+                  uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may, int32_t *d_result,
+                  lsm_rec_desc *d_value, void *stream);
+
 /* ---- encode ---------------------------------------------------------------- */
 
 /* Batch encode of a columnar record batch (CSR: record i's key is
@@ -347,7 +377,7 @@ uint64_t lsm_sst_image_size_host(const uint64_t *koff, const uint64_t *voff, uin
 uint64_t lsm_filter_block_size(uint64_t m);
 /* Device workspace lsm_build_sst needs for nfile files of at most
  * max_file_records records each: when the filter splits into two LDS slices
- * (go-lsm's default m), a 24-byte hash record per key (k <= 16: the key hash
+ * (go-lsm's default m), a 16-byte hash record per key (k <= 16: the key hash
  * runs inside the region writer) or the slice-1 bit positions (k u32 per
  * record); else a token 16 bytes. */
 size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_file_records, uint64_t m,

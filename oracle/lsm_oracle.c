@@ -694,6 +694,53 @@ void ora_level_may_contain(const uint8_t *img, const uint64_t *file_off, const o
     }
 }
 
+/* searchFromTable past MayContain (sstable/manager.go:209-223): Iterator.Seek
+ * (sstable/block/index.go:157-181) over the table's decoded IndexBlock, then
+ * Iterator.Value (sstable/iterator.go:34-46) -> GetValueByOffset
+ * (sstable.go:271-296) -> Value.DecodeFrom (kv.go:181-200) reading the file. */
+void ora_level_get(const uint8_t *img, const uint64_t *file_off, const uint64_t *file_len,
+                   const ora_sst_meta *meta, const ora_desc *idx_desc, const int64_t *idx_val,
+                   const uint64_t *idx_base, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
+                   uint64_t k1, const int32_t *table, const uint8_t *may, int32_t *res,
+                   uint64_t *val_off, uint32_t *val_len) {
+    for (uint64_t i = k0; i < k1; i++) {
+        const uint64_t o = i - k0;
+        res[o] = ORA_GET_ABSENT;
+        val_off[o] = 0;
+        val_len[o] = 0;
+        if (!may[o] || table[o] < 0) continue; /* searchFromTable: !MayContain -> (nil, nil) */
+        const uint32_t t = (uint32_t)table[o];
+        const uint8_t *file = img + file_off[t];
+        const ora_desc *D = idx_desc + idx_base[t];
+        const int64_t *V = idx_val + idx_base[t];
+        const uint64_t n = meta[t].nidx;
+        const uint8_t *key = keys + koff[i];
+        const uint64_t kl = koff[i + 1] - koff[i];
+        /* Seek: left, right := 0, len; for left < right { mid := left + (right-left)/2;
+         * if Indexes[mid].Key < target { left = mid + 1 } else { right = mid } } */
+        uint64_t left = 0, right = n;
+        while (left < right) {
+            const uint64_t mid = left + (right - left) / 2;
+            if (go_strcmp(file + D[mid].rec_off + 4, D[mid].key_len, key, kl) < 0) left = mid + 1;
+            else right = mid;
+        }
+        /* out of range or not an exact match: invalid, it.Valid() false -> (nil, nil) */
+        if (left >= n || go_strcmp(file + D[left].rec_off + 4, D[left].key_len, key, kl) != 0)
+            continue;
+        const int64_t off = V[left];
+        if (off < 0) { res[o] = ORA_GET_SEEK_FAILED; continue; } /* file.Seek: negative position */
+        const uint64_t fl = file_len[t];
+        const uint64_t rem = (uint64_t)off < fl ? fl - (uint64_t)off : 0;
+        if (rem < 4) { res[o] = ORA_GET_VALUE_LENGTH; continue; } /* binary.Read: EOF */
+        const uint32_t vl = ld_u32le(file + off);
+        if (vl > (1u << 30)) { res[o] = ORA_GET_VALUE_TOO_LONG; continue; }
+        if (rem - 4 < vl) { res[o] = ORA_GET_VALUE_SHORT; continue; } /* io.ReadFull */
+        res[o] = ORA_GET_FOUND;
+        val_off[o] = file_off[t] + (uint64_t)off;
+        val_len[o] = vl;
+    }
+}
+
 /* ---- config 1 from a file, the reference's syscall pattern --------------- */
 /* SSTable.DecodeFrom(path) (sstable.go:87-127) then GetDataBlockFromFile(path)
  * (sstable.go:227-268) over an unbuffered *os.File: every binary.Read and

@@ -174,6 +174,25 @@ void ora_level_may_contain(const uint8_t *img, const uint64_t *file_off, const o
                            uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
                            uint64_t k1, int32_t *table, uint8_t *may);
 
+/* searchFromTable past its MayContain (sstable/manager.go:209-223) for keys
+ * [k0, k1) with may[i - k0] = 1 in table t = table[i - k0]: Iterator.Seek
+ * (sstable/block/index.go:157-181: the first entry whose key >= the target by
+ * Go's bisection, valid only on an exact match) over t's decoded index (the
+ * ora_sst_decode rows idx_base[t] .. + meta[t].nidx of idx_desc / idx_val,
+ * rec_off relative to the file), then GetValueByOffset (sstable.go:271-296):
+ * Value.DecodeFrom (kv.go:181-200) at the entry's offset in the file of
+ * file_len[t] bytes at img + file_off[t].  res: ORA_GET_*; on ORA_GET_FOUND
+ * val_off = offset in img of the value's length prefix, val_len its length. */
+enum {
+    ORA_GET_ABSENT = 0, ORA_GET_FOUND = 1, ORA_GET_SEEK_FAILED = 2, ORA_GET_VALUE_LENGTH = 3,
+    ORA_GET_VALUE_TOO_LONG = 4, ORA_GET_VALUE_SHORT = 5,
+};
+void ora_level_get(const uint8_t *img, const uint64_t *file_off, const uint64_t *file_len,
+                   const ora_sst_meta *meta, const ora_desc *idx_desc, const int64_t *idx_val,
+                   const uint64_t *idx_base, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
+                   uint64_t k1, const int32_t *table, const uint8_t *may, int32_t *res,
+                   uint64_t *val_off, uint32_t *val_len);
+
 /* ---- compaction merge ----------------------------- */
 
 enum { ORA_TIE_INPUT = 0, ORA_TIE_GOHEAP = 1 };

@@ -54,6 +54,7 @@ def lib():
         "ora_filter_test": (ctypes.c_int, [vp, u64, u64, u64, vp, u64]),
         "ora_may_contain_batch": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp]),
         "ora_level_may_contain": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp, vp]),
+        "ora_level_get": (None, [vp, vp, vp, vp, vp, vp, vp, vp, vp, u64, u64, vp, vp, vp, vp, vp]),
         "ora_estimate_parameters": (None, [u64, ctypes.c_double, vp, vp]),
         "ora_filter_block_size": (u64, [u64]),
         "ora_filter_encode": (u64, [vp, u64, u64, vp]),
@@ -332,3 +333,45 @@ def level_may_contain(img, file_off, metas, keys, koff, k0, k1):
     lib().ora_level_may_contain(_p(img), _p(file_off), ctypes.cast(arr, vp), nfile, _p(keys),
                                 _p(koff), k0, k1, _p(table), _p(may))
     return table[:k1 - k0], may[:k1 - k0]
+
+
+GET_ABSENT, GET_FOUND, GET_SEEK_FAILED, GET_VALUE_LENGTH, GET_VALUE_TOO_LONG, GET_VALUE_SHORT = range(6)
+
+
+def level_get_index(idx_descs, idx_vals):
+    """The tables' decoded index rows concatenated -> (desc, vals, base)."""
+    nfile = len(idx_descs)
+    base = np.zeros(max(nfile, 1), np.uint64)
+    if nfile:
+        base[:] = np.concatenate([[0], np.cumsum([len(d) for d in idx_descs])[:-1]]).astype(np.uint64)
+    desc = np.concatenate(list(idx_descs) + [np.zeros(1, DESC_DTYPE)]).astype(DESC_DTYPE)
+    vals = np.concatenate(list(idx_vals) + [np.zeros(1, np.int64)]).astype(np.int64)
+    return desc, vals, base
+
+
+def level_get(img, file_off, file_len, metas, idx_descs, idx_vals, keys, koff, k0, k1, table, may,
+              index=None):
+    """searchFromTable past MayContain (manager.go:209-223) for keys [k0, k1):
+    Iterator.Seek over the candidate table's decoded index, then
+    GetValueByOffset.  idx_descs / idx_vals: per table, sst_decode's index
+    rows (rec_off relative to the file); index: level_get_index of them,
+    prepared once.  table / may: rows k0 .. k1 of the level search.
+    -> (int32 res, uint64 val_off into img, uint32 val_len), each (k1-k0,)."""
+    img = _bytes(img)
+    nfile = len(metas)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64) if nfile else np.zeros(1, np.uint64)
+    file_len = np.ascontiguousarray(file_len, dtype=np.uint64) if nfile else np.zeros(1, np.uint64)
+    arr = metas if isinstance(metas, ctypes.Array) else (SstMeta * max(nfile, 1))(*metas)
+    desc, vals, base = index if index is not None else level_get_index(idx_descs, idx_vals)
+    keys = _bytes(keys) if len(keys) else np.zeros(1, np.uint8)
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    n = k1 - k0
+    table = np.ascontiguousarray(table, dtype=np.int32)
+    may = np.ascontiguousarray(may, dtype=np.uint8)
+    res = np.zeros(max(n, 1), np.int32)
+    voff = np.zeros(max(n, 1), np.uint64)
+    vlen = np.zeros(max(n, 1), np.uint32)
+    lib().ora_level_get(_p(img), _p(file_off), _p(file_len), ctypes.cast(arr, vp), _p(desc), _p(vals),
+                        _p(base), _p(keys), _p(koff), k0, k1, _p(table), _p(may), _p(res), _p(voff),
+                        _p(vlen))
+    return res[:n], voff[:n], vlen[:n]

@@ -31,7 +31,7 @@ def test_header_functions_exported():
 
 
 def test_abi_version():
-    assert _lib.load().lsm_abi_version() == 5
+    assert _lib.load().lsm_abi_version() == 6
     assert _lib.load().lsm_input_slack() == 32
 
 
@@ -126,3 +126,28 @@ def test_build_id_ties_library_to_sources(tmp_path):
     spec.loader.exec_module(alt_lib)
     with pytest.raises(RuntimeError, match="built from other sources"):
         alt_lib.load()
+
+
+def test_build_id_covers_compiler_flags():
+    """The id also hashes the compiler, target and flags the Makefile compiles
+    with, overrides included (`make ARCH=... HIPFLAGS=...` built a
+    library with the default id): the Makefile's defaults give the loader's
+    id, any other target or flags another one."""
+    import importlib.util
+    import subprocess
+    pkg = os.path.join(ROOT, "go-lsm_amd")
+    spec = importlib.util.spec_from_file_location("bid", os.path.join(pkg, "build_id.py"))
+    bid = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bid)
+    hipcc, arch, flags = bid.default_flags(pkg)
+    assert arch == "gfx950" and "--offload-arch=gfx950" in flags
+    assert bid.source_id(pkg, [hipcc, arch, flags]) == bid.source_id(pkg)
+    assert bid.source_id(pkg, [hipcc, "gfx942", flags.replace("gfx950", "gfx942")]) != bid.source_id(pkg)
+    assert bid.source_id(pkg, [hipcc, arch, flags + " -O0"]) != bid.source_id(pkg)
+    # the id make compiles in: defaults, and a command-line override
+    def make_id(*args):
+        out = subprocess.run(["make", "-n", "-C", pkg, "-B", "build/api.o", *args], capture_output=True,
+                             text=True, check=True).stdout
+        return out.split("LSM_BUILD_ID='\"")[1].split('"')[0]
+    assert make_id() == bid.source_id(pkg)
+    assert make_id("HIPFLAGS=-O1 --offload-arch=gfx950") != bid.source_id(pkg)

@@ -457,3 +457,43 @@ def test_async_merge_and_device_count_gather(ctx, tie):
             if vb is not None:
                 vbytes = int(a.voff[m])
                 assert torch.equal(a.vals[:vbytes], b.vals[:vbytes])
+
+
+def test_device_count_above_bound_is_capped(ctx):
+    """lsm_gather_kvs_dev with a device count larger than its bound gathers
+    exactly `bound` pairs: the offsets, keys and values equal the host-count
+    gather of those pairs, and nothing past the bound's koff / voff slot or
+    the gathered bytes is written (the count is capped on the
+    device, gather_count in merge.hip)."""
+    rng = random.Random(77)
+    pairs = random_pairs(rng, 3000, b"abc\x00", 9)
+    buf, kd, vd, kpos, vpos = lay_out(pairs, False, random.Random(6))
+    dev = ctx.torch_device
+    d_buf = lsmgpu.to_device_bytes(buf, dev)
+    d_kd = torch.from_numpy(kd.view(np.int32).reshape(-1, 4).copy()).to(dev)
+    d_vd = torch.from_numpy(vd.view(np.int32).reshape(-1, 4).copy()).to(dev)
+    want = lsmgpu.merge_kvs(ctx, d_buf, d_kd, d_vd, level=1)
+    bound = want.nout // 2
+    idx = torch.zeros(len(pairs), dtype=want.out.dtype, device=dev)  # valid pair ids past the bound
+    idx[:bound] = want.out[:bound]
+    kb = vb = buf.size + 64
+    a = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, idx, bound, kb, vb)
+    guard = 64
+    reuse = lsmgpu.codec.RecordBatch(
+        keys=torch.full((lsmgpu.pad16(kb) + 4096,), 0xEE, dtype=torch.uint8, device=dev),
+        koff=torch.full((bound + 1 + guard,), -7, dtype=torch.int64, device=dev),
+        vals=torch.full((lsmgpu.pad16(vb) + 4096,), 0xEE, dtype=torch.uint8, device=dev),
+        voff=torch.full((bound + 1 + guard,), -7, dtype=torch.int64, device=dev),
+        n=0, koff_host=None, voff_host=None)
+    reuse._ws = torch.empty(int(ctx.lib.lsm_gather_kvs_workspace_bytes(bound)), dtype=torch.uint8,
+                            device=dev)
+    d_nout = torch.tensor([bound + 500], dtype=torch.int64, device=dev)
+    b = lsmgpu.gather_kvs(ctx, d_buf, d_kd, d_vd, idx, bound, kb, vb, reuse=reuse, d_nout=d_nout)
+    torch.cuda.synchronize()
+    assert b.koff.data_ptr() == reuse.koff.data_ptr()
+    assert torch.equal(a.koff[:bound + 1], b.koff[:bound + 1])
+    assert torch.equal(a.voff[:bound + 1], b.voff[:bound + 1])
+    assert bool((b.koff[bound + 1:] == -7).all()) and bool((b.voff[bound + 1:] == -7).all())
+    kbytes, vbytes = int(a.koff[bound]), int(a.voff[bound])
+    assert torch.equal(a.keys[:kbytes], b.keys[:kbytes]) and torch.equal(a.vals[:vbytes], b.vals[:vbytes])
+    assert bool((b.keys[kbytes:] == 0xEE).all()) and bool((b.vals[vbytes:] == 0xEE).all())
