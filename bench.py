@@ -354,7 +354,10 @@ def bench_decode(args, world, rank, local):
             "blocks_per_gpu": int(nblk),
             "records_per_gpu": nrec_total,
             "parsed_bytes_per_gpu": int(parsed),
-            "parallelism": f"dp{world} (blocks round-robin, no collective)",
+            "parallelism": (f"dp{world} (logs per rank, no collective)" if args.config == "wal" else
+                            f"dp{world} (blocks round-robin, no collective)"),
+            **({"scaling_note": "weak, per-rank copy: every rank replays its own log set"}
+               if args.config == "wal" else {}),
         },
         "roofline": {
             "bound": "hbm",

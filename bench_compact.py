@@ -192,7 +192,8 @@ def bench_compact(args, world, rank, local):
                    "tie": ("goheap: container/heap's pop order for equal keys (the reference's "
                            "exact output)" if goheap else
                            "input: equal keys in input order (merge.go:41's contract)"),
-                   "parallelism": f"dp{world} (one compaction per rank, no collective)"},
+                   "parallelism": f"dp{world} (one compaction per rank, no collective)",
+                   "scaling_note": "weak, per-rank copy: every rank compacts its own copy-shaped input"},
         # the whole chain: an ideal compaction reads every input image byte
         # once and writes every output image byte once; everything between
         # (descriptors, the permutation, packed keys) is this implementation's

@@ -72,7 +72,8 @@ def bench_sst_decode(args, world, rank, local):
                                f"16 B keys / 100 B values, 2 MiB flush)",
                    "files_per_gpu": nf, "records_per_gpu": n,
                    "parsed_bytes_per_gpu": int(parsed),
-                   "parallelism": f"dp{world} (files per rank, no collective)"},
+                   "parallelism": f"dp{world} (files per rank, no collective)",
+                   "scaling_note": "weak, per-rank copy: every rank decodes its own image set"},
         "roofline": {"bound": "hbm", "kernel": "lsm_decode_sst (4 launches)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -201,7 +202,8 @@ def bench_may_contain(args, world, rank, local):
         "config": {"workload": f"{nprobe} keys x {nf} .sst files per GPU (range check + bloom "
                                f"m=1.6M k=16)", "files_per_gpu": nf, "probes_per_gpu": nprobe,
                    "false_positive_rate_absent": float(rows[~is_held].astype(bool).mean()),
-                   "parallelism": f"dp{world} (probe batches per rank, no collective)"},
+                   "parallelism": f"dp{world} (probe batches per rank, no collective)",
+                   "scaling_note": "weak, per-rank copy: every rank probes its own level copy"},
         # algorithmic bytes per launch: the hit matrix written once, the probe
         # keys and offsets read once, every file's stored filter words read once
         "roofline": {"bound": "hbm", "kernel": "lsm_may_contain (all launches)",
@@ -349,7 +351,8 @@ def bench_level_search(args, world, rank, local):
                                (" -> Iterator.Seek -> GetValueByOffset" if get else "") +
                                ", bloom m=1.6M k=16)",
                    "files_per_gpu": nf, "probes_per_gpu": nprobe,
-                   "parallelism": f"dp{world} (probe batches per rank, no collective)"},
+                   "parallelism": f"dp{world} (probe batches per rank, no collective)",
+                   "scaling_note": "weak, per-rank copy: every rank probes its own level copy"},
         "roofline": {"bound": "hbm", "kernel": "lsm_level_may_contain_indexed (all launches; the level's "
                                "sparse index built once, outside the step)" +
                                (" + lsm_level_get" if get else ""),

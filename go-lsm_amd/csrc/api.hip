@@ -46,6 +46,7 @@ extern "C" int lsm_ctx_destroy(lsm_ctx *ctx) {
         if (ctx->fork) (void)hipEventDestroy(ctx->fork);
         if (ctx->side) (void)hipStreamDestroy(ctx->side);
         if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
+        if (ctx->host_big) (void)hipHostFree(ctx->host_big);
     }
     free(ctx);
     return 0;

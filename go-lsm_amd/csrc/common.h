@@ -25,6 +25,10 @@ struct lsm_ctx {
     hipStream_t side;
     hipEvent_t fork, join;
     void *host_rb;  // kHostReadback bytes of pinned host memory
+    // grow-only pinned host buffer for LSM_TIE_GOHEAP's rank read-back and
+    // pop-order upload (pageable copies staged through the runtime: slower)
+    void *host_big;
+    size_t host_big_bytes;
 };
 constexpr size_t kHostReadback = 256 * 1024;
 

@@ -1469,6 +1469,18 @@ __global__ __launch_bounds__(256) void sst_tail_kernel(SstArgs a) {
 // much is chased twice.
 constexpr uint32_t kWalSeg = 16 * 1024;  // 12 and 8 KiB measured slower
 constexpr uint32_t kWalSegSlots = kWalSeg / 8 + 1;  // records starting in a segment
+// Scratch entry of a record of a segment's chain (wal_seg_lanes_kernel): its
+// start less the segment's start (14 bits) and its key length (18 bits;
+// kWalKlEsc: re-read from the log).  The value length is the distance to the
+// next record's start (or to the chain's exit) less 8 + the key length: 4
+// bytes per record and phase instead of a 16-byte descriptor (the scratch
+// round trip was 1.9x the replay's algorithmic bytes).
+constexpr uint32_t kWalPosBits = 14;
+constexpr uint32_t kWalKlEsc = (1u << (32 - kWalPosBits)) - 1;
+static_assert(kWalSeg <= (1u << kWalPosBits), "segment offsets fit the scratch entry");
+// fin[2q + 1] flags: the chosen phase, and a segment the stitch chased again
+// (its records in the scratch as full descriptors)
+constexpr uint32_t kWalFinPhase1 = 0x80000000u, kWalFinFull = 0x40000000u, kWalFinCount = 0x3FFFFFFFu;
 
 struct WalSeg {
     uint32_t entry, exit, nrec;
@@ -1883,13 +1895,12 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         uint32_t tot;
         const uint32_t pre = wave_excl_scan(acc_cnt, &tot);
         if (acc_cnt) {
-            u32x4 *dst = a.scratch + q * kWalSegSlots + pre;
+            uint32_t *dst = reinterpret_cast<uint32_t *>(a.scratch + q * kWalSegSlots) + pre;
             uint32_t p = acc_entry;
             for (uint32_t i = 0; i < acc_cnt; i++) {
                 uint32_t kl = 0, vl = 0;
                 L.record(p, kl, vl);
-                const uint64_t ro = off + p;
-                dst[i] = u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), kl, vl};
+                dst[i] = (p - start) | (kl < kWalKlEsc ? kl : kWalKlEsc) << kWalPosBits;
                 p += 8 + kl + vl;
             }
         }
@@ -1976,7 +1987,7 @@ __global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
                 const uint32_t xe = ch == 0 ? T0.exit : T1.exit;
                 uint32_t sum;
                 f_pre = total + wave_excl_scan(nr, &sum);
-                f_cnt = nr | (take && ch == 1 ? 0x80000000u : 0u);
+                f_cnt = nr | (take && ch == 1 ? kWalFinPhase1 : 0u);
                 total += uni(sum);
                 e = uni(__builtin_amdgcn_readlane(xe, lim));
                 if (errm) {
@@ -2015,7 +2026,7 @@ __global__ __launch_bounds__(64) void wal_stitch_kernel(WalArgs a) {
                         kWalSegSlots, nr, st, stop, &endp);
                     ex = e + endp;
                 }
-                cnt = nr | (ph == 1 ? 0x80000000u : 0u);
+                cnt = nr | (ph == 1 ? kWalFinPhase1 : ph == 2 ? kWalFinFull : 0u);
                 total += nr;
                 e = ex;
                 if (st != LSM_OK) {
@@ -2049,15 +2060,39 @@ __global__ __launch_bounds__(256) void wal_compact_kernel(WalArgs a) {
     const uint32_t s = blockIdx.x, w = blockIdx.y;
     const uint64_t q = (uint64_t)w * a.segs + s;
     const uint32_t pre = a.fin[2 * q], cf = a.fin[2 * q + 1];
-    const uint32_t cnt = cf & 0x7FFFFFFFu;
+    const uint32_t cnt = cf & kWalFinCount;
     if (cnt == 0) return;
     uint64_t base, cap;
     wal_slots(a, w, base, cap);
     u32x4 *dst = reinterpret_cast<u32x4 *>(a.out.desc);
-    const u32x4 *src = a.scratch + (q * 2 + (cf >> 31)) * kWalSegSlots;
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
-        if ((uint64_t)pre + j < cap)  // nt: written once (A/B: 997 -> 1,017 GiB/s)
-            __builtin_nontemporal_store(src[j], &dst[base + pre + j]);
+    const uint32_t ph = cf >> 31;
+    if (cf & kWalFinFull) {  // chased again by the stitch: full descriptors
+        const u32x4 *src = a.scratch + q * 2 * kWalSegSlots;
+        for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
+            if ((uint64_t)pre + j < cap)  // nt: written once (A/B: 997 -> 1,017 GiB/s)
+                __builtin_nontemporal_store(src[j], &dst[base + pre + j]);
+        return;
+    }
+    // packed entries: record j ends where record j + 1 starts (the chain's
+    // exit after the last), so its value length is that distance less 8 +
+    // its key length
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.scratch + (q * 2 + ph) * kWalSegSlots);
+    const uint64_t start = (uint64_t)a.wal_off[w] + (uint64_t)s * kWalSeg;
+    const uint32_t rel_exit = a.seg[q * 2 + ph].exit - s * kWalSeg;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+        if ((uint64_t)pre + j >= cap) continue;
+        const uint32_t e = src[j];
+        const uint32_t p = e & ((1u << kWalPosBits) - 1);
+        const uint32_t pn = j + 1 < cnt ? (src[j + 1] & ((1u << kWalPosBits) - 1)) : rel_exit;
+        uint32_t kl = e >> kWalPosBits;
+        if (kl == kWalKlEsc) {  // a key of 2^18 bytes or more: its length from the log
+            const uint8_t *kp = a.wal + start + p;
+            kl = (uint32_t)kp[0] | (uint32_t)kp[1] << 8 | (uint32_t)kp[2] << 16 | (uint32_t)kp[3] << 24;
+        }
+        const uint64_t ro = start + p;
+        __builtin_nontemporal_store(u32x4{(uint32_t)ro, (uint32_t)(ro >> 32), kl, pn - p - 8 - kl},
+                                    &dst[base + pre + j]);
+    }
 }
 
 }  // namespace

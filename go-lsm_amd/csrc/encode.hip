@@ -2810,15 +2810,40 @@ __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
         uint32_t kw[4];
         key_prefix(kp, kl, kw);
         uint32_t left = 0, right = n;
-        while (left < right) {
-            const uint32_t mid = left + (right - left) / 2;
-            const lsm_rec_desc d = a.idx_desc[base + mid];
-            const uint8_t *ep = a.img + d.rec_off + 4;
+        if (left < right) {
+            // Go's bisection, with both possible next midpoints' entries
+            // (descriptor, then key prefix) loaded before the current compare
+            // decides between them: one dependent load round per step instead
+            // of two (the midpoints are Go's own, so any index -- sorted or
+            // not -- lands where Seek lands)
+            uint32_t mid = left + (right - left) / 2;
+            lsm_rec_desc d = a.idx_desc[base + mid];
             uint32_t ew[4];
-            key_prefix(ep, d.key_len, ew);
-            const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
-            if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
-            else right = mid;
+            key_prefix(a.img + d.rec_off + 4, d.key_len, ew);
+            for (;;) {
+                const uint32_t mL = left + (mid - left) / 2, mR = mid + 1 + (right - mid - 1) / 2;
+                const bool hasL = left < mid, hasR = mid + 1 < right;
+                lsm_rec_desc dL{0, 0, 0}, dR{0, 0, 0};
+                uint32_t eL[4] = {0, 0, 0, 0}, eR[4] = {0, 0, 0, 0};
+                if (hasL) dL = a.idx_desc[base + mL];
+                if (hasR) dR = a.idx_desc[base + mR];
+                if (hasL) key_prefix(a.img + dL.rec_off + 4, dL.key_len, eL);
+                if (hasR) key_prefix(a.img + dR.rec_off + 4, dR.key_len, eR);
+                const uint8_t *ep = a.img + d.rec_off + 4;
+                const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
+                if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
+                else right = mid;
+                if (left >= right) break;
+                if (c < 0) {
+                    mid = mR;
+                    d = dR;
+                    for (int j = 0; j < 4; j++) ew[j] = eR[j];
+                } else {
+                    mid = mL;
+                    d = dL;
+                    for (int j = 0; j < 4; j++) ew[j] = eL[j];
+                }
+            }
         }
         bool hit = false;
         if (left < n) {

@@ -463,11 +463,15 @@ __global__ __launch_bounds__(kMergeThreads) void merge_flags_kernel(MergeIn m, c
 
 // eq[j] = 1 when sorted position j holds the same key as j - 1 (plain key
 // equality: for container/heap "" equals "", merge.go:21-23's Less is key <)
-__global__ __launch_bounds__(kMergeThreads) void merge_eq_kernel(MergeIn m, const uint32_t *perm,
-                                                                 uint8_t *eq) {
+// LSM_TIE_GOHEAP's dense key ranks, on the device: newg[j] = 1 where sorted
+// position j starts a new key (merge_scan_tiles / merge_scan_partials then
+// give each tile its first rank), and goheap_rank_apply writes each pair's
+// rank by input index -- the only array the host's heap replay reads.
+__global__ __launch_bounds__(kMergeThreads) void goheap_newgroup_kernel(MergeIn m, const uint32_t *perm,
+                                                                        uint32_t *newg) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
     if (j >= m.n) return;
-    eq[j] = j > 0 && keys_equal(m.bytes, view(m, perm[j]), view(m, perm[j - 1]));
+    newg[j] = j > 0 && !keys_equal(m.bytes, view(m, perm[j]), view(m, perm[j - 1]));
 }
 
 // candidate = the first pair of its group that may be written; the backward
@@ -584,6 +588,26 @@ __global__ __launch_bounds__(kPartThreads) void merge_scan_partials(SumPair *par
         }
     }
     if (threadIdx.x == 0) sc[n] = tot;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void goheap_rank_apply(const uint32_t *newg, uint32_t n,
+                                                                   const SumPair *part,
+                                                                   const uint32_t *perm,
+                                                                   uint32_t *rank) {
+    uint32_t f[kScanPer];
+    uint64_t s = 0;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    for (uint32_t t = 0; t < kScanPer; t++) {
+        f[t] = i0 + t < n ? newg[i0 + t] : 0u;
+        s += f[t];
+    }
+    SumPair tot;
+    const SumPair x = block_excl_scan2(s, 0, &tot);
+    uint64_t g = x.s + part[blockIdx.x].s;
+    for (uint32_t t = 0; t < kScanPer; t++) {
+        g += f[t];  // inclusive: the rank of position i0 + t
+        if (i0 + t < n) rank[perm[i0 + t]] = (uint32_t)g;
+    }
 }
 
 // The sums per position, and per candidate c (the walk's plateau space, see
@@ -1861,22 +1885,35 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
         // push / pop history replayed over the ranks on this thread, and
         // its pop order -- sorted by key, equal keys as the heap pops them
         // -- becomes the sorted order the steps below walk
-        hipLaunchKernelGGL(merge_eq_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m, perm,
-                           w.flags);
+        // ranks by input index on the device (newgroup flags, tile scan,
+        // scatter), read back into the context's pinned buffer; the order
+        // goes back from the same buffer
+        const uint32_t ntiles = (N + kScanTile - 1) / kScanTile;
+        uint32_t *rank_d = w.perm[cur ^ 1];
+        hipLaunchKernelGGL(goheap_newgroup_kernel, dim3(grid_for(n)), dim3(kMergeThreads), 0, s, m,
+                           perm, w.csize);
+        hipLaunchKernelGGL(merge_scan_tiles, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
+                           w.scan_part);
+        hipLaunchKernelGGL(merge_scan_partials, dim3(1), dim3(kPartThreads), 0, s, w.scan_part, ntiles,
+                           w.sc, N);
+        hipLaunchKernelGGL(goheap_rank_apply, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
+                           w.scan_part, perm, rank_d);
         LSM_HIP_CHECK(hipGetLastError());
-        std::vector<uint32_t> hperm(N), rank(N), order(N);
-        std::vector<uint8_t> eq(N);
-        LSM_HIP_CHECK(hipMemcpyAsync(hperm.data(), perm, 4ull * N, hipMemcpyDeviceToHost, s));
-        LSM_HIP_CHECK(hipMemcpyAsync(eq.data(), w.flags, N, hipMemcpyDeviceToHost, s));
-        LSM_HIP_CHECK(hipStreamSynchronize(s));
-        uint32_t g = 0;
-        for (uint32_t j = 0; j < N; j++) {
-            g += (j > 0 && !eq[j]) ? 1u : 0u;
-            rank[hperm[j]] = g;
+        const size_t need = 8ull * N;  // ranks, then the pop order
+        if (ctx->host_big_bytes < need) {
+            LSM_HIP_CHECK(hipStreamSynchronize(s));
+            if (ctx->host_big) LSM_HIP_CHECK(hipHostFree(ctx->host_big));
+            ctx->host_big = nullptr;
+            ctx->host_big_bytes = 0;
+            LSM_HIP_CHECK(hipHostMalloc(&ctx->host_big, need, hipHostMallocDefault));
+            ctx->host_big_bytes = need;
         }
-        goheap_pop_order(rank.data(), N, order.data());
-        LSM_HIP_CHECK(hipMemcpyAsync(w.perm[cur], order.data(), 4ull * N, hipMemcpyHostToDevice, s));
-        LSM_HIP_CHECK(hipStreamSynchronize(s));  // `order` is freed on return
+        uint32_t *hrank = static_cast<uint32_t *>(ctx->host_big), *horder = hrank + N;
+        LSM_HIP_CHECK(hipMemcpyAsync(hrank, rank_d, 4ull * N, hipMemcpyDeviceToHost, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));
+        goheap_pop_order(hrank, N, horder);
+        LSM_HIP_CHECK(hipMemcpyAsync(w.perm[cur], horder, 4ull * N, hipMemcpyHostToDevice, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));  // the pinned buffer is reused by the next call
     }
 
     // 3. groups and candidates; 4. sums and the file walk; 5. emit

@@ -290,10 +290,12 @@ int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_o
  * sort.Search (Go's exact bisection) for the first table whose MinKey > key
  * (bytes.Compare), index-- when > 0 (:186-192), then SSTable.MayContain
  * (sstable.go:300-305) of that one table: d_table[i] = the candidate (-1 when
- * the level is empty), d_may[i] = 1 when the table may hold the key.  A table
- * whose header did not decode searches as the zero Header (MinKey "") and,
- * like one whose filter did not decode, answers 0; filter deviations as
- * lsm_may_contain.  Level 0 (searchFromLevel0, :160-176, every table in
+ * the level is empty), d_may[i] = 1 when the table may hold the key.
+ * Deviation (corrupted tables only): a table whose header did not decode
+ * searches as the zero Header (MinKey "") and, like one whose filter did not
+ * decode, answers 0 -- go-lsm's Manager.Recover (manager.go:226-275) would
+ * have failed on such a file and never listed it in the level, so the
+ * reference has no answer to restate; filter deviations as lsm_may_contain.  Level 0 (searchFromLevel0, :160-176, every table in
  * order) is lsm_may_contain.  Workspace: lsm_level_may_contain_workspace_bytes. */
 size_t lsm_level_may_contain_workspace_bytes(uint32_t nfile, uint64_t nkeys);
 int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,

@@ -169,7 +169,9 @@ void ora_may_contain_batch(const uint8_t *img, const uint64_t *file_off, const o
  * Go's sort.Search for the first table whose MinKey > key, index-- when > 0,
  * then SSTable.MayContain of that table.  table[i - k0] = the candidate (-1 for
  * an empty level), may[i - k0] = its MayContain.  A table whose header did not
- * decode searches as the zero Header (MinKey "") and answers 0. */
+ * decode searches as the zero Header (MinKey "") and answers 0 -- the ABI's
+ * stated deviation: Manager.Recover (manager.go:226-275) would not have
+ * listed such a file in the level at all. */
 void ora_level_may_contain(const uint8_t *img, const uint64_t *file_off, const ora_sst_meta *meta,
                            uint32_t nfile, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
                            uint64_t k1, int32_t *table, uint8_t *may);

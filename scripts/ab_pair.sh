@@ -9,7 +9,7 @@ for rep in $(seq ${REPS:-2}); do
 for line in ${LINES:-decode4k}; do
   case $line in
     cfg4) args="--global-blocks 1000000" ;;
-    g*) args="--global-blocks ${line#g}000" ;;
+    g[0-9]*) args="--global-blocks ${line#g}000" ;;
     arena) args="--arena" ;;
     *) args="--config $line" ;;
   esac

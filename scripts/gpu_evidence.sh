@@ -26,7 +26,7 @@ declare -A DA DK
 DA[desc]="--config decode4k"; DK[desc]=decode4k:100000:desc
 DA[arena]="--config decode4k --arena"; DK[arena]=decode4k:100000:arena
 DA[d64]="--config decode64k"; DK[d64]=decode64k:6400:desc
-for t in ${PMC1:-desc arena d64}; do
+for t in ${PMC1-desc arena d64}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_${t}_$c 180 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${TAG}_${t}_$c -o run \
       -- python bench.py ${DA[$t]} --steps 5 --warmup 2 --no-cpu-baseline --no-cold > $OUT/pmc_${TAG}_${t}_$c.log 2>&1 || exit 1
@@ -42,7 +42,8 @@ K[sstdec]=sst_index_kernel,sst_tail_kernel; A[sstdec]=sst_tail_kernel; W[sstdec]
 K[probe]=mc_prep_kernel,mc_classify_kernel,mc_scatter_kernel,mc_test_kernel,may_contain_kernel; A[probe]=mc_prep_kernel; W[probe]=probe:208:1048576
 K[wal]=wal_seg_lanes_kernel,wal_stitch_kernel,wal_compact_kernel; A[wal]=wal_stitch_kernel; W[wal]=wal:64:desc
 K[level]=lv_classify_kernel,lv_test_kernel; A[level]=lv_classify_kernel; W[level]=level:208:1048576
-for cfg in ${PMCM:-sst sstdec probe wal}; do
+K[get]=lv_classify_kernel,lv_test_kernel,level_get_kernel; A[get]=lv_classify_kernel; W[get]=get:208:1048576
+for cfg in ${PMCM-sst sstdec probe wal}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     step pmcm_${cfg}_$c 180 rocprofv3 --pmc $c --output-format csv -d $OUT/pmcm_${TAG}_${cfg}_$c -o run \
       -- python bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-cold > $OUT/pmcm_${TAG}_${cfg}_$c.log 2>&1 || exit 1
