@@ -53,18 +53,19 @@ for cfg in ${PMCM-sst sstdec probe wal}; do
 done
 fi
 if [ "$PHASE" = all ] || [ "$PHASE" = 3 ]; then
-for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal probe level compact e2e}; do
+for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal probe level get compact goheap e2e}; do
   case $line in
     cfg4) args="--global-blocks 1000000 --no-cpu-baseline" ;;
     arena) args="--arena" ;;
     e2e) args="--e2e" ;;
+    goheap) args="--config compact --tie goheap --steps 5 --warmup 1" ;;
     *) args="--config $line" ;;
   esac
   step bench_$line 600 python bench.py $args > $OUT/bench_${TAG}_$line.json 2> $OUT/bench_${TAG}_$line.err \
     || { tail -20 $OUT/bench_${TAG}_$line.err; exit 1; }
   cut -c1-200 $OUT/bench_${TAG}_$line.json
 done
-for p in ${PROF:-decode4k arena decode64k mixed sst sstdec probe level wal compact}; do
+for p in ${PROF:-decode4k arena decode64k mixed sst sstdec probe level get wal compact}; do
   case $p in arena) args="--arena" ;; *) args="--config $p" ;; esac
   step prof_$p 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_$p -o run \
     -- python bench.py $args --steps 20 --warmup 3 --no-cpu-baseline --no-cold > $OUT/prof_${TAG}_$p.log 2>&1 || exit 1
