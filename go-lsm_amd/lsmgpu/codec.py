@@ -877,6 +877,22 @@ def sst_pairs(ctx: Context, r: "SstDecode", stream=None) -> tuple:
     return kd[:n], vd[:n], prefix
 
 
+def compact_merge_into(ctx: Context, d_img: torch.Tensor, r: "SstDecode", key_out: torch.Tensor,
+                       val_out: torch.Tensor, prefix: torch.Tensor, mg: Merge, d_counts: torch.Tensor,
+                       level: int = 1, threshold: int = MAX_SSTABLE_SIZE, tie: int = TIE_INPUT,
+                       stream=None) -> Merge:
+    """lsm_compact_merge_async: sst_pairs_into + merge_kvs_into(d_counts=...)
+    in one call (the join, then CompactAndMergeKVs, on one stream).  mg.n
+    must be the join's pair count; the counts stay on the device in
+    d_counts (int64[3])."""
+    _lib.check(ctx.lib.lsm_compact_merge_async(
+        ctx.handle, _ptr(d_img), _ptr(r.meta), _ptr(r.d_file_off), r.nfile, _ptr(r.idx_desc),
+        _ptr(r.data_desc), mg.n, _ptr(key_out), _ptr(val_out), _ptr(prefix), level, threshold, tie,
+        _ptr(mg.out), _ptr(mg.file_start), _ptr(d_counts), _ptr(mg.workspace), mg.workspace.numel(),
+        _stream_handle(stream)), "lsm_compact_merge_async")
+    return mg
+
+
 def build_sst_views_into(ctx: Context, batch: RecordBatch, sb: "SstBuild", d_bytes: torch.Tensor,
                          key_desc: torch.Tensor, val_desc: Optional[torch.Tensor],
                          idx: torch.Tensor, stream=None) -> None:

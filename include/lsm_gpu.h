@@ -40,7 +40,8 @@ extern "C" {
  * v5: lsm_merge_kvs_async and lsm_gather_kvs_dev (the merge's counts stay on
  * the device; the gather reads its pair count there); the level sparse index
  * (lsm_level_index_build, lsm_level_may_contain_indexed).
- * v6: lsm_level_get (the batched Get past MayContain: Seek + the value). */
+ * v6: lsm_level_get (the batched Get past MayContain: Seek + the value);
+ * lsm_compact_merge_async (the join and the merge as one call). */
 #define LSM_ABI_VERSION 6
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
@@ -510,6 +511,22 @@ int lsm_gather_kvs_dev(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc 
                        const lsm_rec_desc *d_val_desc, const uint32_t *d_idx, const uint64_t *d_nout,
                        uint64_t nout_max, uint8_t *d_keys, uint64_t *d_koff, uint8_t *d_vals,
                        uint64_t *d_voff, void *d_ws, size_t ws_bytes, void *stream);
+
+/* lsm_sst_pairs + lsm_merge_kvs_async in one call (ABI 6): the join of the
+ * decoded files and CompactAndMergeKVs over it, queued in that order on
+ * `stream` (compaction.go:173-193 then :49-95).  n = the join's pair count
+ * (d_prefix[nfile], e.g. the sum of the decoded nidx of the files that
+ * decoded), known to the caller; outputs, workspace
+ * (lsm_merge_kvs_workspace_bytes(n)) and d_counts exactly as the two calls.
+ * Waits on the host for the merge's key statistics, as lsm_merge_kvs_async
+ * does.  (Statistics taken before the join, to overlap their read-back with
+ * it, measured slower and are not used: DESIGN.md section 7.) */
+int lsm_compact_merge_async(lsm_ctx *ctx, const uint8_t *d_img, const lsm_sst_meta *d_meta,
+                            const uint64_t *d_file_off, uint32_t nfile, const lsm_rec_desc *d_idx_desc,
+                            const lsm_rec_desc *d_data_desc, uint64_t n, lsm_rec_desc *d_key_out,
+                            lsm_rec_desc *d_val_out, uint64_t *d_prefix, int level, uint64_t threshold,
+                            int tie, uint32_t *d_out, uint64_t *d_file_start, uint64_t *d_counts,
+                            void *d_ws, size_t ws_bytes, void *stream);
 
 /* The positional join of decoded files in file order -- loadLevelData's
  * allPairs (compaction.go:173-193) over GetKeyValuePairs (sstable.go:248-268):

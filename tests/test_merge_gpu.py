@@ -497,3 +497,88 @@ def test_device_count_above_bound_is_capped(ctx):
     kbytes, vbytes = int(a.koff[bound]), int(a.voff[bound])
     assert torch.equal(a.keys[:kbytes], b.keys[:kbytes]) and torch.equal(a.vals[:vbytes], b.vals[:vbytes])
     assert bool((b.keys[kbytes:] == 0xEE).all()) and bool((b.vals[vbytes:] == 0xEE).all())
+
+
+def _decode_level(ctx, images, rng):
+    offs, pos, parts = [], 0, []
+    for im in images:
+        gap = 16 * int(rng.integers(0, 3))
+        parts += [np.zeros(gap, np.uint8), im]
+        pos += gap
+        offs.append(pos)
+        pos += im.size
+        pad = (-pos) % 16
+        parts.append(np.zeros(pad, np.uint8))
+        pos += pad
+    buf = np.concatenate(parts)
+    d_img = lsmgpu.to_device_bytes(buf, ctx.torch_device)
+    r = lsmgpu.decode_sst(ctx, d_img, np.array(offs, np.uint64), np.array([im.size for im in images], np.uint64))
+    return d_img, r
+
+
+def _compare_compact_merge(ctx, d_img, r, level, threshold, tie):
+    """lsm_compact_merge_async against lsm_sst_pairs + lsm_merge_kvs_async."""
+    kd, vd, prefix = lsmgpu.sst_pairs(ctx, r)
+    n = int(kd.shape[0])
+    want = lsmgpu.alloc_merge(ctx, n)
+    dc_w = torch.full((3,), -1, dtype=torch.int64, device=ctx.torch_device)
+    lsmgpu.merge_kvs_into(ctx, d_img, kd, vd, want, level=level, threshold=threshold, tie=tie, d_counts=dc_w)
+    cap = int(r.idx_desc.shape[0])
+    kd2 = torch.full((cap, 4), -3, dtype=torch.int32, device=ctx.torch_device)
+    vd2 = torch.full((cap, 4), -3, dtype=torch.int32, device=ctx.torch_device)
+    pre2 = torch.full((r.nfile + 1,), -3, dtype=torch.int64, device=ctx.torch_device)
+    got = lsmgpu.alloc_merge(ctx, n)
+    dc_g = torch.full((3,), -1, dtype=torch.int64, device=ctx.torch_device)
+    lsmgpu.compact_merge_into(ctx, d_img, r, kd2, vd2, pre2, got, dc_g, level=level, threshold=threshold, tie=tie)
+    torch.cuda.synchronize()
+    assert torch.equal(pre2, prefix)
+    assert torch.equal(kd2[:n], kd) and torch.equal(vd2[:n], vd)
+    c = dc_w.cpu().tolist()
+    assert dc_g.cpu().tolist() == c
+    assert torch.equal(got.out[:c[0]], want.out[:c[0]])
+    assert torch.equal(got.file_start[:c[1] + 1], want.file_start[:c[1] + 1])
+    return c
+
+
+@pytest.mark.parametrize("tie", TIES)
+def test_compact_merge_matches_two_calls_small(ctx, tie):
+    """Images of random sorted runs (tombstones, duplicates across files,
+    an empty file and one whose header does not decode -- both contribute no
+    pairs, so the statistics' file lookup must step over them) through the
+    one-call join + merge and through the two calls: identical join, pairs,
+    file starts and counts."""
+    rng = np.random.default_rng(808 + tie)
+    images = []
+    for f in range(9):
+        keys = sorted({b"m%05d" % int(x) for x in rng.integers(0, 3000, int(rng.integers(50, 400)))})
+        vals = [TOMB if rng.random() < 0.1 else b"v%d" % f * int(rng.integers(1, 5)) for _ in keys]
+        kb = np.frombuffer(b"".join(keys), np.uint8)
+        ko = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+        vb = np.frombuffer(b"".join(vals), np.uint8)
+        vo = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.uint64)
+        img, _ = ora.build_sst(kb, ko, vb, vo, 0, len(keys))
+        images.append(img.copy())
+    empty, _ = ora.build_sst(np.zeros(1, np.uint8), np.zeros(1, np.uint64), np.zeros(1, np.uint8),
+                             np.zeros(1, np.uint64), 0, 0)
+    broken = images[4].copy()
+    broken[0:4] = 255  # header key length past the file: stage 1
+    images = images[:2] + [empty] + images[2:4] + [broken] + images[4:]
+    d_img, r = _decode_level(ctx, images, rng)
+    for level, thr in ((1, MiB2), (6, 3000), (1, 700)):
+        _compare_compact_merge(ctx, d_img, r, level, thr, tie)
+
+
+def test_compact_merge_matches_two_calls_full_size(ctx):
+    """The compact bench's input (216 images, 3.43M pairs), both tie modes."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench_compact import build_images, level0_runs
+    from lsmgpu import synth
+    n1 = 100_000 * 33
+    img, file_off, file_size = build_images(ctx, level0_runs(n1, 0, 0) + [synth.kv_stream(n1)])
+    r = lsmgpu.alloc_sst_decode(ctx, file_off, file_size, int(img.numel()))
+    lsmgpu.decode_sst_into(ctx, img, r)
+    for tie in TIES:
+        c = _compare_compact_merge(ctx, img, r, 1, MiB2, tie)
+        assert c[1] >= 200
