@@ -69,6 +69,9 @@ def parse(argv=None):
                     help="host-resident blocks: pinned H2D -> decode -> compact -> D2H "
                          "(the PCIe-inclusive rate recorded in DESIGN.md; not the headline)")
     ap.add_argument("--chunk", type=int, default=8192, help="blocks per e2e pipeline chunk")
+    ap.add_argument("--get-tree", default="on", choices=["on", "off"],
+                    help="--config get: the Seek's top levels through the fence tree "
+                         "(lsm_level_get's workspace), or every level in the index")
     ap.add_argument("--tie", default="input", choices=["input", "goheap"],
                     help="--config compact: equal keys in input order (LSM_TIE_INPUT) or in "
                          "container/heap's pop order, the reference's exact output (LSM_TIE_GOHEAP)")

@@ -288,12 +288,16 @@ def bench_level_search(args, world, rank, local):
     get = args.config == "get"
     result = torch.empty(nprobe, dtype=torch.int32, device=dev)
     value = torch.empty((nprobe, 4), dtype=torch.int32, device=dev)
+    # the fence tree (the bisection's top levels as 16-byte prefixes), rebuilt
+    # by every call; --get-tree off walks every level in the index (A/B)
+    gws = lsmgpu.level_get_workspace(ctx, nf) if getattr(args, "get_tree", "on") == "on" else None
 
     def step():
         lsmgpu.level_may_contain_into(ctx, sb.out, r, probes, table, may, ws=ws, stream=stream,
                                       index=index)
         if get:
-            lsmgpu.level_get_into(ctx, sb.out, r, probes, table, may, result, value, stream=stream)
+            lsmgpu.level_get_into(ctx, sb.out, r, probes, table, may, result, value,
+                                  workspace=gws, stream=stream)
 
     for _ in range(args.warmup):
         step()

@@ -2786,7 +2786,20 @@ struct GetArgs {
     const uint8_t *may;
     int32_t *result;
     lsm_rec_desc *value;
+    const u32x4 *tree;  // the fence tree (nfile * kGetTreeNodes), or null
 };
+
+// The fence tree: the first kGetTreeLevels levels of Go's bisection over a
+// table's n index entries do not depend on the keys (the midpoint of [l, r)
+// is l + (r - l)/2 whatever they hold), so node x of table f (breadth-first,
+// the path to it = the bits of x + 1 below the leading one, 1 = the right
+// half) holds the 16-byte big-endian prefix of the key at that interval's
+// midpoint.  A probe walks those levels through 16-byte tree nodes (3.4 MB
+// for 208 tables: L2-resident) instead of an index descriptor plus a key
+// line per level, and takes exactly Go's steps, so any index -- sorted or
+// not -- lands where Seek lands; a prefix tie reads the entry's own bytes.
+constexpr uint32_t kGetTreeLevels = 10;
+constexpr uint32_t kGetTreeNodes = (1u << kGetTreeLevels) - 1;
 
 // key bytes [p, p + len) as four big-endian words, zero padded past len
 // (reads 16 bytes at p: the input slack covers a key that ends a buffer)
@@ -2798,6 +2811,29 @@ __device__ __forceinline__ void key_prefix(const uint8_t *p, uint64_t len, uint3
     kw[1] = __builtin_bswap32((uint32_t)(f0 >> 32));
     kw[2] = __builtin_bswap32((uint32_t)f1);
     kw[3] = __builtin_bswap32((uint32_t)(f1 >> 32));
+}
+
+__global__ __launch_bounds__(256) void get_tree_kernel(GetArgs a, u32x4 *tree) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t f = g / kGetTreeNodes;
+    if (f >= a.nfile) return;
+    const uint32_t x = (uint32_t)(g - f * kGetTreeNodes);
+    const uint32_t depth = 31 - __builtin_clz(x + 1), n = a.meta[f].nidx;
+    uint32_t l = 0, r = n;
+    for (uint32_t b = depth; b-- > 0 && l < r;) {
+        const uint32_t mid = l + (r - l) / 2;
+        if (((x + 1) >> b) & 1) l = mid + 1;
+        else r = mid;
+    }
+    uint32_t kw[4] = {0, 0, 0, 0};  // an empty interval is never walked
+    if (l < r) {
+        const uint64_t base = a.rec_base ? a.rec_base[f] : a.file_off[f] / 4;
+        const lsm_rec_desc d = a.idx_desc[base + l + (r - l) / 2];
+        key_prefix(a.img + d.rec_off + 4, d.key_len, kw);
+    }
+    u32x4 o;
+    o.x = kw[0]; o.y = kw[1]; o.z = kw[2]; o.w = kw[3];
+    tree[g] = o;
 }
 
 __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
@@ -2816,9 +2852,31 @@ __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
         uint32_t kw[4];
         key_prefix(kp, kl, kw);
         uint32_t left = 0, right = n;
-        // Go's bisection (a variant loading both possible next midpoints'
-        // entries before each compare measured slower: 0.549 vs 0.375 ms per
-        // 1M-key Get, 3.0 GB of HBM traffic per call -- round 5, A/B)
+        // Go's bisection: the top levels through the fence tree, the rest over
+        // the index (a variant loading both possible next midpoints' entries
+        // before each compare measured slower: 0.549 vs 0.375 ms per 1M-key
+        // Get, 3.0 GB of HBM traffic per call -- round 5, A/B)
+        if (a.tree) {
+            const u32x4 *tr = a.tree + (uint64_t)t * kGetTreeNodes;
+            uint32_t x = 0;
+            for (uint32_t d = 0; d < kGetTreeLevels && left < right; d++) {
+                const uint32_t mid = left + (right - left) / 2;
+                const u32x4 e = tr[x];
+                const uint32_t ew[4] = {e.x, e.y, e.z, e.w};
+                int c = prefix_cmp(ew, kw);
+                if (c == 0) {  // a prefix tie: the entry's own bytes decide
+                    const lsm_rec_desc dd = a.idx_desc[base + mid];
+                    c = bound_cmp(ew, dd.key_len, a.img + dd.rec_off + 4, kw, kl, kp);
+                }
+                if (c < 0) {
+                    left = mid + 1;
+                    x = 2 * x + 2;
+                } else {
+                    right = mid;
+                    x = 2 * x + 1;
+                }
+            }
+        }
         while (left < right) {
             const uint32_t mid = left + (right - left) / 2;
             const lsm_rec_desc d = a.idx_desc[base + mid];
@@ -3333,7 +3391,8 @@ extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t 
                              const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
                              const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
                              uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may,
-                             int32_t *d_result, lsm_rec_desc *d_value, void *stream) {
+                             int32_t *d_result, lsm_rec_desc *d_value, void *d_workspace,
+                             size_t ws_bytes, void *stream) {
     if (!ctx) return LSM_EINVAL;
     if (nkeys == 0) return 0;
     if (!d_keys || !d_koff || !d_table || !d_may || !d_result || !d_value) return LSM_EINVAL;
@@ -3355,12 +3414,24 @@ extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t 
     a.may = d_may;
     a.result = d_result;
     a.value = d_value;
+    a.tree = nullptr;
+    hipStream_t s = static_cast<hipStream_t>(stream);
     const uint64_t grid = (nkeys + 255) / 256;
     if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
-    hipLaunchKernelGGL(level_get_kernel, dim3((uint32_t)grid), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), a);
+    if (d_workspace && nfile) {
+        if (ws_bytes < lsm_level_get_workspace_bytes(nfile)) return LSM_ESPACE;
+        u32x4 *tree = static_cast<u32x4 *>(d_workspace);
+        const uint64_t tg = ((uint64_t)nfile * kGetTreeNodes + 255) / 256;
+        hipLaunchKernelGGL(get_tree_kernel, dim3((uint32_t)tg), dim3(256), 0, s, a, tree);
+        a.tree = tree;
+    }
+    hipLaunchKernelGGL(level_get_kernel, dim3((uint32_t)grid), dim3(256), 0, s, a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+extern "C" size_t lsm_level_get_workspace_bytes(uint32_t nfile) {
+    return (size_t)nfile * kGetTreeNodes * sizeof(u32x4);
 }
 
 extern "C" int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,

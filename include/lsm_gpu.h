@@ -331,7 +331,12 @@ int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img, const void
  * d_value[i] is a view of the value {rec_off = offset in d_img of its u32
  * length prefix, key_len = 0, val_len}; otherwise d_value[i] is zero.  The
  * Seek runs over the nidx entries the decode kept (a table whose index did
- * not decode is one the Manager would not have loaded, manager.go:226-275). */
+ * not decode is one the Manager would not have loaded, manager.go:226-275).
+ * d_workspace (lsm_level_get_workspace_bytes(nfile) bytes, or NULL) holds the
+ * fence tree: the first levels of every table's bisection (which do not depend
+ * on the keys) as 16-byte key prefixes, built by the call; the probes walk
+ * them there and only the last levels in the index.  The steps are Go's either
+ * way, so the answers are the same with and without it. */
 enum lsm_get_result {
     LSM_GET_ABSENT = 0,         /* (nil, nil): not MayContain, or no entry equals the key        */
     LSM_GET_FOUND = 1,          /* the value, d_value[i]                                          */
@@ -345,7 +350,8 @@ int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off
                   const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
                   const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
                   uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may, int32_t *d_result,
-                  lsm_rec_desc *d_value, void *stream);
+                  lsm_rec_desc *d_value, void *d_workspace, size_t ws_bytes, void *stream);
+size_t lsm_level_get_workspace_bytes(uint32_t nfile);
 
 /* ---- encode ---------------------------------------------------------------- */
 

@@ -53,7 +53,10 @@ def run(ctx, rng, images, probes):
     r = lsmgpu.decode_sst(ctx, d_img, offs, lens)
     table, may = lsmgpu.level_may_contain(ctx, d_img, r, batch)
     res, val = lsmgpu.level_get(ctx, d_img, r, batch, table, may)
+    # without the fence tree: every level of the bisection in the index
+    res0, val0 = lsmgpu.level_get(ctx, d_img, r, batch, table, may, tree=False)
     torch.cuda.synchronize()
+    assert torch.equal(res, res0) and torch.equal(val, val0)
     table, may = table.cpu().numpy(), may.cpu().numpy()
     res = res.cpu().numpy()
     val = val.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
@@ -163,3 +166,21 @@ def test_get_full_level_sample(ctx):
     probes = [synth.keys_for(np.array([i]))[0].tobytes() for i in ids]
     res, _ = run(ctx, rng, images, probes)
     assert (res == ora.GET_FOUND).sum() == int((ids < n).sum())
+
+
+def test_get_deep_unsorted_index(ctx):
+    """Tables deeper than the fence tree (n > 1,023: the walk continues in the
+    index) whose index entries are NOT sorted: Seek's answer is then whatever
+    Go's bisection path reaches, and the tree must take exactly those steps.
+    One sorted table of the same depth beside it, and keys sharing 18 bytes
+    (prefix ties inside the tree)."""
+    rng = np.random.default_rng(205)
+    lp = b"shared-prefix-xyz-"
+    sk = sorted({lp + b"%07d" % int(x) for x in rng.integers(0, 10 ** 7, 3000)})
+    im_sorted = build(sk, [b"s%d" % i for i in range(len(sk))], m=1 << 16, k=5)
+    uk = [b"u%06d" % int(x) for x in rng.permutation(5000)[:2600]]  # shuffled
+    im_unsorted = build(uk, [b"u%d" % i for i in range(len(uk))], m=1 << 16, k=5)
+    probes = sk[::2] + [lp + b"%07d" % int(x) for x in rng.integers(0, 10 ** 7, 2000)]
+    probes += uk + [b"u%06d" % int(x) for x in rng.integers(0, 5000, 2000)] + [lp, lp[:16]]
+    res, _ = run(ctx, rng, [im_sorted, im_unsorted], probes)
+    assert (res[:len(sk[::2])] == ora.GET_FOUND).all()
