@@ -70,8 +70,9 @@ def parse(argv=None):
                          "(the PCIe-inclusive rate recorded in DESIGN.md; not the headline)")
     ap.add_argument("--chunk", type=int, default=8192, help="blocks per e2e pipeline chunk")
     ap.add_argument("--get-tree", default="on", choices=["on", "off"],
-                    help="--config get: the Seek's top levels through the fence tree "
-                         "(lsm_level_get's workspace), or every level in the index")
+                    help="--config get: Seek through the level's Seek tree "
+                         "(lsm_level_get_tree_build, built once with the level), or by "
+                         "bisecting the decoded index itself")
     ap.add_argument("--tie", default="input", choices=["input", "goheap"],
                     help="--config compact: equal keys in input order (LSM_TIE_INPUT) or in "
                          "container/heap's pop order, the reference's exact output (LSM_TIE_GOHEAP)")

@@ -204,6 +204,11 @@ def bench_may_contain(args, world, rank, local):
                    "false_positive_rate_absent": float(rows[~is_held].astype(bool).mean()),
                    "parallelism": f"dp{world} (probe batches per rank, no collective)",
                    "scaling_note": "weak, per-rank copy: every rank probes its own level copy"},
+        **({"seek_tree": ({"bytes": int(gtree.data.numel()), "max_nidx": gtree.max_nidx,
+                          "build_ms_once": round(tree_build_ms, 3),
+                          "note": "built with the level (lsm_level_get_tree_build), outside the step, "
+                                  "like the sparse index"} if gtree is not None else
+                         "off: Seek bisects the decoded index")} if get else {}),
         # algorithmic bytes per launch: the hit matrix written once, the probe
         # keys and offsets read once, every file's stored filter words read once
         "roofline": {"bound": "hbm", "kernel": "lsm_may_contain (all launches)",
@@ -288,16 +293,22 @@ def bench_level_search(args, world, rank, local):
     get = args.config == "get"
     result = torch.empty(nprobe, dtype=torch.int32, device=dev)
     value = torch.empty((nprobe, 4), dtype=torch.int32, device=dev)
-    # the fence tree (the bisection's top levels as 16-byte prefixes), rebuilt
-    # by every call; --get-tree off walks every level in the index (A/B)
-    gws = lsmgpu.level_get_workspace(ctx, nf) if getattr(args, "get_tree", "on") == "on" else None
+    # the level's Seek tree (Go's bisection laid down as 16-byte key prefixes
+    # in 128-byte blocks of three levels), built with the level like the
+    # sparse index; --get-tree off walks the index itself (A/B)
+    gtree = None
+    if get and getattr(args, "get_tree", "on") == "on":
+        t0 = time.perf_counter()
+        gtree = lsmgpu.level_get_tree(ctx, sb.out, r, stream=stream)
+        torch.cuda.synchronize()
+        tree_build_ms = (time.perf_counter() - t0) * 1e3
 
     def step():
         lsmgpu.level_may_contain_into(ctx, sb.out, r, probes, table, may, ws=ws, stream=stream,
                                       index=index)
         if get:
             lsmgpu.level_get_into(ctx, sb.out, r, probes, table, may, result, value,
-                                  workspace=gws, stream=stream)
+                                  tree=gtree, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -357,9 +368,15 @@ def bench_level_search(args, world, rank, local):
                    "files_per_gpu": nf, "probes_per_gpu": nprobe,
                    "parallelism": f"dp{world} (probe batches per rank, no collective)",
                    "scaling_note": "weak, per-rank copy: every rank probes its own level copy"},
+        **({"seek_tree": ({"bytes": int(gtree.data.numel()), "max_nidx": gtree.max_nidx,
+                          "build_ms_once": round(tree_build_ms, 3),
+                          "note": "built with the level (lsm_level_get_tree_build), outside the step, "
+                                  "like the sparse index"} if gtree is not None else
+                         "off: Seek bisects the decoded index")} if get else {}),
         "roofline": {"bound": "hbm", "kernel": "lsm_level_may_contain_indexed (all launches; the level's "
                                "sparse index built once, outside the step)" +
-                               (" + lsm_level_get" if get else ""),
+                               (" + lsm_level_get (Seek tree built once, outside the step)"
+                                if gtree is not None else " + lsm_level_get" if get else ""),
                      "kernel_ms": round(kern_ms, 5),
                      "kernel_ms_median": round(float(np.median(times)), 5),
                      "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1),

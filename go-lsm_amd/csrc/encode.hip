@@ -2786,20 +2786,41 @@ struct GetArgs {
     const uint8_t *may;
     int32_t *result;
     lsm_rec_desc *value;
-    const u32x4 *tree;  // the fence tree (nfile * kGetTreeNodes), or null
+    const uint8_t *tree;  // the Seek tree (lsm_level_get_tree_build), or null
+    uint32_t tree_nidx;   // the tree's max_nidx: larger tables walk the index
+    uint32_t tree_top;    // levels in the tree's top block (1-3)
+    uint64_t tree_stride; // bytes per table
 };
 
-// The fence tree: the first kGetTreeLevels levels of Go's bisection over a
-// table's n index entries do not depend on the keys (the midpoint of [l, r)
-// is l + (r - l)/2 whatever they hold), so node x of table f (breadth-first,
-// the path to it = the bits of x + 1 below the leading one, 1 = the right
-// half) holds the 16-byte big-endian prefix of the key at that interval's
-// midpoint.  A probe walks those levels through 16-byte tree nodes (3.4 MB
-// for 208 tables: L2-resident) instead of an index descriptor plus a key
-// line per level, and takes exactly Go's steps, so any index -- sorted or
-// not -- lands where Seek lands; a prefix tie reads the entry's own bytes.
-constexpr uint32_t kGetTreeLevels = 10;
-constexpr uint32_t kGetTreeNodes = (1u << kGetTreeLevels) - 1;
+// The Seek tree.  Go's bisection over a table's n index entries visits a
+// fixed binary tree of midpoints (the midpoint of [l, r) is l + (r - l)/2
+// whatever the keys hold), so it is laid down once per level -- as the
+// decoded IndexBlocks are, when the level is loaded -- in 128-byte blocks of
+// three tree levels: seven nodes of the key's 16-byte big-endian prefix
+// (bytes 0-111) and its length capped at 0xFFFF (u16 at 112 + 2j).  A probe
+// then reads one 128-byte line per three steps instead of an index
+// descriptor and a key line per step, and takes exactly Go's steps, so any
+// index -- sorted or not -- lands where Seek lands.  Blocks: with D =
+// bitlen(max_nidx) levels, the top block holds the first t = D - 3(G - 1)
+// levels (G = ceil(D / 3) groups); group g >= 1 holds 2^t 8^(g-1) blocks,
+// block i's child c (the three steps taken in it, first step in the high
+// bit) being block 8i + c of the next group (the top block's children: its
+// exit c < 2^t).  Node j of a block (0-6, breadth-first) lies on the path
+// (block path, bits of j + 1 below the leading one; 1 = the right half).
+struct TreeShape {
+    uint32_t D, G, t;
+    uint64_t blocks;
+};
+
+__host__ __device__ inline TreeShape tree_shape(uint32_t max_nidx) {
+    TreeShape T{0, 0, 0, 0};
+    while (T.D < 32 && (max_nidx >> T.D)) T.D++;
+    if (T.D == 0) return T;
+    T.G = (T.D + 2) / 3;
+    T.t = T.D - 3 * (T.G - 1);
+    T.blocks = 1 + ((1ull << T.t) * (((1ull << (3 * (T.G - 1))) - 1) / 7));
+    return T;
+}
 
 // key bytes [p, p + len) as four big-endian words, zero padded past len
 // (reads 16 bytes at p: the input slack covers a key that ends a buffer)
@@ -2813,27 +2834,68 @@ __device__ __forceinline__ void key_prefix(const uint8_t *p, uint64_t len, uint3
     kw[3] = __builtin_bswap32((uint32_t)(f1 >> 32));
 }
 
-__global__ __launch_bounds__(256) void get_tree_kernel(GetArgs a, u32x4 *tree) {
-    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t f = g / kGetTreeNodes;
+// One thread per (table, block, node slot 0-7; slot 7 idle).
+__global__ __launch_bounds__(256) void get_tree_build_kernel(GetArgs a, uint8_t *tree, TreeShape T) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t f = gid / (8 * T.blocks);
     if (f >= a.nfile) return;
-    const uint32_t x = (uint32_t)(g - f * kGetTreeNodes);
-    const uint32_t depth = 31 - __builtin_clz(x + 1), n = a.meta[f].nidx;
+    const uint64_t b = (gid - f * 8 * T.blocks) >> 3;
+    const uint32_t j = (uint32_t)(gid & 7);
+    const uint32_t n = a.meta[f].nidx;
+    if (j == 7 || n > a.tree_nidx) return;
+    // the block's group g and index i in it, its root's depth and path
+    uint64_t off = 1, cnt = 1ull << T.t, i = 0;
+    uint32_t depth = 0;
+    if (b > 0) {
+        depth = T.t;
+        while (b >= off + cnt) {
+            off += cnt;
+            cnt *= 8;
+            depth += 3;
+        }
+        i = b - off;
+    }
+    const uint32_t levels = b == 0 ? T.t : 3;
+    const uint32_t ld = 31 - __builtin_clz(j + 1);
+    if (ld >= levels) return;
+    const uint64_t path = (i << ld) | (uint64_t)(j + 1 - (1u << ld));
+    depth += ld;
     uint32_t l = 0, r = n;
-    for (uint32_t b = depth; b-- > 0 && l < r;) {
+    for (uint32_t s = depth; s-- > 0 && l < r;) {
         const uint32_t mid = l + (r - l) / 2;
-        if (((x + 1) >> b) & 1) l = mid + 1;
+        if ((path >> s) & 1) l = mid + 1;
         else r = mid;
     }
-    uint32_t kw[4] = {0, 0, 0, 0};  // an empty interval is never walked
+    uint32_t kw[4] = {0, 0, 0, 0}, len = 0;  // an empty interval is never walked
     if (l < r) {
         const uint64_t base = a.rec_base ? a.rec_base[f] : a.file_off[f] / 4;
         const lsm_rec_desc d = a.idx_desc[base + l + (r - l) / 2];
         key_prefix(a.img + d.rec_off + 4, d.key_len, kw);
+        len = d.key_len < 0xFFFFu ? d.key_len : 0xFFFFu;
     }
+    uint8_t *blk = tree + f * a.tree_stride + b * 128;
     u32x4 o;
     o.x = kw[0]; o.y = kw[1]; o.z = kw[2]; o.w = kw[3];
-    tree[g] = o;
+    *reinterpret_cast<u32x4 *>(blk + 16 * j) = o;
+    *reinterpret_cast<uint16_t *>(blk + 112 + 2 * j) = (uint16_t)len;
+}
+
+// Go's comparison of index entry (prefix ew, length el -- exact up to 16,
+// capped past it -- at mid) against the probe: the prefix, then the lengths
+// when either key fits in 16 bytes (the bytes both hold are then all in the
+// prefixes), the bytes past 16 otherwise.
+__device__ __forceinline__ int tree_cmp(const GetArgs &a, uint64_t base, uint32_t mid, const uint32_t ew[4],
+                                        uint32_t el, const uint32_t kw[4], uint64_t kl, const uint8_t *kp) {
+    int c = prefix_cmp(ew, kw);
+    if (c == 0) {
+        if (el <= 16 || kl <= 16) {
+            c = (uint64_t)el < kl ? -1 : (uint64_t)el > kl ? 1 : 0;
+        } else {
+            const lsm_rec_desc d = a.idx_desc[base + mid];
+            c = bound_cmp(ew, d.key_len, a.img + d.rec_off + 4, kw, kl, kp);
+        }
+    }
+    return c;
 }
 
 __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
@@ -2852,46 +2914,70 @@ __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
         uint32_t kw[4];
         key_prefix(kp, kl, kw);
         uint32_t left = 0, right = n;
-        // Go's bisection: the top levels through the fence tree, the rest over
-        // the index (a variant loading both possible next midpoints' entries
-        // before each compare measured slower: 0.549 vs 0.375 ms per 1M-key
-        // Get, 3.0 GB of HBM traffic per call -- round 5, A/B)
-        if (a.tree) {
-            const u32x4 *tr = a.tree + (uint64_t)t * kGetTreeNodes;
-            uint32_t x = 0;
-            for (uint32_t d = 0; d < kGetTreeLevels && left < right; d++) {
-                const uint32_t mid = left + (right - left) / 2;
-                const u32x4 e = tr[x];
-                const uint32_t ew[4] = {e.x, e.y, e.z, e.w};
-                int c = prefix_cmp(ew, kw);
-                if (c == 0) {  // a prefix tie: the entry's own bytes decide
-                    const lsm_rec_desc dd = a.idx_desc[base + mid];
-                    c = bound_cmp(ew, dd.key_len, a.img + dd.rec_off + 4, kw, kl, kp);
-                }
-                if (c < 0) {
-                    left = mid + 1;
-                    x = 2 * x + 2;
-                } else {
-                    right = mid;
-                    x = 2 * x + 1;
-                }
-            }
-        }
-        while (left < right) {
-            const uint32_t mid = left + (right - left) / 2;
-            const lsm_rec_desc d = a.idx_desc[base + mid];
-            const uint8_t *ep = a.img + d.rec_off + 4;
-            uint32_t ew[4];
-            key_prefix(ep, d.key_len, ew);
-            const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
-            if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
-            else right = mid;
-        }
         bool hit = false;
-        if (left < n) {
-            const lsm_rec_desc d = a.idx_desc[base + left];
-            const uint8_t *ep = a.img + d.rec_off + 4;
-            hit = d.key_len == kl && go_cmp(ep, d.key_len, kp, kl) == 0;
+        if (a.tree && n <= a.tree_nidx) {
+            // Go's bisection through the Seek tree: one 128-byte block per
+            // three steps.  The final left is the midpoint of the last step
+            // that set right, so Indexes[left].Key == target is that step's
+            // comparison being 0 (hit).
+            const uint8_t *tb = a.tree + (uint64_t)t * a.tree_stride;
+            uint64_t off = 0, cnt = 1, bi = 0;
+            uint32_t levels = a.tree_top;
+            while (left < right) {
+                const u32x4 *B = reinterpret_cast<const u32x4 *>(tb + (off + bi) * 128);
+                u32x4 nd[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) nd[q] = B[q];
+                uint32_t j = 0;
+#pragma unroll
+                for (uint32_t d = 0; d < 3; d++) {
+                    if (d >= levels || left >= right) break;
+                    u32x4 e = nd[0];
+                    if (d == 1) e = j == 1 ? nd[1] : nd[2];
+                    if (d == 2) {
+                        const u32x4 lo = j == 3 ? nd[3] : nd[4], hi = j == 5 ? nd[5] : nd[6];
+                        e = j < 5 ? lo : hi;
+                    }
+                    const uint32_t lw = j < 2 ? nd[7].x : j < 4 ? nd[7].y : j < 6 ? nd[7].z : nd[7].w;
+                    const uint32_t el = (lw >> (16 * (j & 1))) & 0xFFFFu;
+                    const uint32_t ew[4] = {e.x, e.y, e.z, e.w};
+                    const uint32_t mid = left + (right - left) / 2;
+                    const int c = tree_cmp(a, base, mid, ew, el, kw, kl, kp);
+                    if (c < 0) {
+                        left = mid + 1;
+                        j = 2 * j + 2;
+                    } else {
+                        right = mid;
+                        hit = c == 0;
+                        j = 2 * j + 1;
+                    }
+                }
+                // the child block: group g + 1, index 8 bi + the exit's rank
+                bi = off == 0 ? j - ((1u << levels) - 1) : 8 * bi + (j - 7);
+                off += cnt;
+                cnt = off == 1 ? (1ull << a.tree_top) : cnt * 8;
+                levels = 3;
+            }
+        } else {
+            // Go's bisection over the index (a variant loading both possible
+            // next midpoints' entries before each compare measured slower:
+            // 0.549 vs 0.375 ms per 1M-key Get, 3.0 GB of HBM traffic per
+            // call -- round 5, A/B)
+            while (left < right) {
+                const uint32_t mid = left + (right - left) / 2;
+                const lsm_rec_desc d = a.idx_desc[base + mid];
+                const uint8_t *ep = a.img + d.rec_off + 4;
+                uint32_t ew[4];
+                key_prefix(ep, d.key_len, ew);
+                const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
+                if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
+                else right = mid;
+            }
+            if (left < n) {
+                const lsm_rec_desc d = a.idx_desc[base + left];
+                const uint8_t *ep = a.img + d.rec_off + 4;
+                hit = d.key_len == kl && go_cmp(ep, d.key_len, kp, kl) == 0;
+            }
         }
         if (hit) {
             const int64_t off = a.idx_value[base + left];
@@ -3386,19 +3472,10 @@ extern "C" int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img,
                         d_table, d_may, w);
 }
 
-extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
-                             const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
-                             const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
-                             const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
-                             uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may,
-                             int32_t *d_result, lsm_rec_desc *d_value, void *d_workspace,
-                             size_t ws_bytes, void *stream) {
-    if (!ctx) return LSM_EINVAL;
-    if (nkeys == 0) return 0;
-    if (!d_keys || !d_koff || !d_table || !d_may || !d_result || !d_value) return LSM_EINVAL;
-    if (nfile && (!d_img || !d_file_off || !d_file_len || !d_meta || !d_idx_desc || !d_idx_value))
-        return LSM_EINVAL;
-    GetArgs a;
+static GetArgs get_args(const uint8_t *d_img, const uint64_t *d_file_off, const uint64_t *d_file_len,
+                        const lsm_sst_meta *d_meta, uint32_t nfile, const uint64_t *d_rec_base,
+                        const lsm_rec_desc *d_idx_desc, const int64_t *d_idx_value) {
+    GetArgs a{};
     a.img = d_img;
     a.file_off = d_file_off;
     a.file_len = d_file_len;
@@ -3407,6 +3484,49 @@ extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t 
     a.rec_base = d_rec_base;
     a.idx_desc = d_idx_desc;
     a.idx_value = d_idx_value;
+    return a;
+}
+
+extern "C" size_t lsm_level_get_tree_bytes(uint32_t nfile, uint32_t max_nidx) {
+    return (size_t)nfile * tree_shape(max_nidx).blocks * 128;
+}
+
+extern "C" int lsm_level_get_tree_build(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                                        const lsm_sst_meta *d_meta, uint32_t nfile,
+                                        const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
+                                        uint32_t max_nidx, void *d_tree, size_t tree_bytes,
+                                        void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    const TreeShape T = tree_shape(max_nidx);
+    if (nfile == 0 || T.D == 0) return 0;
+    if (!d_img || !d_file_off || !d_meta || !d_idx_desc || !d_tree) return LSM_EINVAL;
+    if (tree_bytes < lsm_level_get_tree_bytes(nfile, max_nidx)) return LSM_ESPACE;
+    GetArgs a = get_args(d_img, d_file_off, nullptr, d_meta, nfile, d_rec_base, d_idx_desc, nullptr);
+    a.tree_nidx = max_nidx;
+    a.tree_top = T.t;
+    a.tree_stride = T.blocks * 128;
+    const uint64_t grid = ((uint64_t)nfile * T.blocks * 8 + 255) / 256;
+    if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
+    hipLaunchKernelGGL(get_tree_build_kernel, dim3((uint32_t)grid), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), a, static_cast<uint8_t *>(d_tree), T);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                             const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
+                             const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
+                             const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
+                             uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may,
+                             int32_t *d_result, lsm_rec_desc *d_value, const void *d_tree,
+                             uint32_t tree_nidx, void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nkeys == 0) return 0;
+    if (!d_keys || !d_koff || !d_table || !d_may || !d_result || !d_value) return LSM_EINVAL;
+    if (nfile && (!d_img || !d_file_off || !d_file_len || !d_meta || !d_idx_desc || !d_idx_value))
+        return LSM_EINVAL;
+    GetArgs a = get_args(d_img, d_file_off, d_file_len, d_meta, nfile, d_rec_base, d_idx_desc,
+                         d_idx_value);
     a.keys = d_keys;
     a.koff = d_koff;
     a.nkeys = nkeys;
@@ -3414,24 +3534,19 @@ extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t 
     a.may = d_may;
     a.result = d_result;
     a.value = d_value;
-    a.tree = nullptr;
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    const TreeShape T = tree_shape(tree_nidx);
+    if (d_tree && T.D) {
+        a.tree = static_cast<const uint8_t *>(d_tree);
+        a.tree_nidx = tree_nidx;
+        a.tree_top = T.t;
+        a.tree_stride = T.blocks * 128;
+    }
     const uint64_t grid = (nkeys + 255) / 256;
     if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
-    if (d_workspace && nfile) {
-        if (ws_bytes < lsm_level_get_workspace_bytes(nfile)) return LSM_ESPACE;
-        u32x4 *tree = static_cast<u32x4 *>(d_workspace);
-        const uint64_t tg = ((uint64_t)nfile * kGetTreeNodes + 255) / 256;
-        hipLaunchKernelGGL(get_tree_kernel, dim3((uint32_t)tg), dim3(256), 0, s, a, tree);
-        a.tree = tree;
-    }
-    hipLaunchKernelGGL(level_get_kernel, dim3((uint32_t)grid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(level_get_kernel, dim3((uint32_t)grid), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), a);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
-}
-
-extern "C" size_t lsm_level_get_workspace_bytes(uint32_t nfile) {
-    return (size_t)nfile * kGetTreeNodes * sizeof(u32x4);
 }
 
 extern "C" int lsm_sum256(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,

@@ -503,40 +503,56 @@ def level_may_contain(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "R
 GET_ABSENT, GET_FOUND, GET_SEEK_FAILED, GET_VALUE_LENGTH, GET_VALUE_TOO_LONG, GET_VALUE_SHORT = range(6)
 
 
-def level_get_workspace(ctx: Context, nfile: int) -> torch.Tensor:
-    """The fence tree's workspace for lsm_level_get over nfile tables."""
-    nb = int(ctx.lib.lsm_level_get_workspace_bytes(nfile))
-    return torch.empty(max(nb, 16), dtype=torch.uint8, device=ctx.torch_device)
+@dataclass
+class SeekTree:
+    """lsm_level_get_tree_build's output for one level: the tree bytes and the
+    max_nidx it was built for (tables above it walk the index)."""
+    data: torch.Tensor
+    max_nidx: int
+
+
+def level_get_tree(ctx: Context, d_img: torch.Tensor, r: SstDecode, max_nidx: Optional[int] = None,
+                   stream=None) -> SeekTree:
+    """The level's Seek tree (lsm_level_get_tree_build), built once per level
+    load.  max_nidx None = the largest decoded nidx (read back once)."""
+    if max_nidx is None:
+        max_nidx = int(r.meta_numpy()[:r.nfile]["nidx"].max()) if r.nfile else 0
+    nb = int(ctx.lib.lsm_level_get_tree_bytes(r.nfile, max_nidx))
+    data = torch.empty(max(nb, 16), dtype=torch.uint8, device=ctx.torch_device)
+    if r.nfile and nb:
+        _lib.check(ctx.lib.lsm_level_get_tree_build(
+            ctx.handle, _ptr(d_img), _ptr(r.d_file_off), _ptr(r.meta), r.nfile, None,
+            _ptr(r.idx_desc), max_nidx, _ptr(data), nb, _stream_handle(stream)),
+            "lsm_level_get_tree_build")
+    return SeekTree(data, max_nidx)
 
 
 def level_get_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
                    table: torch.Tensor, may: torch.Tensor, result: torch.Tensor,
-                   value: torch.Tensor, workspace: Optional[torch.Tensor] = None,
-                   stream=None) -> None:
+                   value: torch.Tensor, tree: Optional[SeekTree] = None, stream=None) -> None:
     """lsm_level_get: searchFromTable past MayContain for each key with
     may = 1 -- Iterator.Seek over its table's decoded index, then the value
     (GetValueByOffset).  result int32 per key (GET_*), value int32[nkeys, 4]
-    (a lsm_rec_desc view of the value in d_img on GET_FOUND).  workspace
-    (level_get_workspace) holds the fence tree; None walks every level in the
-    index (the same answers)."""
+    (a lsm_rec_desc view of the value in d_img on GET_FOUND).  tree
+    (level_get_tree) walks the bisection through the Seek tree; None walks
+    the index (the same answers)."""
     _lib.check(ctx.lib.lsm_level_get(
         ctx.handle, _ptr(d_img) if r.nfile else None, _ptr(r.d_file_off) if r.nfile else None,
         _ptr(r.d_file_len) if r.nfile else None, _ptr(r.meta) if r.nfile else None, r.nfile, None,
         _ptr(r.idx_desc) if r.nfile else None, _ptr(r.idx_value) if r.nfile else None,
         _ptr(batch.keys), _ptr(batch.koff), batch.n, _ptr(table), _ptr(may), _ptr(result),
-        _ptr(value), _ptr(workspace) if workspace is not None else None,
-        workspace.numel() if workspace is not None else 0, _stream_handle(stream)), "lsm_level_get")
+        _ptr(value), _ptr(tree.data) if tree is not None else None,
+        tree.max_nidx if tree is not None else 0, _stream_handle(stream)), "lsm_level_get")
 
 
 def level_get(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
-              table: torch.Tensor, may: torch.Tensor, tree: bool = True, stream=None):
+              table: torch.Tensor, may: torch.Tensor, tree: Optional[SeekTree] = None,
+              stream=None):
     """-> (result int32[nkeys], value int32[nkeys, 4]) on the device."""
     result = torch.empty(max(batch.n, 1), dtype=torch.int32, device=ctx.torch_device)
     value = torch.empty((max(batch.n, 1), 4), dtype=torch.int32, device=ctx.torch_device)
-    ws = level_get_workspace(ctx, r.nfile) if tree else None
     if batch.n:
-        level_get_into(ctx, d_img, r, batch, table, may, result, value, workspace=ws,
-                       stream=stream)
+        level_get_into(ctx, d_img, r, batch, table, may, result, value, tree=tree, stream=stream)
     return result[:batch.n], value[:batch.n]
 
 

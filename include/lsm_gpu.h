@@ -40,7 +40,8 @@ extern "C" {
  * v5: lsm_merge_kvs_async and lsm_gather_kvs_dev (the merge's counts stay on
  * the device; the gather reads its pair count there); the level sparse index
  * (lsm_level_index_build, lsm_level_may_contain_indexed).
- * v6: lsm_level_get (the batched Get past MayContain: Seek + the value);
+ * v6: lsm_level_get (the batched Get past MayContain: Seek + the value) and
+ * its Seek tree (lsm_level_get_tree_bytes, lsm_level_get_tree_build);
  * lsm_compact_merge_async (the join and the merge as one call). */
 #define LSM_ABI_VERSION 6
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
@@ -332,11 +333,10 @@ int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img, const void
  * length prefix, key_len = 0, val_len}; otherwise d_value[i] is zero.  The
  * Seek runs over the nidx entries the decode kept (a table whose index did
  * not decode is one the Manager would not have loaded, manager.go:226-275).
- * d_workspace (lsm_level_get_workspace_bytes(nfile) bytes, or NULL) holds the
- * fence tree: the first levels of every table's bisection (which do not depend
- * on the keys) as 16-byte key prefixes, built by the call; the probes walk
- * them there and only the last levels in the index.  The steps are Go's either
- * way, so the answers are the same with and without it. */
+ * d_tree (or NULL) is the level's Seek tree from lsm_level_get_tree_build
+ * over the same decoded tables with max_nidx = tree_nidx; tables with more
+ * index entries than that walk the index.  The steps are Go's either way, so
+ * the answers are the same with and without the tree. */
 enum lsm_get_result {
     LSM_GET_ABSENT = 0,         /* (nil, nil): not MayContain, or no entry equals the key        */
     LSM_GET_FOUND = 1,          /* the value, d_value[i]                                          */
@@ -350,8 +350,21 @@ int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off
                   const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
                   const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
                   uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may, int32_t *d_result,
-                  lsm_rec_desc *d_value, void *d_workspace, size_t ws_bytes, void *stream);
-size_t lsm_level_get_workspace_bytes(uint32_t nfile);
+                  lsm_rec_desc *d_value, const void *d_tree, uint32_t tree_nidx, void *stream);
+
+/* The Seek tree of a level for lsm_level_get, built once when the level is
+ * loaded (the Manager keeps each table's decoded IndexBlock in memory,
+ * manager.go:226-275; Seek bisects it, index.go:157-181).  Go's bisection
+ * over n entries visits a fixed tree of midpoints whatever the keys hold; the
+ * tree stores, per table, each midpoint's 16-byte key prefix and length in
+ * 128-byte blocks of three levels, so a Seek reads one line per three steps.
+ * Tables with nidx <= max_nidx are built; lsm_level_get_tree_bytes(nfile,
+ * max_nidx) bytes (about 18 per entry at max_nidx).  Asynchronous. */
+size_t lsm_level_get_tree_bytes(uint32_t nfile, uint32_t max_nidx);
+int lsm_level_get_tree_build(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                             const lsm_sst_meta *d_meta, uint32_t nfile, const uint64_t *d_rec_base,
+                             const lsm_rec_desc *d_idx_desc, uint32_t max_nidx, void *d_tree,
+                             size_t tree_bytes, void *stream);
 
 /* ---- encode ---------------------------------------------------------------- */
 

@@ -52,9 +52,15 @@ def run(ctx, rng, images, probes):
     d_img = lsmgpu.to_device_bytes(buf, ctx.torch_device)
     r = lsmgpu.decode_sst(ctx, d_img, offs, lens)
     table, may = lsmgpu.level_may_contain(ctx, d_img, r, batch)
-    res, val = lsmgpu.level_get(ctx, d_img, r, batch, table, may)
-    # without the fence tree: every level of the bisection in the index
-    res0, val0 = lsmgpu.level_get(ctx, d_img, r, batch, table, may, tree=False)
+    res0, val0 = lsmgpu.level_get(ctx, d_img, r, batch, table, may)  # bisecting the index
+    # through the Seek tree: built for every table, and for a max_nidx below
+    # some tables' (they walk the index); the same answers
+    tree = lsmgpu.level_get_tree(ctx, d_img, r)
+    res, val = lsmgpu.level_get(ctx, d_img, r, batch, table, may, tree=tree)
+    if tree.max_nidx > 1:
+        part = lsmgpu.level_get_tree(ctx, d_img, r, max_nidx=tree.max_nidx // 2)
+        res1, val1 = lsmgpu.level_get(ctx, d_img, r, batch, table, may, tree=part)
+        assert torch.equal(res, res1) and torch.equal(val, val1)
     torch.cuda.synchronize()
     assert torch.equal(res, res0) and torch.equal(val, val0)
     table, may = table.cpu().numpy(), may.cpu().numpy()
@@ -169,11 +175,10 @@ def test_get_full_level_sample(ctx):
 
 
 def test_get_deep_unsorted_index(ctx):
-    """Tables deeper than the fence tree (n > 1,023: the walk continues in the
-    index) whose index entries are NOT sorted: Seek's answer is then whatever
-    Go's bisection path reaches, and the tree must take exactly those steps.
-    One sorted table of the same depth beside it, and keys sharing 18 bytes
-    (prefix ties inside the tree)."""
+    """Deep tables (n > 2,048: several tree groups) whose index entries are
+    NOT sorted: Seek's answer is then whatever Go's bisection path reaches,
+    and the tree must take exactly those steps.  One sorted table beside it,
+    and keys sharing 18 bytes (prefix ties: the bytes past 16 decide)."""
     rng = np.random.default_rng(205)
     lp = b"shared-prefix-xyz-"
     sk = sorted({lp + b"%07d" % int(x) for x in rng.integers(0, 10 ** 7, 3000)})
@@ -184,3 +189,17 @@ def test_get_deep_unsorted_index(ctx):
     probes += uk + [b"u%06d" % int(x) for x in rng.integers(0, 5000, 2000)] + [lp, lp[:16]]
     res, _ = run(ctx, rng, [im_sorted, im_unsorted], probes)
     assert (res[:len(sk[::2])] == ora.GET_FOUND).all()
+
+
+def test_seek_tree_shapes(ctx):
+    """Tables of every size from 0 to 70 entries (every top-block depth
+    1-3 and group count up to three), each probed with all its keys and the
+    keys between them, against the oracle with and without the tree."""
+    rng = np.random.default_rng(206)
+    images, probes = [], []
+    for n in list(range(1, 18)) + [31, 32, 33, 63, 64, 65, 70]:
+        keys = [b"t%03d-%05d" % (n, 10 * x) for x in range(n)]
+        images.append(build(keys, [b"%d" % x for x in range(n)], m=2048, k=3))
+        probes += keys + [b"t%03d-%05d" % (n, 10 * x + 5) for x in range(-1, n)]
+    res, _ = run(ctx, rng, images, probes)
+    assert (res == ora.GET_FOUND).sum() == sum(list(range(1, 18)) + [31, 32, 33, 63, 64, 65, 70])
