@@ -908,6 +908,7 @@ struct BloomOrArgs {
     const uint32_t *rec;
     uint32_t m, k, c64;
     uint32_t split;     // slice 0 = bits [0, split), slice 1 = [split, m)
+    uint32_t nfiles;
     uint64_t nwords;
     const uint64_t *koff;
     uint8_t *out;
@@ -1713,7 +1714,13 @@ __device__ __forceinline__ void bloom_or_body(const BloomOrArgs &a, uint64_t s, 
 
 __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs sa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
-    const uint32_t f = blockIdx.x, sl = blockIdx.y;
+    // workgroups b and b + 8 share an XCD (blocks are dealt round-robin over
+    // the 8 XCDs, the guide's observed placement; speed only): the two
+    // slices of filter f are blocks 16 (f / 8) + f % 8 and that + 8, so they
+    // run side by side on one XCD and the second read of the filter's hash
+    // records is served by that XCD's L2
+    const uint32_t b = blockIdx.x, f = (b / 16) * 8 + b % 8, sl = (b / 8) % 2;
+    if (f >= a.nfiles) return;
     // the image's header, filter prefix and footer (disjoint from the words)
     if (sl == 0 && threadIdx.x < kWave) sst_meta_body(sa, f);
     const uint32_t lo = sl * a.split, hi = lo + a.split < a.m ? lo + a.split : a.m;
@@ -3280,8 +3287,9 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         bo.koff = d_koff;
         bo.out = d_out;
         bo.file_off = d_file_off;
-        hipLaunchKernelGGL(bloom_or_kernel, dim3(nfile, (uint32_t)((m + osb - 1) / osb)), dim3(1024),
-                           (size_t)(osb / 8), s, bo, a);
+        bo.nfiles = nfile;
+        hipLaunchKernelGGL(bloom_or_kernel, dim3((nfile + 7) / 8 * 16), dim3(1024), (size_t)(osb / 8), s,
+                           bo, a);
         LSM_TRY(hipGetLastError());
     }
     if (forked || vfork) {  // join (also after an error): the caller's stream waits for the side
