@@ -978,6 +978,7 @@ constexpr uint32_t kSstChunkRecs = kSstWaves * kWave;  // records per workgroup
 constexpr uint32_t kRegWaves = 2;         // waves per workgroup
 constexpr uint32_t kRegWaveChunks = 1;    // 64-record chunks per wave (4: config 3 0.2573 ms, 2: 0.2500, 8: 0.2650; 1: 0.2488 vs 0.2531, round 5; A/B)
 constexpr uint32_t kRegBufDwords = 2432;  // both images of a chunk (9.5 KiB)
+constexpr uint32_t kRegIdxDwords = 1024;  // the IDX image alone (values from views: 4 KiB)
 constexpr uint32_t kRegSpanRecs = kRegWaves * kRegWaveChunks * kWave;  // records per workgroup
 constexpr uint32_t kRegMaxImage = 32 * kGatherMaskWords;  // dwords one mask covers
 
@@ -1195,8 +1196,15 @@ __device__ __forceinline__ void region_finish(const RegionPlan &R, uint32_t *buf
     __asm__ __volatile__("" ::: "memory");
 }
 
+// WithV = false (lsm_build_sst_views: the data region comes from the value
+// views' kernel): the buffer holds only the IDX image, 4 instead of 9.5 KiB
+// per wave, so a CU holds twice the waves (compaction 1.031-1.037 -> 1.018 ms
+// per call, A/B; the data region straight from the values arena without the
+// LDS image measured 0.250 -> 0.332 ms per config-3 build and is not used).
+template <bool WithV>
 __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kRegWaves][kRegBufDwords + kGatherMaskWords];
+    constexpr uint32_t BD = WithV ? kRegBufDwords : kRegIdxDwords;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kRegWaves][BD + kGatherMaskWords];
     const uint32_t f = blockIdx.x;
     const SstLayout L = sst_layout(a, f);
     const uint32_t wave = uni(threadIdx.x / kWave);
@@ -1204,7 +1212,7 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
     if (c0 >= L.e) return;
     const uint64_t cend = L.e - c0 < (uint64_t)kRegWaveChunks * kWave ? L.e : c0 + kRegWaveChunks * kWave;
     uint32_t *buf = lds[wave];
-    uint32_t *mask = buf + kRegBufDwords;
+    uint32_t *mask = buf + BD;
     uint8_t *img = a.out + uni64(a.file_off[f]);
     const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
     const uint64_t K0 = a.hrec ? uni64(a.file_start[0]) : 0;
@@ -1221,20 +1229,20 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
         RegionPlan pv, pi;
         bool ok = true;
         uint32_t ibase = 0;
-        if (!a.skip_v) {
-            ok = region_plan<LSM_GRAMMAR_V>(pv, off, cnt, dV, 0, kRegBufDwords, 0);
+        if (WithV) {
+            ok = region_plan<LSM_GRAMMAR_V>(pv, off, cnt, dV, 0, BD, 0);
             ibase = (pv.OD + pv.nD + 8 + 63) & ~63u;
         }
-        ok = ok && region_plan<LSM_GRAMMAR_IDX>(pi, off, cnt, dI, ibase, kRegBufDwords, xo_base);
+        ok = ok && region_plan<LSM_GRAMMAR_IDX>(pi, off, cnt, dI, ibase, BD, xo_base);
         const uint64_t cn = c0 + kWave;
         const bool more = cn < cend;
         if (ok) {
-            if (!a.skip_v) region_issue<LSM_GRAMMAR_V>(pv, buf, mask, a.vals);
+            if (WithV) region_issue<LSM_GRAMMAR_V>(pv, buf, mask, a.vals);
             region_issue<LSM_GRAMMAR_IDX>(pi, buf, mask, a.keys);
             const ChunkOffs nxt = more ? load_offs(a, cn, count(cn)) : off;
             // The DMA writes are invisible to the compiler's LDS tracking.
             __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-            if (!a.skip_v) region_finish<LSM_GRAMMAR_V>(pv, buf);
+            if (WithV) region_finish<LSM_GRAMMAR_V>(pv, buf);
             region_finish<LSM_GRAMMAR_IDX>(pi, buf);
             if (a.hrec && lane_id() < cnt) {
                 // Filter.Add's key hash (bloom.go:175-181) from the key
@@ -1259,8 +1267,8 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
             S.rs = L.s;
             S.vrs = Vs;
             ChunkTable *ct = reinterpret_cast<ChunkTable *>(buf);
-            if (!a.skip_v) encode_chunk_any<LSM_GRAMMAR_V, kRegMaxImage>(S, c0, cnt, dV, buf, nullptr, ct);
-            encode_chunk_any<LSM_GRAMMAR_IDX, kRegMaxImage>(S, c0, cnt, dI, buf, nullptr, ct);
+            if (WithV) encode_chunk_any<LSM_GRAMMAR_V, kRegMaxImage>(S, c0, cnt, dV, buf, nullptr, ct);
+            encode_chunk_any<LSM_GRAMMAR_IDX, (WithV ? kRegMaxImage : kRegIdxDwords)>(S, c0, cnt, dI, buf, nullptr, ct);
             if (a.hrec && lane_id() < cnt) {
                 uint64_t h[4];
                 sum256(a.keys + off.k0, off.k1 - off.k0, h);
@@ -3256,7 +3264,10 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     } while (0)
     if (chunks) {
         const uint32_t rspans = (max_file_records + kRegSpanRecs - 1) / kRegSpanRecs;
-        hipLaunchKernelGGL(sst_regions_kernel, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
+        if (a.skip_v)
+            hipLaunchKernelGGL(sst_regions_kernel<false>, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
+        else
+            hipLaunchKernelGGL(sst_regions_kernel<true>, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
         LSM_TRY(hipGetLastError());
         if (views && rc == 0) {
             // V descriptors: the records are copied whole (runs); KV

@@ -176,6 +176,22 @@ def test_sst_edge_records(ctx):
     sst_vs_oracle(ctx, kd, ko, vd, vo, starts, 1_600_000, 16)
 
 
+@pytest.mark.parametrize("vlen", [0, 1, 3, 8, 11, 12, 13, 100, 1021])
+def test_sst_uniform_value_sizes(ctx, vlen):
+    """Values of one size (the region writer's reciprocal record lookup):
+    sizes whose 16-byte output segments hold several value prefixes (< 12),
+    exactly one, or none; files starting at the arena's first byte and at odd
+    offsets."""
+    n = 3000
+    keys = np.frombuffer(b"".join(b"k%015d" % i for i in range(n)), np.uint8)
+    koff = np.arange(n + 1, dtype=np.uint64) * 16
+    rng = np.random.default_rng(vlen)
+    vals = rng.integers(0, 256, max(n * vlen, 1), dtype=np.uint8)
+    voff = np.arange(n + 1, dtype=np.uint64) * vlen
+    starts = np.array([0, 1, 70, 777, 1500, 2999, n], np.uint64)
+    sst_vs_oracle(ctx, keys, koff, vals, voff, starts, 1_600_000, 16)
+
+
 def test_sst_config3_full(ctx):
     """Config 3: 3.3 M records (16 B / 100 B) -> builder rule -> 207 full
     .sst images of 2,297,320 B + 1 partial, every image byte-identical."""
