@@ -204,11 +204,6 @@ def bench_may_contain(args, world, rank, local):
                    "false_positive_rate_absent": float(rows[~is_held].astype(bool).mean()),
                    "parallelism": f"dp{world} (probe batches per rank, no collective)",
                    "scaling_note": "weak, per-rank copy: every rank probes its own level copy"},
-        **({"seek_tree": ({"bytes": int(gtree.data.numel()), "max_nidx": gtree.max_nidx,
-                          "build_ms_once": round(tree_build_ms, 3),
-                          "note": "built with the level (lsm_level_get_tree_build), outside the step, "
-                                  "like the sparse index"} if gtree is not None else
-                         "off: Seek bisects the decoded index")} if get else {}),
         # algorithmic bytes per launch: the hit matrix written once, the probe
         # keys and offsets read once, every file's stored filter words read once
         "roofline": {"bound": "hbm", "kernel": "lsm_may_contain (all launches)",

@@ -11,8 +11,9 @@ OUT=gpurun_out; TAG=${TAG:-r03}
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)" >&2; timeout -k 10 $lim "$@"; }
-PHASE=${PHASE:-all}
-if [ "$PHASE" = all ] || [ "$PHASE" = 1 ]; then
+PHASE=${PHASE:-all}  # all, or a list of phases: "1 2"
+has() { [ "$PHASE" = all ] || [[ " $PHASE " == *" $1 "* ]]; }
+if has 1; then
 step pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1 \
   || { tail -60 $OUT/pytest_gpu_$TAG.log; exit 1; }
 tail -1 $OUT/pytest_gpu_$TAG.log
@@ -20,7 +21,7 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$
   || { tail -30 $OUT/smoke_$TAG.log; exit 1; }
 tail -1 $OUT/smoke_$TAG.log
 fi
-if [ "$PHASE" = all ] || [ "$PHASE" = 2 ]; then
+if has 2; then
 # single-kernel decode lines: FETCH_SIZE x2 + WRITE_SIZE of decode_v2_kernel
 declare -A DA DK
 DA[desc]="--config decode4k"; DK[desc]=decode4k:100000:desc
@@ -52,7 +53,7 @@ for cfg in ${PMCM-sst sstdec probe wal}; do
     profiles/${TAG}_pmc_$cfg.json $OUT/${TAG}_pmc_$cfg.json > /dev/null || exit 1
 done
 fi
-if [ "$PHASE" = all ] || [ "$PHASE" = 3 ]; then
+if has 3; then
 for line in ${LINES:-decode4k cfg4 decode64k mixed arena sst sstdec sstdec1 wal probe level get compact goheap e2e}; do
   case $line in
     cfg4) args="--global-blocks 1000000 --no-cpu-baseline" ;;
