@@ -2,6 +2,7 @@
 import sys
 R = ''  # run in the csrc directory (scripts/build_variant.sh's copy)
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+FIRST = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0  # > 0: two groups, the first this share of the files
 p = R + 'common.h'
 s = open(p).read()
 old = '''    hipEvent_t fork, join;'''
@@ -127,3 +128,13 @@ constexpr uint32_t kOrGroups = %d;  // file groups of the split build (<= lsm_ct
 assert old in s; s = s.replace(old, new)
 open(p, 'w').write(s)
 print('ok', G)
+if FIRST > 0:  # two unequal groups: the first FIRST of the files, then the rest
+    s = open(p).read()
+    old = '''                const uint32_t f0 = (uint32_t)((uint64_t)nfile * g / ngrp);
+                const uint32_t f1 = (uint32_t)((uint64_t)nfile * (g + 1) / ngrp);'''
+    new = '''                const uint32_t cut = (uint32_t)((double)nfile * %f);
+                const uint32_t f0 = g == 0 ? 0u : cut, f1 = g == 0 ? cut : nfile;''' % FIRST
+    assert old in s
+    s = s.replace(old, new)
+    open(p, 'w').write(s)
+    print('first', FIRST)
