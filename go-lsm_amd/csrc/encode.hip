@@ -2246,6 +2246,46 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nf
     }
 }
 
+// Filter.Test (bloom.go:371-379) of one probe against F, the bytes below
+// in_lds from LDS (lb), the rest from the image through L2.  Sixteen
+// locations at a time, every read of a round issued before any is waited for:
+// the LDS read at a clamped address, the tail read under a predicate into its
+// own register (a read per branch whose join waits for it is sixteen
+// serialized round trips).  Lds = false: no LDS copy, every bit from src.
+template <bool Lds = true>
+__device__ __forceinline__ uint32_t filter_test(const McFile &F, const uint64_t h[4], const uint8_t *lb,
+                                                uint64_t in_lds, const uint8_t *src) {
+    // k == 0: true; m == 0 < k: Go panics, answered false (DESIGN.md §3)
+    uint32_t r = F.k == 0 || F.m != 0;
+    const bool small = F.m <= (1ull << 30);
+    const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
+    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
+        uint64_t p[16];
+        uint32_t lv[16], gv[16];
+#pragma unroll
+        for (uint32_t u = 0; u < 16; u++) {
+            const uint64_t x = location(h[0], h[1], h[2], h[3], j0 + u);
+            p[u] = small ? mod_small(x, m32, rl, rh) : mod_barrett(x, F.m, F.mr);
+            const uint64_t q = 8 * (p[u] >> 6) + 7 - ((p[u] & 63) >> 3);
+            const bool inl = Lds && q < in_lds;
+            lv[u] = Lds ? lb[inl ? q : 0] : 0u;
+            gv[u] = 0xFFu;
+            if (j0 + u < F.k && !inl && p[u] < F.nbits) gv[u] = gbl(src)[q];
+        }
+        uint32_t bits = 1;
+#pragma unroll
+        for (uint32_t u = 0; u < 16; u++) {
+            const uint64_t q = 8 * (p[u] >> 6) + 7 - ((p[u] & 63) >> 3);
+            const uint32_t byte = Lds && q < in_lds ? lv[u] : gv[u];
+            // bitset.Test is false past its length
+            const uint32_t bit = p[u] < F.nbits ? (byte >> (p[u] & 7)) & 1u : 0u;
+            bits &= j0 + u < F.k ? bit : 1u;
+        }
+        r = bits;
+    }
+    return r;
+}
+
 // One workgroup per file: the first kMcLdsBytes of the stored filter words
 // go to LDS (all loads in flight), the rest (a 1.6M-bit filter is 200 KB) is
 // read from L2, where the workgroup's repeated touches keep it.  Each probe's
@@ -2308,31 +2348,8 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
             n0 = w.hash[4 * (uint64_t)in]; n1 = w.hash[4 * (uint64_t)in + 1];
             n2 = w.hash[4 * (uint64_t)in + 2]; n3 = w.hash[4 * (uint64_t)in + 3];
         }
-        // k == 0: true; m == 0 < k: Go panics, answered false
-        uint32_t r = F.k == 0 || F.m != 0;
-        // Test is the AND of all k bits (its early exit changes nothing):
-        // sixteen bit reads in flight at a time
-        for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
-            uint32_t bits = 1;
-#pragma unroll
-            for (uint32_t u = 0; u < 16; u++) {
-                const uint32_t j = j0 + u;
-                if (j < F.k) {
-                    const uint64_t x = location(h0, h1, h2, h3, j);
-                    const uint64_t p = small ? mod_small(x, m32, rl, rh) : mod_barrett(x, F.m, F.mr);
-                    if (p >= F.nbits) {
-                        bits = 0;  // bitset.Test is false past its length
-                    } else {
-                        const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
-                        uint32_t byte;
-                        if (q < in_lds) byte = lb[q];
-                        else byte = gbl(src)[q];  // the tail past the LDS copy, from L2
-                        bits &= byte >> (p & 7);
-                    }
-                }
-            }
-            r = bits & 1;
-        }
+        const uint64_t h[4] = {h0, h1, h2, h3};
+        const uint32_t r = filter_test(F, h, lb, in_lds, src);
         if (!r) hit[(uint64_t)i * nfile + f] = 0;
         t = tn; i = in; h0 = n0; h1 = n1; h2 = n2; h3 = n3;
     }
@@ -2610,61 +2627,44 @@ __device__ __forceinline__ uint64_t stage_filter(const uint8_t *src, uint64_t nb
     return n16 ? in_lds : 0;
 }
 
-// Filter.Test (bloom.go:371-379) of one probe against F, the bytes below
-// in_lds from LDS (lb), the rest from the image through L2.
-__device__ __forceinline__ uint32_t filter_test(const McFile &F, const uint64_t h[4], const uint8_t *lb,
-                                                uint64_t in_lds, const uint8_t *src) {
-    // k == 0: true; m == 0 < k: Go panics, answered false (DESIGN.md §3)
-    uint32_t r = F.k == 0 || F.m != 0;
-    const bool small = F.m <= (1ull << 30);
-    const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
-    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
-        uint32_t bits = 1;
-#pragma unroll
-        for (uint32_t u = 0; u < 16; u++) {
-            const uint32_t j = j0 + u;
-            if (j < F.k) {
-                const uint64_t x = location(h[0], h[1], h[2], h[3], j);
-                const uint64_t p = small ? mod_small(x, m32, rl, rh) : mod_barrett(x, F.m, F.mr);
-                if (p >= F.nbits) {
-                    bits = 0;  // bitset.Test is false past its length
-                } else {
-                    const uint64_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
-                    const uint32_t byte = q < in_lds ? lb[q] : gbl(src)[q];
-                    bits &= byte >> (p & 7);
-                }
-            }
-        }
-        r = bits & 1;
-    }
-    return r;
-}
-
 // filter_test from a probe's hash record (lv_compact tables): the k <= 16
-// locations by additions (unpack_hash_rec), each bit read as filter_test does.
+// locations by additions (unpack_hash_rec), the bits read as filter_test does
+// (all reads in flight, then combined).
 __device__ __forceinline__ uint32_t filter_test_rec(const McFile &F, const HashRecSteps &H0,
                                                     uint32_t m, const uint8_t *lb, uint64_t in_lds,
                                                     const uint8_t *src) {
     uint32_t r[4] = {H0.r[0], H0.r[1], H0.r[2], H0.r[3]};
-    uint32_t bits = 1;
+    uint32_t pos[kSplitMaxK];
 #pragma unroll
     for (uint32_t j = 0; j < kSplitMaxK; j++) {
         const uint32_t c = j & 3, n = j >> 2;
-        if (j >= F.k) break;
-        const uint32_t p = r[c];
-        if (p >= F.nbits) {
-            bits = 0;  // bitset.Test is false past its length
-        } else {
-            const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
-            const uint32_t byte = q < in_lds ? lb[q] : gbl(src)[q];
-            bits &= byte >> (p & 7);
-        }
+        pos[j] = r[c];
         if (n < 3) {
-            const uint32_t t = p + H0.st[c][n];
+            const uint32_t t = r[c] + H0.st[c][n];
             r[c] = min(t, t - m);
         }
     }
-    return bits & 1;
+    uint32_t lv[kSplitMaxK], gv[kSplitMaxK];
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t p = pos[j];
+        const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+        const bool inl = q < in_lds;
+        lv[j] = lb[inl ? q : 0u];
+        gv[j] = 0xFFu;
+        if (j < F.k && !inl && p < F.nbits) gv[j] = gbl(src)[q];
+    }
+    uint32_t bits = 1;
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t p = pos[j];
+        const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+        const uint32_t byte = q < in_lds ? lv[j] : gv[j];
+        // bitset.Test is false past its length
+        const uint32_t bit = p < F.nbits ? (byte >> (p & 7)) & 1u : 0u;
+        bits &= j < F.k ? bit : 1u;
+    }
+    return bits;
 }
 
 __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
@@ -2672,10 +2672,12 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
                                                              uint8_t *may) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
     __shared__ uint32_t sb[kLvMaxWgs + 1];  // first probe of each workgroup's segment
+    __shared__ uint32_t sg[kLvMaxWgs];      // its first slot in that workgroup
     __shared__ uint32_t part[kLvThreads];
     const uint32_t f = blockIdx.x, t = threadIdx.x;
     // the table's segments: counts scanned (nwg <= 1,024: one per thread)
     const uint32_t c = t < nwg ? w.cnt[(uint64_t)f * nwg + t] : 0u;
+    if (t < nwg) sg[t] = w.grid[(uint64_t)f * nwg + t];
     part[t] = c;
     __syncthreads();
     for (uint32_t d = 1; d < kLvThreads; d <<= 1) {
@@ -2698,7 +2700,7 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
             if (sb[mid] <= q) a = mid;
             else b = mid;
         }
-        return (uint64_t)a * kLvProbes + w.grid[(uint64_t)f * nwg + a] + (q - sb[a]);
+        return (uint64_t)a * kLvProbes + sg[a] + (q - sb[a]);
     };
     const bool compact = lv_compact(F);
     const uint32_t m32 = (uint32_t)F.m;
@@ -2769,7 +2771,7 @@ __global__ __launch_bounds__(256) void lv_probe_kernel(const uint8_t *img, uint3
                 uint64_t h[4];
                 sum256(kp, kl, h);
                 const uint8_t *src = img + F.words_at;
-                r = (uint8_t)filter_test(F, h, src, ~0ull, src);
+                r = (uint8_t)filter_test<false>(F, h, nullptr, 0, src);
             }
         }
         may[i] = r;
