@@ -2038,6 +2038,18 @@ struct McWs {
     uint32_t *list;     // nkeys
 };
 
+// key bytes [p, p + len) as four big-endian words, zero padded past len
+// (reads 16 bytes at p: the input slack covers a key that ends a buffer)
+__device__ __forceinline__ void key_prefix(const uint8_t *p, uint64_t len, uint32_t kw[4]) {
+    uint64_t f0 = ldg_u64_unaligned(p), f1 = ldg_u64_unaligned(p + 8);
+    if (len < 8) { f0 &= len ? (~0ull >> (64 - 8 * len)) : 0; f1 = 0; }
+    else if (len < 16) f1 &= len > 8 ? (~0ull >> (128 - 8 * len)) : 0;
+    kw[0] = __builtin_bswap32((uint32_t)f0);
+    kw[1] = __builtin_bswap32((uint32_t)(f0 >> 32));
+    kw[2] = __builtin_bswap32((uint32_t)f1);
+    kw[3] = __builtin_bswap32((uint32_t)(f1 >> 32));
+}
+
 __device__ __forceinline__ McFile mc_file(const uint8_t *img, const uint64_t *file_off,
                                           const lsm_sst_meta &M, uint32_t f) {
     const uint64_t fo = file_off[f];
@@ -2046,9 +2058,12 @@ __device__ __forceinline__ McFile mc_file(const uint8_t *img, const uint64_t *fi
     F.ok = M.stage != 1 && M.stage != 2;
     F.lo_len = (uint32_t)M.min_key_len;
     F.hi_len = (uint32_t)M.max_key_len;
-    for (uint32_t j = 0; j < 4; j++) {
-        F.lo[j] = F.ok ? be_word_at(base + M.min_key_off, M.min_key_len, j) : 0;
-        F.hi[j] = F.ok ? be_word_at(base + M.max_key_off, M.max_key_len, j) : 0;
+    // the key prefixes by unaligned 8-byte loads, all in flight (byte loads
+    // under a per-byte condition were 32 serialized round trips per file)
+    for (uint32_t j = 0; j < 4; j++) F.lo[j] = F.hi[j] = 0;
+    if (F.ok) {
+        key_prefix(base + M.min_key_off, M.min_key_len, F.lo);
+        key_prefix(base + M.max_key_off, M.max_key_len, F.hi);
     }
     F.lo_at = fo + M.min_key_off;
     F.hi_at = fo + M.max_key_off;
@@ -2337,8 +2352,6 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint8_t *lb = fbytes + delta;  // LDS
-    const bool small = F.m <= (1ull << 30);
-    const uint32_t m32 = (uint32_t)F.m, rl = (uint32_t)F.mr, rh = (uint32_t)(F.mr >> 32);
     while (t < b1) {
         const uint32_t tn = t + kMcTestThreads;
         uint32_t in = 0;
@@ -2451,10 +2464,8 @@ __device__ __forceinline__ McFile lv_file(const uint8_t *img, const uint64_t *fi
     McFile F = mc_file(img, file_off, M, f);
     if (M.stage == 2) {  // header decoded, filter not: search by its MinKey
         const uint8_t *base = img + file_off[f];
-        for (uint32_t j = 0; j < 4; j++) {
-            F.lo[j] = be_word_at(base + M.min_key_off, M.min_key_len, j);
-            F.hi[j] = be_word_at(base + M.max_key_off, M.max_key_len, j);
-        }
+        key_prefix(base + M.min_key_off, M.min_key_len, F.lo);
+        key_prefix(base + M.max_key_off, M.max_key_len, F.hi);
     } else if (M.stage == 1) {
         F.lo_len = F.hi_len = 0;
     }
@@ -2839,17 +2850,6 @@ __host__ __device__ inline TreeShape tree_shape(uint32_t max_nidx) {
     return T;
 }
 
-// key bytes [p, p + len) as four big-endian words, zero padded past len
-// (reads 16 bytes at p: the input slack covers a key that ends a buffer)
-__device__ __forceinline__ void key_prefix(const uint8_t *p, uint64_t len, uint32_t kw[4]) {
-    uint64_t f0 = ldg_u64_unaligned(p), f1 = ldg_u64_unaligned(p + 8);
-    if (len < 8) { f0 &= len ? (~0ull >> (64 - 8 * len)) : 0; f1 = 0; }
-    else if (len < 16) f1 &= len > 8 ? (~0ull >> (128 - 8 * len)) : 0;
-    kw[0] = __builtin_bswap32((uint32_t)f0);
-    kw[1] = __builtin_bswap32((uint32_t)(f0 >> 32));
-    kw[2] = __builtin_bswap32((uint32_t)f1);
-    kw[3] = __builtin_bswap32((uint32_t)(f1 >> 32));
-}
 
 // One thread per (table, block, node slot 0-7; slot 7 idle).
 __global__ __launch_bounds__(256) void get_tree_build_kernel(GetArgs a, uint8_t *tree, TreeShape T) {
