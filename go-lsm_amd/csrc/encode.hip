@@ -2027,6 +2027,15 @@ constexpr uint32_t kMcGroupPer = 2;  // probes per thread
 constexpr uint32_t kMcGroupProbes = kMcGroupThreads * kMcGroupPer;
 constexpr uint32_t kMcMaxFiles = 2048;  // LDS bounds + counters; more files: per-probe path
 
+// A table whose filter takes the 16-byte hash record of the encode path
+// (store_hash_rec: m <= 2^21, k <= 16; go-lsm's 1.6 Mbit, k = 16): classify
+// stores the record for the table's m, and the test rebuilds the locations
+// from it by additions -- 16 bytes per probe through the workspace instead
+// of the 32-byte sum256, and no modulo in the test.
+__device__ __forceinline__ bool lv_compact(const McFile &F) {
+    return F.m != 0 && F.m <= (1ull << kHashRecBits) && F.k <= kSplitMaxK;
+}
+
 struct McWs {
     uint32_t *flag;     // [0] = 1: grouped path
     McFile *files;
@@ -2034,7 +2043,8 @@ struct McWs {
     uint32_t *off;      // nfile + 1: exclusive offsets of the files' probe lists
     uint32_t *cursor;   // nfile
     uint32_t *cand;     // nkeys
-    uint64_t *hash;     // 4 * nkeys
+    uint64_t *hash;     // 4 * nkeys: sum256 (files that are not lv_compact)
+    u32x4 *rec;         // nkeys: 16-byte hash record (lv_compact files)
     uint32_t *list;     // nkeys
 };
 
@@ -2193,7 +2203,13 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
                 atomicAdd(&lh[c], 1u);
                 uint64_t h[4];  // only candidates are ever tested
                 sum256_pre(kp, kl[p], f0[p], f1[p], h);
-                for (int j = 0; j < 4; j++) w.hash[4 * i + j] = h[j];
+                const McFile &F = w.files[c];
+                if (lv_compact(F)) {  // 16 bytes, and no modulo in the test
+                    store_hash_rec(h, (uint32_t)F.m, (uint32_t)F.mr, (uint32_t)(F.mr >> 32),
+                                   reinterpret_cast<uint32_t *>(w.rec + i));
+                } else {
+                    for (int j = 0; j < 4; j++) w.hash[4 * i + j] = h[j];
+                }
             }
         }
         w.cand[i] = c;
@@ -2301,6 +2317,46 @@ __device__ __forceinline__ uint32_t filter_test(const McFile &F, const uint64_t 
     return r;
 }
 
+// filter_test from a probe's hash record (lv_compact tables): the k <= 16
+// locations by additions (unpack_hash_rec), the bits read as filter_test does
+// (all reads in flight, then combined).
+__device__ __forceinline__ uint32_t filter_test_rec(const McFile &F, const HashRecSteps &H0,
+                                                    uint32_t m, const uint8_t *lb, uint64_t in_lds,
+                                                    const uint8_t *src) {
+    uint32_t r[4] = {H0.r[0], H0.r[1], H0.r[2], H0.r[3]};
+    uint32_t pos[kSplitMaxK];
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t c = j & 3, n = j >> 2;
+        pos[j] = r[c];
+        if (n < 3) {
+            const uint32_t t = r[c] + H0.st[c][n];
+            r[c] = min(t, t - m);
+        }
+    }
+    uint32_t lv[kSplitMaxK], gv[kSplitMaxK];
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t p = pos[j];
+        const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+        const bool inl = q < in_lds;
+        lv[j] = lb[inl ? q : 0u];
+        gv[j] = 0xFFu;
+        if (j < F.k && !inl && p < F.nbits) gv[j] = gbl(src)[q];
+    }
+    uint32_t bits = 1;
+#pragma unroll
+    for (uint32_t j = 0; j < kSplitMaxK; j++) {
+        const uint32_t p = pos[j];
+        const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
+        const uint32_t byte = q < in_lds ? lv[j] : gv[j];
+        // bitset.Test is false past its length
+        const uint32_t bit = p < F.nbits ? (byte >> (p & 7)) & 1u : 0u;
+        bits &= j < F.k ? bit : 1u;
+    }
+    return bits;
+}
+
 // One workgroup per file: the first kMcLdsBytes of the stored filter words
 // go to LDS (all loads in flight), the rest (a 1.6M-bit filter is 200 KB) is
 // read from L2, where the workgroup's repeated touches keep it.  Each probe's
@@ -2315,12 +2371,23 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     const uint32_t b0 = w.off[f], b1 = w.off[f + 1];
     if (b0 == b1) return;
     const McFile F = w.files[f];
+    // lv_compact files: the probe's 16-byte hash record (classify), the
+    // locations rebuilt by additions; others: its sum256
+    const bool compact = lv_compact(F);
+    const uint32_t m32 = (uint32_t)F.m;
+    // 2^64 mod m for the record's carried steps
+    const uint32_t c64 = compact ? (mod_small(~0ull, m32, (uint32_t)F.mr, (uint32_t)(F.mr >> 32)) + 1) % m32 : 0u;
+    const u32x4 *hash4 = reinterpret_cast<const u32x4 *>(w.hash);
     uint32_t t = b0 + threadIdx.x, i = 0;
-    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    u32x4 hx = {0, 0, 0, 0}, hy = {0, 0, 0, 0};
     if (t < b1) {
         i = w.list[t];
-        h0 = w.hash[4 * (uint64_t)i]; h1 = w.hash[4 * (uint64_t)i + 1];
-        h2 = w.hash[4 * (uint64_t)i + 2]; h3 = w.hash[4 * (uint64_t)i + 3];
+        if (compact) {
+            hx = w.rec[i];
+        } else {
+            hx = hash4[2 * (uint64_t)i];
+            hy = hash4[2 * (uint64_t)i + 1];
+        }
     }
     // LDS holds the words from the 16-byte boundary below them: aligned
     // 16-byte global->LDS loads (no VGPR staging, all in flight), each chunk
@@ -2355,16 +2422,26 @@ __global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *
     while (t < b1) {
         const uint32_t tn = t + kMcTestThreads;
         uint32_t in = 0;
-        uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+        u32x4 xn = {0, 0, 0, 0}, yn = {0, 0, 0, 0};
         if (tn < b1) {  // next probe's hash in flight during this one's tests
             in = w.list[tn];
-            n0 = w.hash[4 * (uint64_t)in]; n1 = w.hash[4 * (uint64_t)in + 1];
-            n2 = w.hash[4 * (uint64_t)in + 2]; n3 = w.hash[4 * (uint64_t)in + 3];
+            if (compact) {
+                xn = w.rec[in];
+            } else {
+                xn = hash4[2 * (uint64_t)in];
+                yn = hash4[2 * (uint64_t)in + 1];
+            }
         }
-        const uint64_t h[4] = {h0, h1, h2, h3};
-        const uint32_t r = filter_test(F, h, lb, in_lds, src);
+        uint32_t r;
+        if (compact) {
+            r = filter_test_rec(F, unpack_hash_rec(hx, m32, c64), m32, lb, in_lds, src);
+        } else {
+            const uint64_t h[4] = {(uint64_t)hx.y << 32 | hx.x, (uint64_t)hx.w << 32 | hx.z,
+                                   (uint64_t)hy.y << 32 | hy.x, (uint64_t)hy.w << 32 | hy.z};
+            r = filter_test(F, h, lb, in_lds, src);
+        }
         if (!r) hit[(uint64_t)i * nfile + f] = 0;
-        t = tn; i = in; h0 = n0; h1 = n1; h2 = n2; h3 = n3;
+        t = tn; i = in; hx = xn; hy = yn;
     }
 }
 
@@ -2383,6 +2460,7 @@ McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) 
     w.cursor = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
     w.cand = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
     w.hash = reinterpret_cast<uint64_t *>(take(32 * (nkeys ? nkeys : 1)));
+    w.rec = reinterpret_cast<u32x4 *>(take(16 * (nkeys ? nkeys : 1)));
     w.list = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
     if (total) *total = at;
     return w;
@@ -2425,14 +2503,6 @@ struct LvWs {
     u32x4 *ext;       // [nwg * 2048] h2, h3 (tables that are not lv_compact)
 };
 
-// A table whose filter takes the 16-byte hash record of the encode path
-// (store_hash_rec: m <= 2^21, k <= 16; go-lsm's 1.6 Mbit, k = 16): classify
-// stores the record for the table's m, and the test rebuilds the locations
-// from it by additions -- 16 bytes per probe through the workspace instead
-// of the 32-byte sum256, and no modulo in the test.
-__device__ __forceinline__ bool lv_compact(const McFile &F) {
-    return F.m != 0 && F.m <= (1ull << kHashRecBits) && F.k <= kSplitMaxK;
-}
 
 LvWs lv_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
     LvWs w{};
@@ -2638,45 +2708,6 @@ __device__ __forceinline__ uint64_t stage_filter(const uint8_t *src, uint64_t nb
     return n16 ? in_lds : 0;
 }
 
-// filter_test from a probe's hash record (lv_compact tables): the k <= 16
-// locations by additions (unpack_hash_rec), the bits read as filter_test does
-// (all reads in flight, then combined).
-__device__ __forceinline__ uint32_t filter_test_rec(const McFile &F, const HashRecSteps &H0,
-                                                    uint32_t m, const uint8_t *lb, uint64_t in_lds,
-                                                    const uint8_t *src) {
-    uint32_t r[4] = {H0.r[0], H0.r[1], H0.r[2], H0.r[3]};
-    uint32_t pos[kSplitMaxK];
-#pragma unroll
-    for (uint32_t j = 0; j < kSplitMaxK; j++) {
-        const uint32_t c = j & 3, n = j >> 2;
-        pos[j] = r[c];
-        if (n < 3) {
-            const uint32_t t = r[c] + H0.st[c][n];
-            r[c] = min(t, t - m);
-        }
-    }
-    uint32_t lv[kSplitMaxK], gv[kSplitMaxK];
-#pragma unroll
-    for (uint32_t j = 0; j < kSplitMaxK; j++) {
-        const uint32_t p = pos[j];
-        const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
-        const bool inl = q < in_lds;
-        lv[j] = lb[inl ? q : 0u];
-        gv[j] = 0xFFu;
-        if (j < F.k && !inl && p < F.nbits) gv[j] = gbl(src)[q];
-    }
-    uint32_t bits = 1;
-#pragma unroll
-    for (uint32_t j = 0; j < kSplitMaxK; j++) {
-        const uint32_t p = pos[j];
-        const uint32_t q = 8 * (p >> 6) + 7 - ((p & 63) >> 3);
-        const uint32_t byte = q < in_lds ? lv[j] : gv[j];
-        // bitset.Test is false past its length
-        const uint32_t bit = p < F.nbits ? (byte >> (p & 7)) & 1u : 0u;
-        bits &= j < F.k ? bit : 1u;
-    }
-    return bits;
-}
 
 __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
                                                              uint32_t nwg, LvWs w, uint64_t k_begin,

@@ -176,3 +176,20 @@ def test_level_search_two_passes(ctx):
     x = rng.integers(0, 17000, n)
     probes = [b"Q%06d" % int(v) for v in x]
     check(ctx, rng, images, probes)
+
+
+def test_level_search_mixed_filter_shapes(ctx):
+    """Tables whose filters take the 16-byte hash record (m <= 2^21, k <= 16)
+    beside tables that take the full sum256 (m just above 2^21, k = 20) in one
+    level: both record kinds and both test paths in one call."""
+    rng = np.random.default_rng(105)
+    shapes = [(2048, 4), (3_000_000, 7), (4096, 20), (1_600_000, 16), (1 << 21, 16), ((1 << 21) + 1, 3),
+              (64, 17), (700_000, 9)]
+    images, held = [], []
+    for f, (m, k) in enumerate(shapes):
+        keys = sorted({b"X%07d" % (f * 100000 + int(x)) for x in rng.integers(0, 90000, 600)})
+        images.append(build(keys, m=m, k=k))
+        held += keys[::40]
+    probes = held + [b"X%07d" % int(x) for x in rng.integers(0, 850_000, 20_000)] + [b"", b"Y"]
+    table, may = check(ctx, rng, images, probes)
+    assert may[:len(held)].all()

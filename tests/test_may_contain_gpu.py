@@ -164,6 +164,21 @@ def test_may_contain_sorted_large_filters(ctx):
     check(ctx, rng, images, probes)
 
 
+def test_may_contain_sorted_mixed_filter_shapes(ctx):
+    """Grouped path with files whose filters take the 16-byte hash record
+    (m <= 2^21, k <= 16) beside files that take the full sum256 (m just above
+    2^21, k = 20): both record kinds and both test paths in one call."""
+    rng = np.random.default_rng(56)
+    shapes = [(2048, 4), (3_000_000, 7), (4096, 20), (1_600_000, 16), (1 << 21, 16), ((1 << 21) + 1, 3),
+              (64, 17), (700_000, 9)]
+    images = []
+    for f, (m, k) in enumerate(shapes):
+        keys = sorted({b"X%07d" % (f * 10000 + int(x)) for x in rng.integers(0, 9000, 300)})
+        images.append(build(keys, m=m, k=k))
+    probes = [b"X%07d" % int(x) for x in rng.integers(0, 85000, 3000)] + [b"", b"X", b"Y"]
+    check(ctx, rng, images, probes)
+
+
 def test_may_contain_sorted_shared_long_prefixes(ctx):
     """Grouped path where every bound shares its first 16+ bytes (the LDS
     bound prefixes tie and the byte comparison decides): keys "tenant-...-/"
