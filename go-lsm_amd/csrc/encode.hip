@@ -2015,12 +2015,12 @@ __global__ __launch_bounds__(kMcThreads) void may_contain_kernel(const uint8_t *
 
 // Grouped path for the level >= 1 shape (every file decoded, files in key
 // order with disjoint ranges, at most kMcMaxFiles files): each probe has at
-// most one candidate file.  The candidates are hashed once, grouped by file
-// (a counting sort), and each file's workgroup stages the filter in LDS and
-// tests its probes' bits there: the filter bits are read once from HBM
-// instead of once per probe bit.
+// most one candidate file.  mc_classify_kernel hashes the candidates once and
+// groups each workgroup's by file into its slots (the level search's layout,
+// LvWs), and lv_test_kernel<true> (one workgroup per file) stages the filter
+// in LDS and tests its probes' bits there: the filter bits are read once from
+// HBM instead of once per probe bit.
 constexpr uint32_t kMcLdsBytes = 144 * 1024;  // filter words staged in LDS per file
-constexpr uint32_t kMcTestThreads = 1024;
 constexpr uint32_t kMcNone = 0xFFFFFFFFu;
 constexpr uint32_t kMcGroupThreads = 1024;
 constexpr uint32_t kMcGroupPer = 2;  // probes per thread
@@ -2036,16 +2036,51 @@ __device__ __forceinline__ bool lv_compact(const McFile &F) {
     return F.m != 0 && F.m <= (1ull << kHashRecBits) && F.k <= kSplitMaxK;
 }
 
+constexpr uint32_t kLvThreads = 1024;
+constexpr uint32_t kLvPer = 2;  // probes per thread
+constexpr uint32_t kLvProbes = kLvThreads * kLvPer;
+constexpr uint32_t kLvMaxFiles = 2048;
+constexpr uint32_t kLvMaxWgs = 1024;  // classify workgroups per pass (2M probes)
+
+struct LvWs {
+    McFile *files;
+    uint32_t *grid;   // [nfile][nwg]: the table's first slot in the workgroup
+    uint32_t *cnt;    // [nfile][nwg]: the table's probes in the workgroup
+    uint32_t *ids;    // [nwg * 2048] probe of each slot
+    u32x4 *rec;       // [nwg * 2048] its 16-byte hash record (lv_compact tables),
+                      // else h0, h1 of its sum256
+    u32x4 *ext;       // [nwg * 2048] h2, h3 (tables that are not lv_compact)
+};
+
+
+LvWs lv_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
+    LvWs w{};
+    size_t at = 0;
+    auto take = [&](size_t bytes) -> uint8_t * {
+        uint8_t *p = base ? base + at : nullptr;
+        at += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    const uint64_t pass = nkeys < (uint64_t)kLvMaxWgs * kLvProbes ? nkeys : (uint64_t)kLvMaxWgs * kLvProbes;
+    const uint64_t nwg = (pass + kLvProbes - 1) / kLvProbes;
+    const size_t nf = nfile ? nfile : 1;
+    w.files = reinterpret_cast<McFile *>(take(sizeof(McFile) * nf));
+    w.grid = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
+    w.cnt = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
+    w.ids = reinterpret_cast<uint32_t *>(take(4 * (nwg ? nwg : 1) * kLvProbes));
+    w.rec = reinterpret_cast<u32x4 *>(take(16 * (nwg ? nwg : 1) * kLvProbes));
+    w.ext = reinterpret_cast<u32x4 *>(take(16 * (nwg ? nwg : 1) * kLvProbes));
+    if (total) *total = at;
+    return w;
+}
+
+static_assert(kMcGroupProbes == kLvProbes && kMcGroupThreads == kLvThreads && kMcMaxFiles == kLvMaxFiles,
+              "the all-tables classify fills the level search's slot layout");
+
 struct McWs {
     uint32_t *flag;     // [0] = 1: grouped path
     McFile *files;
-    uint32_t *hist;     // nfile + 1: candidate counts per file
-    uint32_t *off;      // nfile + 1: exclusive offsets of the files' probe lists
-    uint32_t *cursor;   // nfile
-    uint32_t *cand;     // nkeys
-    uint64_t *hash;     // 4 * nkeys: sum256 (files that are not lv_compact)
-    u32x4 *rec;         // nkeys: 16-byte hash record (lv_compact files)
-    uint32_t *list;     // nkeys
+    LvWs lv;            // the probes grouped by candidate file, as the level search's
 };
 
 // key bytes [p, p + len) as four big-endian words, zero padded past len
@@ -2092,8 +2127,6 @@ __global__ __launch_bounds__(256) void mc_prep_kernel(const uint8_t *img, const 
     for (uint32_t f = threadIdx.x; f < nfile; f += blockDim.x) {
         const McFile F = mc_file(img, file_off, meta[f], f);
         w.files[f] = F;
-        w.hist[f] = 0;
-        w.cursor[f] = 0;
         // m < 2^63 for the Barrett reduction; MinKey <= MaxKey (a corrupted
         // header with min > max would break the order of the bound search)
         ok = ok && F.ok && F.m < (1ull << 63) &&
@@ -2106,10 +2139,7 @@ __global__ __launch_bounds__(256) void mc_prep_kernel(const uint8_t *img, const 
         ok = ok && bound_cmp_fast(A.hi, A.hi_len, img + A.hi_at, B.lo, B.lo_len, img + B.lo_at) < 0;
     }
     ok = __syncthreads_and(ok);
-    if (threadIdx.x == 0) {
-        w.flag[0] = ok ? 1u : 0u;
-        w.hist[nfile] = 0;
-    }
+    if (threadIdx.x == 0) w.flag[0] = ok ? 1u : 0u;
 }
 
 // Probes are grouped block-locally first (LDS counters), so each workgroup
@@ -2119,11 +2149,14 @@ __global__ __launch_bounds__(256) void mc_prep_kernel(const uint8_t *img, const 
 __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint8_t *img, uint32_t nfile,
                                                                       const uint8_t *keys,
                                                                       const uint64_t *koff,
-                                                                      uint64_t nkeys, McWs w,
+                                                                      uint64_t k_begin, uint64_t nkeys,
+                                                                      McWs w, uint32_t nwg,
                                                                       uint8_t *hit) {
     __shared__ uint4 slo[kMcMaxFiles], shi[kMcMaxFiles];
     __shared__ uint32_t lh[kMcMaxFiles];
+    __shared__ uint32_t part[kMcGroupThreads];
     if (!w.flag[0]) return;
+    const uint32_t t = threadIdx.x;
     for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads) {
         const McFile &F = w.files[f];
         slo[f] = make_uint4(F.lo[0], F.lo[1], F.lo[2], F.lo[3]);
@@ -2135,19 +2168,19 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
     uint64_t k0[kMcGroupPer], kl[kMcGroupPer], f0[kMcGroupPer], f1[kMcGroupPer];
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + t;
         k0[p] = i < nkeys ? koff[i] : 0;
         kl[p] = i < nkeys ? koff[i + 1] - k0[p] : 0;
     }
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + t;
         f0[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p]) : 0;
         f1[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p] + 8) : 0;
     }
     {   // the workgroup's rows of the hit matrix start at 0 (16-byte stores
         // while the key loads are in flight)
-        const uint64_t r0 = (uint64_t)blockIdx.x * kMcGroupProbes;
+        const uint64_t r0 = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes;
         const uint64_t r1 = r0 + kMcGroupProbes < nkeys ? r0 + kMcGroupProbes : nkeys;
         uint8_t *z = hit + r0 * nfile;
         const uint64_t nz = (r1 - r0) * nfile;
@@ -2171,9 +2204,13 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
         kw[p][3] = __builtin_bswap32((uint32_t)(f1[p] >> 32));
     }
     __syncthreads();
+    uint32_t cand[kMcGroupPer], rank[kMcGroupPer];
+    uint64_t hh[kMcGroupPer][4];
+#pragma unroll
+    for (uint32_t p = 0; p < kMcGroupPer; p++) cand[p] = kMcNone;
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + t;
         if (i >= nkeys) break;
         const uint8_t *kp = keys + k0[p];
         uint32_t lo = 0, hi = nfile;  // first file with MinKey > key
@@ -2189,7 +2226,6 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
             if (c <= 0) lo = mid + 1;
             else hi = mid;
         }
-        uint32_t c = kMcNone;
         if (lo > 0) {
             const uint4 v = shi[lo - 1];
             const uint32_t bw[4] = {v.x, v.y, v.z, v.w};
@@ -2198,81 +2234,52 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
                 const McFile &F = w.files[lo - 1];
                 r = bound_cmp(bw, F.hi_len, img + F.hi_at, kw[p], kl[p], kp);
             }
-            if (r >= 0) {
-                c = lo - 1;
-                atomicAdd(&lh[c], 1u);
-                uint64_t h[4];  // only candidates are ever tested
-                sum256_pre(kp, kl[p], f0[p], f1[p], h);
-                const McFile &F = w.files[c];
-                if (lv_compact(F)) {  // 16 bytes, and no modulo in the test
-                    store_hash_rec(h, (uint32_t)F.m, (uint32_t)F.mr, (uint32_t)(F.mr >> 32),
-                                   reinterpret_cast<uint32_t *>(w.rec + i));
-                } else {
-                    for (int j = 0; j < 4; j++) w.hash[4 * i + j] = h[j];
-                }
+            if (r >= 0) {  // only candidates are ever tested
+                cand[p] = lo - 1;
+                rank[p] = atomicAdd(&lh[lo - 1], 1u);
+                sum256_pre(kp, kl[p], f0[p], f1[p], hh[p]);
             }
         }
-        w.cand[i] = c;
     }
     __syncthreads();
-    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads)
-        if (lh[f]) atomicAdd(&w.hist[f], lh[f]);
-}
-
-__global__ __launch_bounds__(kMcGroupThreads) void mc_scatter_kernel(uint32_t nfile, uint64_t nkeys, McWs w,
-                                                                     uint8_t *hit) {
-    __shared__ uint32_t lh[kMcMaxFiles], loff[kMcMaxFiles], part[kMcGroupThreads];
-    if (!w.flag[0]) return;
-    // The files' list offsets: every workgroup scans the <= 2,048 candidate
-    // counts itself (no separate offsets launch); workgroup 0 publishes them
-    // for mc_test_kernel.
-    constexpr uint32_t kPer = kMcMaxFiles / kMcGroupThreads;
-    const uint32_t t = threadIdx.x;
-    uint32_t cv[kPer], sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t f = t * kPer + j;
-        cv[j] = f < nfile ? w.hist[f] : 0u;
-        sum += cv[j];
-    }
-    part[t] = sum;
+    // the workgroup's candidates grouped by file into its slots, as the level
+    // search's classify does: exclusive scan of the per-file counts (<= 2,048
+    // files, 2 per thread), the file-major grid, then the ids and records
+    const uint32_t c0 = 2 * t < nfile ? lh[2 * t] : 0u, c1 = 2 * t + 1 < nfile ? lh[2 * t + 1] : 0u;
+    part[t] = c0 + c1;
     __syncthreads();
-    for (uint32_t d = 1; d < kMcGroupThreads; d <<= 1) {  // inclusive scan in LDS
+    for (uint32_t d = 1; d < kMcGroupThreads; d <<= 1) {
         const uint32_t x = t >= d ? part[t - d] : 0u;
         __syncthreads();
         part[t] += x;
         __syncthreads();
     }
-    uint32_t ex = part[t] - sum;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t f = t * kPer + j;
-        if (f < nfile) {
-            loff[f] = ex;
-            lh[f] = 0;
-            if (blockIdx.x == 0) w.off[f] = ex;
-        }
-        ex += cv[j];
+    const uint32_t ex = part[t] - c0 - c1;
+    __syncthreads();  // every lh read before it is overwritten with offsets
+    if (2 * t < nfile) {
+        lh[2 * t] = ex;
+        w.lv.grid[(uint64_t)(2 * t) * nwg + blockIdx.x] = ex;
+        w.lv.cnt[(uint64_t)(2 * t) * nwg + blockIdx.x] = c0;
     }
-    if (blockIdx.x == 0 && t == kMcGroupThreads - 1) w.off[nfile] = part[t];
-    __syncthreads();
-    uint32_t c[kMcGroupPer], rk[kMcGroupPer];
-#pragma unroll
-    for (uint32_t p = 0; p < kMcGroupPer; p++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
-        c[p] = i < nkeys ? w.cand[i] : kMcNone;
-        rk[p] = c[p] != kMcNone ? atomicAdd(&lh[c[p]], 1u) : 0;
+    if (2 * t + 1 < nfile) {
+        lh[2 * t + 1] = ex + c0;
+        w.lv.grid[(uint64_t)(2 * t + 1) * nwg + blockIdx.x] = ex + c0;
+        w.lv.cnt[(uint64_t)(2 * t + 1) * nwg + blockIdx.x] = c1;
     }
-    __syncthreads();
-    for (uint32_t f = threadIdx.x; f < nfile; f += kMcGroupThreads)
-        if (lh[f]) lh[f] = loff[f] + atomicAdd(&w.cursor[f], lh[f]);
     __syncthreads();
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
-        const uint64_t i = (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + threadIdx.x;
-        if (c[p] != kMcNone) {
-            w.list[lh[c[p]] + rk[p]] = (uint32_t)i;
-            hit[i * nfile + c[p]] = 1;
+        if (cand[p] == kMcNone) continue;
+        const uint64_t i = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes + p * kMcGroupThreads + t;
+        const uint64_t slot = (uint64_t)blockIdx.x * kMcGroupProbes + lh[cand[p]] + rank[p];
+        w.lv.ids[slot] = (uint32_t)(i - k_begin);
+        const McFile &F = w.files[cand[p]];
+        if (lv_compact(F)) {  // 16 bytes, and no modulo in the test
+            store_hash_rec(hh[p], (uint32_t)F.m, (uint32_t)F.mr, (uint32_t)(F.mr >> 32),
+                           reinterpret_cast<uint32_t *>(w.lv.rec + slot));
+        } else {
+            *(gptr_t<u64x2>)gbl(w.lv.rec + slot) = u64x2{hh[p][0], hh[p][1]};
+            *(gptr_t<u64x2>)gbl(w.lv.ext + slot) = u64x2{hh[p][2], hh[p][3]};
         }
     }
 }
@@ -2357,94 +2364,6 @@ __device__ __forceinline__ uint32_t filter_test_rec(const McFile &F, const HashR
     return bits;
 }
 
-// One workgroup per file: the first kMcLdsBytes of the stored filter words
-// go to LDS (all loads in flight), the rest (a 1.6M-bit filter is 200 KB) is
-// read from L2, where the workgroup's repeated touches keep it.  Each probe's
-// k locations are computed once; a probe whose bit is clear stores 0 over the
-// 1 the scatter wrote.  The hashes of the first probes are loaded before the
-// LDS fill.
-__global__ __launch_bounds__(kMcTestThreads) void mc_test_kernel(const uint8_t *img, uint32_t nfile, McWs w,
-                                                                 uint8_t *hit) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
-    if (!w.flag[0]) return;
-    const uint32_t f = blockIdx.x;
-    const uint32_t b0 = w.off[f], b1 = w.off[f + 1];
-    if (b0 == b1) return;
-    const McFile F = w.files[f];
-    // lv_compact files: the probe's 16-byte hash record (classify), the
-    // locations rebuilt by additions; others: its sum256
-    const bool compact = lv_compact(F);
-    const uint32_t m32 = (uint32_t)F.m;
-    // 2^64 mod m for the record's carried steps
-    const uint32_t c64 = compact ? (mod_small(~0ull, m32, (uint32_t)F.mr, (uint32_t)(F.mr >> 32)) + 1) % m32 : 0u;
-    const u32x4 *hash4 = reinterpret_cast<const u32x4 *>(w.hash);
-    uint32_t t = b0 + threadIdx.x, i = 0;
-    u32x4 hx = {0, 0, 0, 0}, hy = {0, 0, 0, 0};
-    if (t < b1) {
-        i = w.list[t];
-        if (compact) {
-            hx = w.rec[i];
-        } else {
-            hx = hash4[2 * (uint64_t)i];
-            hy = hash4[2 * (uint64_t)i + 1];
-        }
-    }
-    // LDS holds the words from the 16-byte boundary below them: aligned
-    // 16-byte global->LDS loads (no VGPR staging, all in flight), each chunk
-    // holding at least one filter byte (no fault).  Lanes past the end load
-    // the last chunk again into LDS the filter does not use.
-    const uint8_t *src = img + F.words_at;
-    const uint64_t nb = 8 * (F.nbits / 64 + ((F.nbits & 63) != 0));
-    const uint32_t delta = (uint32_t)((uintptr_t)src & 15);
-    const uint64_t in_lds = nb < kMcLdsBytes - 16 ? nb : kMcLdsBytes - 16;  // bytes [0, in_lds)
-    const uint4 *src16 = reinterpret_cast<const uint4 *>(src - delta);
-    const uint32_t n16 = (uint32_t)((delta + in_lds + 15) / 16);
-    constexpr uint32_t kU = kMcLdsBytes / 16 / kMcTestThreads;
-    static_assert(kMcLdsBytes % (16 * kMcTestThreads) == 0, "whole rounds of 16-byte loads");
-    // 1 KiB wave chunks, the order rotated per file: the filters sit at the
-    // same offset of ~2 MB files, so unrotated fills hit the same channels
-    const uint32_t nwc = (n16 + kWave - 1) / kWave, wave = threadIdx.x / kWave;
-    const uint32_t rot = nwc ? (f * 37u) % nwc : 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) {
-        const uint32_t cl = u * (kMcTestThreads / kWave) + wave;
-        if (cl < nwc) {
-            const uint32_t c = cl + rot < nwc ? cl + rot : cl + rot - nwc;
-            const uint32_t xw = c * kWave, x = xw + (threadIdx.x & (kWave - 1));
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(src16 + (x < n16 ? x : n16 - 1)),
-                (__attribute__((address_space(3))) void *)(fbytes + 16 * xw), 16, 0, 0);
-        }
-    }
-    __asm__ __volatile__("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const uint8_t *lb = fbytes + delta;  // LDS
-    while (t < b1) {
-        const uint32_t tn = t + kMcTestThreads;
-        uint32_t in = 0;
-        u32x4 xn = {0, 0, 0, 0}, yn = {0, 0, 0, 0};
-        if (tn < b1) {  // next probe's hash in flight during this one's tests
-            in = w.list[tn];
-            if (compact) {
-                xn = w.rec[in];
-            } else {
-                xn = hash4[2 * (uint64_t)in];
-                yn = hash4[2 * (uint64_t)in + 1];
-            }
-        }
-        uint32_t r;
-        if (compact) {
-            r = filter_test_rec(F, unpack_hash_rec(hx, m32, c64), m32, lb, in_lds, src);
-        } else {
-            const uint64_t h[4] = {(uint64_t)hx.y << 32 | hx.x, (uint64_t)hx.w << 32 | hx.z,
-                                   (uint64_t)hy.y << 32 | hy.x, (uint64_t)hy.w << 32 | hy.z};
-            r = filter_test(F, h, lb, in_lds, src);
-        }
-        if (!r) hit[(uint64_t)i * nfile + f] = 0;
-        t = tn; i = in; hx = xn; hy = yn;
-    }
-}
-
 McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
     McWs w{};
     size_t at = 0;
@@ -2455,13 +2374,10 @@ McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) 
     };
     w.flag = reinterpret_cast<uint32_t *>(take(16));
     w.files = reinterpret_cast<McFile *>(take(sizeof(McFile) * (size_t)(nfile ? nfile : 1)));
-    w.hist = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
-    w.off = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
-    w.cursor = reinterpret_cast<uint32_t *>(take(4 * ((size_t)nfile + 1)));
-    w.cand = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
-    w.hash = reinterpret_cast<uint64_t *>(take(32 * (nkeys ? nkeys : 1)));
-    w.rec = reinterpret_cast<u32x4 *>(take(16 * (nkeys ? nkeys : 1)));
-    w.list = reinterpret_cast<uint32_t *>(take(4 * (nkeys ? nkeys : 1)));
+    size_t lt = 0;
+    w.lv = lv_ws_layout(base ? base + at : nullptr, nfile, nkeys, &lt);
+    at += lt;
+    w.lv.files = w.files;
     if (total) *total = at;
     return w;
 }
@@ -2487,43 +2403,6 @@ McWs mc_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) 
 //    each probe's k bits tested there.
 // Tables beyond kLvMaxFiles take lv_probe_kernel (search over the table
 // list in global memory, bits read from the image).
-constexpr uint32_t kLvThreads = 1024;
-constexpr uint32_t kLvPer = 2;  // probes per thread
-constexpr uint32_t kLvProbes = kLvThreads * kLvPer;
-constexpr uint32_t kLvMaxFiles = 2048;
-constexpr uint32_t kLvMaxWgs = 1024;  // classify workgroups per pass (2M probes)
-
-struct LvWs {
-    McFile *files;
-    uint32_t *grid;   // [nfile][nwg]: the table's first slot in the workgroup
-    uint32_t *cnt;    // [nfile][nwg]: the table's probes in the workgroup
-    uint32_t *ids;    // [nwg * 2048] probe of each slot
-    u32x4 *rec;       // [nwg * 2048] its 16-byte hash record (lv_compact tables),
-                      // else h0, h1 of its sum256
-    u32x4 *ext;       // [nwg * 2048] h2, h3 (tables that are not lv_compact)
-};
-
-
-LvWs lv_ws_layout(uint8_t *base, uint32_t nfile, uint64_t nkeys, size_t *total) {
-    LvWs w{};
-    size_t at = 0;
-    auto take = [&](size_t bytes) -> uint8_t * {
-        uint8_t *p = base ? base + at : nullptr;
-        at += (bytes + 255) & ~(size_t)255;
-        return p;
-    };
-    const uint64_t pass = nkeys < (uint64_t)kLvMaxWgs * kLvProbes ? nkeys : (uint64_t)kLvMaxWgs * kLvProbes;
-    const uint64_t nwg = (pass + kLvProbes - 1) / kLvProbes;
-    const size_t nf = nfile ? nfile : 1;
-    w.files = reinterpret_cast<McFile *>(take(sizeof(McFile) * nf));
-    w.grid = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
-    w.cnt = reinterpret_cast<uint32_t *>(take(4 * nf * (nwg ? nwg : 1)));
-    w.ids = reinterpret_cast<uint32_t *>(take(4 * (nwg ? nwg : 1) * kLvProbes));
-    w.rec = reinterpret_cast<u32x4 *>(take(16 * (nwg ? nwg : 1) * kLvProbes));
-    w.ext = reinterpret_cast<u32x4 *>(take(16 * (nwg ? nwg : 1) * kLvProbes));
-    if (total) *total = at;
-    return w;
-}
 
 // The search view of table f: MinKey / MaxKey prefixes whenever the header
 // decoded (stage != 1); a table whose header did not decode searches as the
@@ -2709,13 +2588,18 @@ __device__ __forceinline__ uint64_t stage_filter(const uint8_t *src, uint64_t nb
 }
 
 
+// Matrix = false: the level search's may-bit per probe (may[k]); true: the
+// all-tables form's hit matrix (may[k * nfile + f], the rows zeroed by
+// mc_classify_kernel), run only when the grouped path holds (*flag).
+template <bool Matrix>
 __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
                                                              uint32_t nwg, LvWs w, uint64_t k_begin,
-                                                             uint8_t *may) {
+                                                             uint8_t *may, const uint32_t *flag) {
     extern __shared__ __attribute__((aligned(16))) uint8_t fbytes[];
     __shared__ uint32_t sb[kLvMaxWgs + 1];  // first probe of each workgroup's segment
     __shared__ uint32_t sg[kLvMaxWgs];      // its first slot in that workgroup
     __shared__ uint32_t part[kLvThreads];
+    if (Matrix && !flag[0]) return;
     const uint32_t f = blockIdx.x, t = threadIdx.x;
     // the table's segments: counts scanned (nwg <= 1,024: one per thread)
     const uint32_t c = t < nwg ? w.cnt[(uint64_t)f * nwg + t] : 0u;
@@ -2780,7 +2664,8 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
                                    (uint64_t)y.y << 32 | y.x, (uint64_t)y.w << 32 | y.z};
             r = filter_test(F, h, lb, in_lds, src);
         }
-        may[k_begin + id] = (uint8_t)r;
+        if (Matrix) may[(k_begin + id) * nfile + f] = (uint8_t)r;
+        else may[k_begin + id] = (uint8_t)r;
         q = qn;
         id = idn;
         x = xn;
@@ -3413,13 +3298,17 @@ extern "C" int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_
         LSM_HIP_CHECK(hipMemsetAsync(w.flag, 0, 4, s));
     } else {
         hipLaunchKernelGGL(mc_prep_kernel, dim3(1), dim3(256), 0, s, d_img, d_file_off, d_meta, nfile, w);
-        const uint32_t ggrid = (uint32_t)((nkeys + kMcGroupProbes - 1) / kMcGroupProbes);
-        hipLaunchKernelGGL(mc_classify_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, d_img,
-                           nfile, d_keys, d_koff, nkeys, w, d_hit);
-        hipLaunchKernelGGL(mc_scatter_kernel, dim3(ggrid), dim3(kMcGroupThreads), 0, s, nfile, nkeys, w,
-                           d_hit);
-        hipLaunchKernelGGL(mc_test_kernel, dim3(nfile), dim3(kMcTestThreads), kMcLdsBytes, s,
-                           d_img, nfile, w, d_hit);
+        // passes of up to 2M probes (the test kernel's segment table), as the
+        // level search runs them
+        const uint64_t pass = (uint64_t)kLvMaxWgs * kLvProbes;
+        for (uint64_t k0 = 0; k0 < nkeys; k0 += pass) {
+            const uint64_t n = nkeys - k0 < pass ? nkeys - k0 : pass;
+            const uint32_t nwg = (uint32_t)((n + kMcGroupProbes - 1) / kMcGroupProbes);
+            hipLaunchKernelGGL(mc_classify_kernel, dim3(nwg), dim3(kMcGroupThreads), 0, s, d_img, nfile,
+                               d_keys, d_koff, k0, k0 + n, w, nwg, d_hit);
+            hipLaunchKernelGGL(lv_test_kernel<true>, dim3(nfile), dim3(kLvThreads), kMcLdsBytes, s,
+                               d_img, nfile, nwg, w.lv, k0, d_hit, (const uint32_t *)w.flag);
+        }
     }
     const uint32_t pgrid = grid < kMcProbeGrid ? (uint32_t)grid : kMcProbeGrid;
     hipLaunchKernelGGL(may_contain_kernel, dim3(pgrid), dim3(kMcThreads), 0, s, d_img,
@@ -3453,8 +3342,8 @@ static int level_search(hipStream_t s, const uint8_t *d_img, const McFile *files
             const uint32_t nwg = (uint32_t)((n + kLvProbes - 1) / kLvProbes);
             hipLaunchKernelGGL(lv_classify_kernel, dim3(nwg), dim3(kLvThreads), 0, s, d_img, nfile,
                                d_keys, d_koff, k0, k0 + n, w, nwg, d_table, d_may);
-            hipLaunchKernelGGL(lv_test_kernel, dim3(nfile), dim3(kLvThreads), kMcLdsBytes, s, d_img,
-                               nfile, nwg, w, k0, d_may);
+            hipLaunchKernelGGL(lv_test_kernel<false>, dim3(nfile), dim3(kLvThreads), kMcLdsBytes, s,
+                               d_img, nfile, nwg, w, k0, d_may, nullptr);
         }
     }
     LSM_HIP_CHECK(hipGetLastError());

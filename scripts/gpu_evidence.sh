@@ -40,7 +40,7 @@ declare -A K A W
 K[sst]=sst_regions_kernel,bloom_or_kernel,bloom_file_kernel,sst_meta_kernel; A[sst]=sst_regions_kernel; W[sst]=sst:208
 K[mixed]=sched_hist_kernel,sched_scatter_kernel,decode_v2_kernel; A[mixed]=decode_v2_kernel; W[mixed]=mixed:37450:desc
 K[sstdec]=sst_index_kernel,sst_tail_kernel; A[sstdec]=sst_tail_kernel; W[sstdec]=sstdec:208
-K[probe]=mc_prep_kernel,mc_classify_kernel,mc_scatter_kernel,mc_test_kernel,may_contain_kernel; A[probe]=mc_prep_kernel; W[probe]=probe:208:1048576
+K[probe]=mc_prep_kernel,mc_classify_kernel,lv_test_kernel,may_contain_kernel; A[probe]=mc_prep_kernel; W[probe]=probe:208:1048576
 K[wal]=wal_seg_lanes_kernel,wal_stitch_kernel,wal_compact_kernel; A[wal]=wal_stitch_kernel; W[wal]=wal:64:desc
 K[level]=lv_classify_kernel,lv_test_kernel; A[level]=lv_classify_kernel; W[level]=level:208:1048576
 K[get]=lv_classify_kernel,lv_test_kernel,level_get_kernel; A[get]=lv_classify_kernel; W[get]=get:208:1048576
