@@ -2178,19 +2178,6 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
         f0[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p]) : 0;
         f1[p] = i < nkeys ? ldg_u64_unaligned(keys + k0[p] + 8) : 0;
     }
-    {   // the workgroup's rows of the hit matrix start at 0 (16-byte stores
-        // while the key loads are in flight)
-        const uint64_t r0 = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes;
-        const uint64_t r1 = r0 + kMcGroupProbes < nkeys ? r0 + kMcGroupProbes : nkeys;
-        uint8_t *z = hit + r0 * nfile;
-        const uint64_t nz = (r1 - r0) * nfile;
-        const uint64_t head = ((16 - ((uintptr_t)z & 15)) & 15) < nz ? ((16 - ((uintptr_t)z & 15)) & 15) : nz;
-        const uint64_t n16 = (nz - head) / 16, tail = head + 16 * n16;
-        if (threadIdx.x < head) z[threadIdx.x] = 0;
-        uint4 *z16 = reinterpret_cast<uint4 *>(z + head);
-        for (uint64_t x = threadIdx.x; x < n16; x += kMcGroupThreads) z16[x] = make_uint4(0, 0, 0, 0);
-        if (tail + threadIdx.x < nz) z[tail + threadIdx.x] = 0;
-    }
     uint32_t kw[kMcGroupPer][4];
 #pragma unroll
     for (uint32_t p = 0; p < kMcGroupPer; p++) {
@@ -2240,6 +2227,40 @@ __global__ __launch_bounds__(kMcGroupThreads) void mc_classify_kernel(const uint
                 sum256_pre(kp, kl[p], f0[p], f1[p], hh[p]);
             }
         }
+    }
+    {   // the workgroup's rows of the hit matrix, written once: 0 except the
+        // candidate's 1 (the test clears it when a bit is 0), 16-byte stores;
+        // the candidates through LDS (the scan's row, free until the scan)
+        uint16_t *scand = reinterpret_cast<uint16_t *>(part);
+#pragma unroll
+        for (uint32_t p = 0; p < kMcGroupPer; p++)
+            scand[p * kMcGroupThreads + t] = cand[p] == kMcNone ? (uint16_t)0xFFFFu : (uint16_t)cand[p];
+        __syncthreads();
+        const uint64_t r0 = k_begin + (uint64_t)blockIdx.x * kMcGroupProbes;
+        const uint64_t r1 = r0 + kMcGroupProbes < nkeys ? r0 + kMcGroupProbes : nkeys;
+        uint8_t *z = hit + r0 * nfile;
+        const uint32_t nz = (uint32_t)((r1 - r0) * nfile);  // <= 2,048 rows x 2,048 files
+        const uint32_t mis = (uint32_t)((uintptr_t)z & 15);
+        const uint32_t head = ((16 - mis) & 15) < nz ? ((16 - mis) & 15) : nz;
+        const uint32_t n16 = (nz - head) / 16, tail = head + 16 * n16;
+        auto one_at = [&](uint32_t o) -> uint32_t {  // byte o of the rows: the candidate's 1
+            const uint32_t row = o / nfile;
+            const uint32_t c = scand[row];
+            return c != 0xFFFFu && row * nfile + c == o ? 1u : 0u;
+        };
+        if (t < head) z[t] = (uint8_t)one_at(t);
+        u32x4 *z16 = reinterpret_cast<u32x4 *>(z + head);
+        for (uint32_t x = t; x < n16; x += kMcGroupThreads) {
+            const uint32_t o = head + 16 * x;
+            uint32_t wd[4] = {0, 0, 0, 0};
+            for (uint32_t row = o / nfile; row * nfile < o + 16; row++) {
+                const uint32_t c = scand[row];
+                const uint32_t at = row * nfile + c;
+                if (c != 0xFFFFu && at >= o && at < o + 16) wd[(at - o) >> 2] |= 1u << (8 * ((at - o) & 3));
+            }
+            z16[x] = u32x4{wd[0], wd[1], wd[2], wd[3]};
+        }
+        if (tail + t < nz) z[tail + t] = (uint8_t)one_at(tail + t);
     }
     __syncthreads();
     // the workgroup's candidates grouped by file into its slots, as the level
@@ -2589,8 +2610,9 @@ __device__ __forceinline__ uint64_t stage_filter(const uint8_t *src, uint64_t nb
 
 
 // Matrix = false: the level search's may-bit per probe (may[k]); true: the
-// all-tables form's hit matrix (may[k * nfile + f], the rows zeroed by
-// mc_classify_kernel), run only when the grouped path holds (*flag).
+// all-tables form's hit matrix (may[k * nfile + f]; mc_classify_kernel wrote
+// the rows with each candidate's 1, the test clears the candidates whose bit
+// is 0), run only when the grouped path holds (*flag).
 template <bool Matrix>
 __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
                                                              uint32_t nwg, LvWs w, uint64_t k_begin,
@@ -2664,7 +2686,9 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
                                    (uint64_t)y.y << 32 | y.x, (uint64_t)y.w << 32 | y.z};
             r = filter_test(F, h, lb, in_lds, src);
         }
-        if (Matrix) may[(k_begin + id) * nfile + f] = (uint8_t)r;
+        if (Matrix) {
+            if (!r) may[(k_begin + id) * nfile + f] = 0;  // classify wrote the 1
+        }
         else may[k_begin + id] = (uint8_t)r;
         q = qn;
         id = idn;
