@@ -2535,10 +2535,8 @@ __global__ __launch_bounds__(kLvThreads) void lv_classify_kernel(const uint8_t *
                 test = r >= 0;
             }
         }
-        if (!test) {
-            may[i] = 0;
-            continue;
-        }
+        may[i] = test ? 1 : 0;  // the test clears a candidate whose bit is 0
+        if (!test) continue;
         cand[p] = idx;
         rank[p] = atomicAdd(&lh[idx], 1u);
         sum256_pre(kp, kl[p], f0[p], f1[p], hh[p]);
@@ -2610,9 +2608,9 @@ __device__ __forceinline__ uint64_t stage_filter(const uint8_t *src, uint64_t nb
 
 
 // Matrix = false: the level search's may-bit per probe (may[k]); true: the
-// all-tables form's hit matrix (may[k * nfile + f]; mc_classify_kernel wrote
-// the rows with each candidate's 1, the test clears the candidates whose bit
-// is 0), run only when the grouped path holds (*flag).
+// all-tables form's hit matrix (may[k * nfile + f]), run only when the grouped
+// path holds (*flag).  Either way classify wrote each candidate's 1 and the
+// test clears the candidates whose bit is 0.
 template <bool Matrix>
 __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img, uint32_t nfile,
                                                              uint32_t nwg, LvWs w, uint64_t k_begin,
@@ -2689,7 +2687,7 @@ __global__ __launch_bounds__(kLvThreads) void lv_test_kernel(const uint8_t *img,
         if (Matrix) {
             if (!r) may[(k_begin + id) * nfile + f] = 0;  // classify wrote the 1
         }
-        else may[k_begin + id] = (uint8_t)r;
+        else if (!r) may[k_begin + id] = 0;
         q = qn;
         id = idn;
         x = xn;
