@@ -65,23 +65,25 @@ def bench_sst(args, world, rank, local):
     (keys, koff, vals, voff), starts, mine, nf_all, rule_ms = sst_deal(args, world, rank)
     n = len(koff) - 1
     batch = lsmgpu.batch_to_device(ctx, keys, koff, vals, voff)
-    # the builder rule (builder.go:34-59: EstimateSize sums, flush at 2 MiB)
-    # and the image layout run on the host once per stream; their cost is
-    # reported next to the line (builder_rule_ms)
-    tb1 = time.perf_counter()
-    sb = lsmgpu.prepare_sst(ctx, batch, starts)
-    torch.cuda.synchronize()
-    tb2 = time.perf_counter()
+    # One step = the whole builder path over this rank's stream as one call
+    # (lsm_build_sst_stream): the builder rule on the device (builder.go:34-42
+    # as merge.go:106-128 drives it), the image layout, then the images with
+    # the fused bloom -- sized on host-known bounds, nothing read back.
+    ss = lsmgpu.prepare_sst_stream(ctx, batch, lsmgpu.MAX_SSTABLE_SIZE)
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
-        lsmgpu.build_sst_into(ctx, batch, sb, stream=stream)
+        lsmgpu.build_sst_stream_into(ctx, batch, ss, stream=stream)
     torch.cuda.synchronize()
 
     def step():
-        lsmgpu.build_sst_into(ctx, batch, sb, stream=stream)
+        lsmgpu.build_sst_stream_into(ctx, batch, ss, stream=stream)
 
     elapsed = timed_region(world, step, args.steps)
     times, kern_ms = kernel_times(step, stream, args.steps)
+    sb = ss.result()
+    # the device rule cut this rank's stream into exactly the files dealt to it
+    if not np.array_equal(sb.file_start, starts):
+        raise SystemExit("bench_sst: the device builder rule disagrees with the host rule")
     img = float(sb.file_size.astype(np.float64).sum())
     img_all = sum_over_ranks(world, img)
     nf = len(starts) - 1
@@ -109,12 +111,16 @@ def bench_sst(args, world, rank, local):
                                f"(16 B / 100 B) into {nf_all} .sst (2 MiB flush, bloom m=1.6M "
                                f"k=16), whole files dealt round-robin over {world} GPU(s)",
                    "files_total": nf_all, "files_rank0": nf, "image_bytes_rank0": int(img),
-                   "builder_rule_ms": round(rule_ms, 3),
-                   "layout_ms": round((tb2 - tb1) * 1e3, 3),
-                   "builder_rule": "lsm_segment_files_host (O(files log n) host search over the "
-                                   "CSR offsets), outside the timed region; layout incl. H2D",
+                   "step": "lsm_build_sst_stream: the builder rule (device), the layout and the "
+                           "images in one call, no host round trip",
+                   "deal_rule_ms": round(rule_ms, 3),
+                   "deal": "the host rule cuts the global stream to deal whole files over the "
+                           "ranks (outside the timed region); each rank's device rule re-derives "
+                           "its files inside the step",
                    "parallelism": f"dp{world} (file f -> rank f mod {world}, no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "lsm_build_sst: sst_regions_kernel (regions + key hash) -> bloom_or_kernel (filter bits + framing)",
+        "roofline": {"bound": "hbm", "kernel": "lsm_build_sst_stream: sst_stream_plan_kernel (rule + layout) -> "
+                                               "sst_regions_kernel (regions + key hash) -> bloom_or_kernel "
+                                               "(filter bits + framing)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": tsrc,
@@ -126,7 +132,8 @@ def bench_sst(args, world, rank, local):
         out["roofline"]["aggregate"] = aggregate_roofline(world, alg, kern_ms)
     if not args.no_verify:
         verify_sst(ctx, batch, sb, keys, koff)
-    out["config"]["verified"] = False if args.no_verify else ("every image parsed by lsm_decode_sst, V/IDX regions equal to the "
+    out["config"]["verified"] = False if args.no_verify else ("device file starts equal the host rule's; "
+                                 "every image parsed by lsm_decode_sst, V/IDX regions equal to the "
                                  "input, every 16th key present in its file's filter")
     return out, (keys, koff, vals, voff, starts, sb.file_size)
 

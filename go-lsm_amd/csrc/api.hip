@@ -11,6 +11,11 @@ extern "C" int lsm_input_slack(void) { return LSM_INPUT_SLACK; }
 #endif
 // hash of the sources this library was compiled from (go-lsm_amd/build_id.py)
 extern "C" const char *lsm_build_id(void) { return LSM_BUILD_ID; }
+#ifndef LSM_BUILD_FLAGS
+#define LSM_BUILD_FLAGS ""
+#endif
+// "HIPCC|ARCH|HIPFLAGS" the library was compiled with (part of the build id)
+extern "C" const char *lsm_build_flags(void) { return LSM_BUILD_FLAGS; }
 
 extern "C" int lsm_ctx_create(int device, lsm_ctx **out) {
     if (!out) return LSM_EINVAL;

@@ -913,6 +913,7 @@ struct BloomOrArgs {
     const uint64_t *koff;
     uint8_t *out;
     const uint64_t *file_off;
+    const uint64_t *dnf;  // the stream build: the file count on the device (nfiles bounds it)
 };
 
 // ---- .sst image writer ------------------------------------------------------
@@ -933,6 +934,21 @@ struct SstArgs {
     // key (store_hash_rec, key file_start[0] first), or null
     uint32_t *hrec;
     uint32_t hm, hrl, hrh;
+    // the stream build (lsm_build_sst_stream): the region writer's grid is one
+    // dimension of 128-record spans, span j of file span_file[j], whose
+    // layout is desc[span_file[j]] (written by sst_stream_plan_kernel); null
+    // for the file-major grid of lsm_build_sst
+    const uint32_t *span_file;
+    const struct FileDesc *desc;
+};
+
+// One file of a stream build, as the plan kernel lays it out: records
+// [s, e), the image at out + img, its V / IDX regions at data_off / idx_off
+// inside it, Ks = koff[s], Vs = voff[s], and its first span in the region
+// writer's grid.  64 bytes: one scalar load of 16 dwords.
+struct FileDesc {
+    uint64_t s, e, img, data_off, idx_off, Ks, Vs;
+    uint32_t span0, pad;
 };
 
 struct SstLayout {
@@ -1201,21 +1217,44 @@ __device__ __forceinline__ void region_finish(const RegionPlan &R, uint32_t *buf
 // per wave, so a CU holds twice the waves (compaction 1.031-1.037 -> 1.018 ms
 // per call, A/B; the data region straight from the values arena without the
 // LDS image measured 0.250 -> 0.332 ms per config-3 build and is not used).
-template <bool WithV>
+// Desc (the stream build): the grid is one dimension of spans and each file's
+// layout comes precomputed in one 64-byte FileDesc (two dependent scalar
+// loads per wave instead of sst_layout's eight loads and its 64-bit
+// arithmetic: a wave writes one chunk, so this setup is paid per chunk).
+template <bool WithV, bool Desc>
 __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a) {
     constexpr uint32_t BD = WithV ? kRegBufDwords : kRegIdxDwords;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kRegWaves][BD + kGatherMaskWords];
-    const uint32_t f = blockIdx.x;
-    const SstLayout L = sst_layout(a, f);
     const uint32_t wave = uni(threadIdx.x / kWave);
-    uint64_t c0 = L.s + (uint64_t)blockIdx.y * kRegSpanRecs + (uint64_t)wave * kRegWaveChunks * kWave;
+    SstLayout L;
+    uint64_t c0, imgo, Ks, Vs, K0;
+    if (Desc) {
+        const uint32_t f = a.span_file[blockIdx.x];
+        if (f == ~0u) return;
+        const FileDesc D = a.desc[f];
+        L.s = D.s;
+        L.e = D.e;
+        L.data_off = D.data_off;
+        L.idx_off = D.idx_off;
+        c0 = D.s + (uint64_t)(blockIdx.x - D.span0) * kRegSpanRecs + (uint64_t)wave * kRegWaveChunks * kWave;
+        imgo = D.img;
+        Ks = D.Ks;
+        Vs = D.Vs;
+        K0 = 0;  // the stream starts at record 0
+    } else {
+        const uint32_t f = blockIdx.x;
+        L = sst_layout(a, f);
+        c0 = L.s + (uint64_t)blockIdx.y * kRegSpanRecs + (uint64_t)wave * kRegWaveChunks * kWave;
+        imgo = uni64(a.file_off[f]);
+        Ks = uni64(a.koff[L.s]);
+        Vs = uni64(a.voff[L.s]);
+        K0 = a.hrec ? uni64(a.file_start[0]) : 0;
+    }
     if (c0 >= L.e) return;
     const uint64_t cend = L.e - c0 < (uint64_t)kRegWaveChunks * kWave ? L.e : c0 + kRegWaveChunks * kWave;
     uint32_t *buf = lds[wave];
     uint32_t *mask = buf + BD;
-    uint8_t *img = a.out + uni64(a.file_off[f]);
-    const uint64_t Ks = uni64(a.koff[L.s]), Vs = uni64(a.voff[L.s]);
-    const uint64_t K0 = a.hrec ? uni64(a.file_start[0]) : 0;
+    uint8_t *img = a.out + imgo;
     auto count = [&](uint64_t c) { return (uint32_t)(cend - c < (uint64_t)kWave ? cend - c : kWave); };
     ChunkOffs off = load_offs(a, c0, count(c0));
     for (;;) {
@@ -1278,6 +1317,343 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
         }
         if (!more) break;
         c0 = cn;
+    }
+}
+
+// ---- builder rule on the device (lsm_segment_files / lsm_build_sst_stream) --
+//
+// Builder.Add sums EstimateSize = 16 + key + value bytes (kv.go:118-121) and
+// the driver flushes once the sum reaches the threshold (builder.go:40-42,
+// merge.go:118-121); the leftovers make a last file (merge.go:125-128).
+// With S(t) = 16 t + koff[t] + voff[t] (strictly increasing), the file after
+// a file starting at s starts at next(s) = the smallest t in (s, n] with
+// S(t) - S(s) >= T, or n when no t reaches it.  The starts are the orbit of 0
+// under next(), a serial chain; one workgroup resolves it in rounds:
+//  * from the exact start `cur`, slot i of the round predicts file i's start
+//    at cur + i G (G = the records per file seen so far) and computes next()
+//    there exactly (a galloping search seeded at the prediction + G: one
+//    round trip when the prediction holds);
+//  * W = 1 (1,024 slots): slot i is verified when every earlier slot's next()
+//    equals the following slot's prediction (a min-reduction finds the first
+//    break; for records of one size every prediction holds and one round
+//    resolves every file);
+//  * W = 32 (32 slots of 32 window positions): after a break, positions
+//    around each prediction, and one thread walks the chain through the
+//    windows; a full walk returns to W = 1.
+// Every file start written is exact: a slot's next() is only used once the
+// slot's own position is known to be a start.  Then, in the same launch, the
+// image layout (sizes, 16-byte aligned offsets, lsm_sst_layout's) and, for
+// the build, each file's FileDesc and the span table of the region writer.
+constexpr uint32_t kSegThreads = 1024;
+constexpr uint32_t kSegWin = 32;
+constexpr uint32_t kSegLdsFiles = 4096;  // file starts kept in LDS for the layout
+constexpr uint64_t kSegNone = ~0ull;
+
+struct StreamPlanArgs {
+    const uint64_t *koff, *voff;
+    uint64_t n, T;
+    uint32_t nfile_max, span_max;
+    uint64_t filter_bytes, align;
+    uint64_t *file_start;  // nfile_max + 1
+    uint64_t *file_off;    // nfile_max + 1, or null (the rule alone)
+    FileDesc *desc;        // nfile_max, or null
+    uint32_t *span_file;   // span_max, or null
+    uint64_t *counts;      // {nfile, most records in a file, image bytes, overflow}
+};
+
+struct SegPair {
+    uint64_t s, c;
+};
+
+// Exclusive sums of two values over the plan kernel's 1,024 threads.
+__device__ __forceinline__ SegPair seg_block_scan2(uint64_t s, uint64_t c, SegPair *total) {
+    constexpr uint32_t NW = kSegThreads / kWave;
+    __shared__ uint64_t ws_[NW], wc_[NW];
+    uint64_t ts, tc;
+    const uint64_t xs = wave_excl_scan64(s, &ts), xc = wave_excl_scan64(c, &tc);
+    const uint32_t w = threadIdx.x / kWave;
+    if (lane_id() == 0) {
+        ws_[w] = ts;
+        wc_[w] = tc;
+    }
+    __syncthreads();
+    uint64_t ps = 0, pc = 0, as = 0, ac = 0;
+    for (uint32_t i = 0; i < NW; i++) {
+        if (i < w) {
+            ps += ws_[i];
+            pc += wc_[i];
+        }
+        as += ws_[i];
+        ac += wc_[i];
+    }
+    __syncthreads();
+    *total = SegPair{as, ac};
+    return SegPair{ps + xs, pc + xc};
+}
+
+__device__ __forceinline__ uint64_t est_at(const uint64_t *koff, const uint64_t *voff, uint64_t t) {
+    return 16 * t + koff[t] + voff[t];
+}
+
+// next(p) for p < n with S(n) >= S(p) + T known: the smallest t in (p, n]
+// with S(t) >= target, searched from `guess` by galloping, then bisection.
+__device__ uint64_t seg_next(const uint64_t *koff, const uint64_t *voff, uint64_t p, uint64_t n,
+                             uint64_t target, uint64_t guess) {
+    uint64_t lo = p + 1, hi = n;  // the answer is in [lo, hi]; S(hi) >= target
+    const uint64_t g = guess < lo ? lo : (guess > hi ? hi : guess);
+    {
+        // S(g - 1) and S(g) in one round trip: the prediction holds when
+        // they bracket the target
+        const uint64_t a = g > lo ? est_at(koff, voff, g - 1) : 0;
+        const uint64_t b = est_at(koff, voff, g);
+        if (b >= target) {
+            if (g == lo || a < target) return g;
+            hi = g - 1;  // S(g - 1) >= target
+            uint64_t d = 1;
+            for (;;) {  // gallop down
+                const uint64_t x = hi - lo > d ? hi - d : lo;
+                if (est_at(koff, voff, x) >= target) {
+                    hi = x;
+                    if (x == lo) return lo;
+                    d <<= 1;
+                } else {
+                    lo = x + 1;
+                    break;
+                }
+            }
+        } else {
+            lo = g + 1;
+            uint64_t d = 1;
+            while (lo < hi) {  // gallop up
+                const uint64_t x = hi - lo > d ? lo + d - 1 : hi;
+                if (est_at(koff, voff, x) >= target) {
+                    hi = x;
+                    break;
+                }
+                lo = x + 1;
+                d <<= 1;
+            }
+        }
+    }
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (est_at(koff, voff, mid) >= target) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlanArgs a) {
+    __shared__ uint64_t s_pos[kSegThreads], s_nxt[kSegThreads];
+    __shared__ uint64_t s_fs[kSegLdsFiles + 1];  // the first file starts, for the layout
+    __shared__ uint64_t s_cur, s_G;
+    __shared__ uint32_t s_nf, s_W, s_brk, s_over;
+    __shared__ uint64_t s_carry, s_scarry, s_maxr;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t n = a.n, T = a.T;
+    // every thread reads the stream's ends itself (the same two lines: no
+    // round trip through thread 0 and a barrier)
+    const uint64_t Sn = n ? est_at(a.koff, a.voff, n) : 0;
+    const uint64_t S0 = n ? est_at(a.koff, a.voff, 0) : 0;
+    if (tid == 0) {
+        s_cur = 0;
+        s_nf = 0;
+        s_W = 1;
+        s_over = 0;
+        // records per file if every record had the mean size
+        const uint64_t tot = Sn - S0;
+        const double g = tot ? ceil((double)T * (double)n / (double)tot) : 1.0;
+        s_G = g < 1.0 ? 1 : (g > 4.0e18 ? (uint64_t)4e18 : (uint64_t)g);
+    }
+    __syncthreads();
+    if (n && T == 0) {  // never flush (BuildSSTableFromIMemTable): one file
+        if (tid == 0) {
+            if (a.nfile_max >= 1) {
+                a.file_start[0] = 0;
+                s_fs[0] = 0;
+                s_nf = 1;
+            } else {
+                s_over = 1;
+            }
+            s_cur = n;
+        }
+        __syncthreads();
+    }
+    for (;;) {
+        const uint64_t cur = s_cur;
+        const uint32_t nf = s_nf;
+        if (cur >= n || s_over) break;
+        const uint32_t W = s_W, R = kSegThreads / W;
+        const uint64_t G = s_G;
+        const uint32_t i = tid / W, w = tid % W;
+        uint64_t P = kSegNone;
+        if (i == 0) {
+            if (w == 0) P = cur;
+        } else {
+            const uint64_t c = cur + (uint64_t)i * G;  // may exceed n: no slot
+            const uint64_t h = W / 2;
+            if (c >= h && c - h + w > cur && c - h + w < n) P = c - h + w;
+        }
+        uint64_t nx = kSegNone;
+        if (P != kSegNone) {
+            // S(P) and the predicted end's bracket S(g - 1), S(g) in one
+            // round trip (T > 0 here, so S(P) < target: g = P + 1 is covered)
+            const uint64_t g = P + G < n ? P + G : n;
+            const uint64_t sp = est_at(a.koff, a.voff, P);
+            const uint64_t sa = est_at(a.koff, a.voff, g - 1), sb = est_at(a.koff, a.voff, g);
+            const uint64_t target = sp + T;
+            nx = Sn < target ? n : (sb >= target && sa < target ? g : seg_next(a.koff, a.voff, P, n, target, g));
+        }
+        s_pos[tid] = P;
+        s_nxt[tid] = nx;
+        if (tid == 0) s_brk = R - 1;
+        __syncthreads();
+        uint32_t adv = 0;  // files whose start this round resolved
+        uint64_t ncur = cur;
+        if (W == 1) {
+            // slot tid is the chain's last of this round if its next() is
+            // not slot tid + 1's prediction (or ends the stream)
+            if (tid < R - 1 && s_nxt[tid] != kSegNone &&
+                (s_nxt[tid] >= n || s_nxt[tid] != s_pos[tid + 1]))
+                atomicMin(&s_brk, tid);
+            if (tid < R - 1 && s_nxt[tid] == kSegNone) atomicMin(&s_brk, tid);
+            __syncthreads();
+            const uint32_t J = s_brk;  // slots 0 .. J are starts; slot J's next() is exact
+            adv = J + 1;
+            ncur = s_nxt[J];
+            if (nf + adv > a.nfile_max) {
+                if (tid == 0) s_over = 1;
+            } else if (tid <= J) {
+                a.file_start[nf + tid] = s_pos[tid];
+                if (nf + tid <= kSegLdsFiles) s_fs[nf + tid] = s_pos[tid];
+            }
+        } else {
+            if (tid == 0) {
+                uint64_t c = cur;
+                uint32_t k = nf;
+                for (uint32_t j = 0; j < R && c < n; j++) {
+                    uint64_t x = kSegNone;
+                    if (j == 0) {
+                        x = s_nxt[0];
+                    } else {
+                        const uint64_t lo = cur + (uint64_t)j * G - W / 2;
+                        if (cur + (uint64_t)j * G >= W / 2 && c >= lo && c - lo < W) x = s_nxt[j * W + (c - lo)];
+                    }
+                    if (x == kSegNone) break;  // c is a start, next(c) not in the window
+                    if (k >= a.nfile_max) {
+                        s_over = 1;
+                        break;
+                    }
+                    if (k <= kSegLdsFiles) s_fs[k] = c;
+                    a.file_start[k++] = c;
+                    c = x;
+                }
+                s_brk = k - nf;
+                s_pos[0] = c;
+            }
+            __syncthreads();
+            adv = s_brk;
+            ncur = s_pos[0];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (adv) {
+                const uint64_t g = (ncur - cur + adv / 2) / adv;  // mean records per file
+                s_G = g ? g : 1;
+            }
+            s_W = (W == 1 && adv < R && ncur < n) ? kSegWin : (W > 1 && adv == R ? 1 : W);
+            s_cur = ncur;
+            s_nf = nf + adv;
+        }
+        __syncthreads();
+    }
+    const uint32_t nfile = s_over ? 0 : s_nf;
+    if (tid == 0) {
+        a.file_start[nfile] = n;
+        if (nfile <= kSegLdsFiles) s_fs[nfile] = n;
+        a.counts[0] = nfile;
+        a.counts[3] = s_over;
+        s_carry = 0;
+        s_scarry = 0;
+        s_maxr = 0;
+    }
+    __syncthreads();
+    if (!a.file_off) {
+        // the rule alone: the most records in one file
+        uint64_t mr = 0;
+        for (uint32_t f = tid; f < nfile; f += kSegThreads) {
+            const uint64_t r = (f + 1 <= kSegLdsFiles ? s_fs[f + 1] : a.file_start[f + 1]) -
+                               (f <= kSegLdsFiles ? s_fs[f] : a.file_start[f]);
+            mr = r > mr ? r : mr;
+        }
+        __syncthreads();
+        if (mr) atomicMax((unsigned long long *)&s_maxr, (unsigned long long)mr);
+        __syncthreads();
+        if (tid == 0) {
+            a.counts[1] = s_maxr;
+            a.counts[2] = 0;
+        }
+        return;
+    }
+    __syncthreads();
+    // layout: sizes, aligned offsets, FileDesc, span starts (tile after tile)
+    __shared__ uint32_t s_span0[kSegThreads + 1];
+    for (uint32_t f0 = 0; f0 < nfile; f0 += kSegThreads) {
+        const uint32_t f = f0 + tid;
+        uint64_t sz = 0, nr = 0, r0 = 0, r1 = 0, k0 = 0, k1 = 0, v0 = 0, v1 = 0, hdr = 8;
+        if (f < nfile) {
+            r0 = f <= kSegLdsFiles ? s_fs[f] : a.file_start[f];
+            r1 = f + 1 <= kSegLdsFiles ? s_fs[f + 1] : a.file_start[f + 1];
+            nr = r1 - r0;
+            k0 = a.koff[r0];
+            k1 = a.koff[r1];
+            v0 = a.voff[r0];
+            v1 = a.voff[r1];
+            hdr += (a.koff[r0 + 1] - k0) + (k1 - a.koff[r1 - 1]);  // nr >= 1
+            // Header | Filter | V region (4 + vlen) | IDX region (4 + klen + 8) | Footer
+            sz = hdr + a.filter_bytes + 4 * nr + (v1 - v0) + 12 * nr + (k1 - k0) + 32;
+        }
+        const uint64_t nsp = (nr + kRegSpanRecs - 1) / kRegSpanRecs;
+        SegPair tot;
+        const SegPair x = seg_block_scan2((sz + a.align - 1) / a.align * a.align, nsp, &tot);
+        if (f < nfile) {
+            const uint64_t off = s_carry + x.s;
+            a.file_off[f] = off;
+            FileDesc D;
+            D.s = r0;
+            D.e = r1;
+            D.img = off;
+            D.data_off = hdr + a.filter_bytes;
+            D.idx_off = D.data_off + 4 * nr + (v1 - v0);
+            D.Ks = k0;
+            D.Vs = v0;
+            D.span0 = (uint32_t)(s_scarry + x.c);
+            D.pad = 0;
+            a.desc[f] = D;
+            s_span0[tid] = D.span0;
+            atomicMax((unsigned long long *)&s_maxr, (unsigned long long)nr);
+        }
+        if (tid == 0) s_span0[min(kSegThreads, nfile - f0)] = (uint32_t)(s_scarry + tot.c);
+        __syncthreads();
+        // the span table, one wave per file (lane-strided stores)
+        const uint32_t wv = tid / kWave, nw = kSegThreads / kWave;
+        for (uint32_t g = wv; g < kSegThreads && f0 + g < nfile; g += nw) {
+            const uint32_t b0 = s_span0[g], b1 = s_span0[g + 1];
+            for (uint32_t j = b0 + lane_id(); j < b1; j += kWave) a.span_file[j] = f0 + g;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            s_carry += tot.s;
+            s_scarry += tot.c;
+        }
+        __syncthreads();
+    }
+    // spans past the last file's: no work (the grid is sized on the bound)
+    for (uint32_t j = (uint32_t)s_scarry + tid; j < a.span_max; j += kSegThreads) a.span_file[j] = ~0u;
+    if (tid == 0) {
+        a.file_off[nfile] = s_carry;
+        a.counts[1] = s_maxr;
+        a.counts[2] = s_carry;
     }
 }
 
@@ -1728,7 +2104,7 @@ __global__ __launch_bounds__(1024) void bloom_or_kernel(BloomOrArgs a, SstArgs s
     // run side by side on one XCD and the second read of the filter's hash
     // records is served by that XCD's L2
     const uint32_t b = blockIdx.x, f = (b / 16) * 8 + b % 8, sl = (b / 8) % 2;
-    if (f >= a.nfiles) return;
+    if (f >= a.nfiles || (a.dnf && f >= uni64(*a.dnf))) return;
     // the image's header, filter prefix and footer (disjoint from the words)
     if (sl == 0 && threadIdx.x < kWave) sst_meta_body(sa, f);
     const uint32_t lo = sl * a.split, hi = lo + a.split < a.m ? lo + a.split : a.m;
@@ -3088,12 +3464,22 @@ extern "C" size_t lsm_build_sst_workspace_bytes(uint32_t nfile, uint32_t max_fil
 
 static uint64_t barrett_recip(uint64_t m) { return ~0ull / m; }
 
+// The stream build's plan outputs (lsm_build_sst_stream): nfile is then the
+// bound nfile_max, the real count is *dnf on the device.
+struct StreamGrid {
+    const uint32_t *span_file;
+    const FileDesc *desc;
+    uint32_t span_max;
+    const uint64_t *dnf;
+};
+
 static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
                           const uint8_t *d_vals, const uint64_t *d_voff,
                           const uint64_t *d_file_start, uint32_t nfile,
                           uint32_t max_file_records, uint64_t m, uint32_t k, uint8_t *d_out,
                           const uint64_t *d_file_off, int64_t *d_footer, void *d_workspace,
-                          size_t ws_bytes, void *stream, const VViewArgs *views) {
+                          size_t ws_bytes, void *stream, const VViewArgs *views,
+                          const StreamGrid *sg = nullptr) {
     if (!ctx || m == 0 || m >= (1ull << 63)) return LSM_EINVAL;
     if (nfile == 0) return 0;
     if (!d_keys || !d_koff || (!d_vals && !views) || !d_voff || !d_file_start || !d_out ||
@@ -3119,12 +3505,15 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     a.skip_v = views != nullptr;
     a.hrec = nullptr;
     a.hm = a.hrl = a.hrh = 0;
+    a.span_file = sg ? sg->span_file : nullptr;
+    a.desc = sg ? sg->desc : nullptr;
 
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
     bool forked = false, split = false;
     if (hash_once_bloom(m)) {
-        const size_t need = lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
+        // the stream build's records are indexed by stream position (16 n bytes)
+        const size_t need = sg ? 0 : lsm_build_sst_workspace_bytes(nfile, max_file_records, m, kk);
         if (need > 16 && (!d_workspace || ws_bytes < need)) return LSM_ESPACE;
         if (split_bloom(m, kk, max_file_records)) {
             // Filter.Add's key hash runs inside the region writer (the keys
@@ -3202,12 +3591,19 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         const hipError_t _e = (expr);                   \
         if (_e != hipSuccess && rc == 0) rc = -(1000 + (int)_e); \
     } while (0)
-    if (chunks) {
+    if (sg) {
+        if (sg->span_max)
+            hipLaunchKernelGGL((sst_regions_kernel<true, true>), dim3(sg->span_max), dim3(kRegWaves * kWave), 0,
+                               rs, a);
+        LSM_TRY(hipGetLastError());
+    } else if (chunks) {
         const uint32_t rspans = (max_file_records + kRegSpanRecs - 1) / kRegSpanRecs;
         if (a.skip_v)
-            hipLaunchKernelGGL(sst_regions_kernel<false>, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
+            hipLaunchKernelGGL((sst_regions_kernel<false, false>), dim3(nfile, rspans), dim3(kRegWaves * kWave), 0,
+                               rs, a);
         else
-            hipLaunchKernelGGL(sst_regions_kernel<true>, dim3(nfile, rspans), dim3(kRegWaves * kWave), 0, rs, a);
+            hipLaunchKernelGGL((sst_regions_kernel<true, false>), dim3(nfile, rspans), dim3(kRegWaves * kWave), 0,
+                               rs, a);
         LSM_TRY(hipGetLastError());
         if (views && rc == 0) {
             // V descriptors: the records are copied whole (runs); KV
@@ -3239,6 +3635,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
         bo.out = d_out;
         bo.file_off = d_file_off;
         bo.nfiles = nfile;
+        bo.dnf = sg ? sg->dnf : nullptr;
         hipLaunchKernelGGL(bloom_or_kernel, dim3((nfile + 7) / 8 * 16), dim3(1024), (size_t)(osb / 8), s,
                            bo, a);
         LSM_TRY(hipGetLastError());
@@ -3280,6 +3677,134 @@ extern "C" int lsm_build_sst_views(lsm_ctx *ctx, const uint8_t *d_keys, const ui
     return build_sst_impl(ctx, d_keys, d_koff, nullptr, d_voff, d_file_start, nfile,
                           max_file_records, m, k, d_out, d_file_off, d_footer, d_workspace,
                           ws_bytes, stream, &v);
+}
+
+// ---- the builder path over one sorted stream (ABI 7) ------------------------
+
+// Each file but the last holds EstimateSize sums >= threshold, so
+// (nfile - 1) * threshold <= 16 n + key bytes + value bytes.
+extern "C" uint32_t lsm_stream_max_files(uint64_t n, uint64_t key_bytes, uint64_t val_bytes,
+                                         uint64_t threshold) {
+    if (n == 0) return 0;
+    if (threshold == 0) return 1;
+    uint64_t b = (16 * n + key_bytes + val_bytes) / threshold + 1;
+    if (b > n) b = n;
+    return b > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)b;
+}
+
+// every record adds at least 16 to the running size, so a file reaches the
+// threshold within ceil(threshold / 16) records
+static uint64_t stream_max_recs(uint64_t n, uint64_t threshold) {
+    if (threshold == 0) return n;
+    const uint64_t r = (threshold + 15) / 16;
+    return r < n ? r : n;
+}
+static uint64_t stream_span_max(uint64_t n, uint32_t nfile_max) {
+    return (n + kRegSpanRecs - 1) / kRegSpanRecs + nfile_max;
+}
+static bool stream_split(uint64_t n, uint64_t threshold, uint64_t m, uint32_t k) {
+    return split_bloom(m, k ? k : 1, stream_max_recs(n, threshold));
+}
+
+struct StreamWs {
+    FileDesc *desc;
+    uint32_t *span_file;
+    void *rest;  // the hash records (split build) or lsm_build_sst's workspace
+    size_t rest_bytes;
+};
+static size_t stream_ws_layout(uint8_t *base, uint64_t n, uint64_t threshold, uint32_t nfile_max,
+                               uint64_t m, uint32_t k, StreamWs *w) {
+    size_t o = 64ull * nfile_max;
+    const size_t sp = o;
+    o += (4 * stream_span_max(n, nfile_max) + 255) / 256 * 256;
+    const size_t rest = stream_split(n, threshold, m, k)
+                            ? 4ull * kHashRecDwords * n + 16
+                            : lsm_build_sst_workspace_bytes(nfile_max, (uint32_t)stream_max_recs(n, threshold), m,
+                                                            k ? k : 1);
+    if (w) {
+        w->desc = reinterpret_cast<FileDesc *>(base);
+        w->span_file = reinterpret_cast<uint32_t *>(base + sp);
+        w->rest = base + o;
+        w->rest_bytes = rest;
+    }
+    return o + rest;
+}
+
+extern "C" size_t lsm_build_sst_stream_workspace_bytes(uint64_t n, uint64_t threshold, uint32_t nfile_max,
+                                                       uint64_t m, uint32_t k) {
+    return stream_ws_layout(nullptr, n, threshold, nfile_max, m, k, nullptr);
+}
+
+extern "C" uint64_t lsm_build_sst_stream_out_bytes(uint64_t n, uint64_t key_bytes, uint64_t val_bytes,
+                                                   uint32_t nfile_max, uint64_t m, uint32_t align) {
+    return (uint64_t)nfile_max * (lsm_filter_block_size(m) + 40 + (align ? align : 1) - 1) + 16 * n +
+           3 * key_bytes + val_bytes;
+}
+
+static StreamPlanArgs stream_plan_args(const uint64_t *d_koff, const uint64_t *d_voff, uint64_t n,
+                                       uint64_t threshold, uint32_t nfile_max, uint64_t *d_file_start,
+                                       uint64_t *d_counts) {
+    StreamPlanArgs p{};
+    p.koff = d_koff;
+    p.voff = d_voff;
+    p.n = n;
+    p.T = threshold;
+    p.nfile_max = nfile_max;
+    p.file_start = d_file_start;
+    p.counts = d_counts;
+    return p;
+}
+
+extern "C" int lsm_segment_files(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff, uint64_t n,
+                                 uint64_t threshold, uint32_t nfile_max, uint64_t *d_file_start,
+                                 uint64_t *d_counts, void *stream) {
+    if (!ctx || !d_file_start || !d_counts || (n && (!d_koff || !d_voff))) return LSM_EINVAL;
+    const StreamPlanArgs p = stream_plan_args(d_koff, d_voff, n, threshold, nfile_max, d_file_start, d_counts);
+    hipLaunchKernelGGL(sst_stream_plan_kernel, dim3(1), dim3(kSegThreads), 0, static_cast<hipStream_t>(stream), p);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_build_sst_stream(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                                    const uint8_t *d_vals, const uint64_t *d_voff, uint64_t n,
+                                    uint64_t threshold, uint32_t nfile_max, uint64_t m, uint32_t k,
+                                    uint32_t align, uint8_t *d_out, uint64_t *d_file_start,
+                                    uint64_t *d_file_off, int64_t *d_footer, uint64_t *d_counts,
+                                    void *d_workspace, size_t ws_bytes, void *stream) {
+    if (!ctx || m == 0 || m >= (1ull << 63) || align == 0) return LSM_EINVAL;
+    if (!d_file_start || !d_file_off || !d_counts) return LSM_EINVAL;
+    if (n && (!d_keys || !d_koff || !d_vals || !d_voff || !d_out || !d_workspace)) return LSM_EINVAL;
+    const uint64_t span_max = stream_span_max(n, nfile_max);
+    if (span_max > 0x7FFFFFFFull) return LSM_EINVAL;
+    StreamWs w;
+    const size_t need = stream_ws_layout(static_cast<uint8_t *>(d_workspace), n, threshold, nfile_max, m, k, &w);
+    if (ws_bytes < need) return LSM_ESPACE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    StreamPlanArgs p = stream_plan_args(d_koff, d_voff, n, threshold, nfile_max, d_file_start, d_counts);
+    p.span_max = (uint32_t)span_max;
+    p.filter_bytes = lsm_filter_block_size(m);
+    p.align = align;
+    p.file_off = d_file_off;
+    p.desc = w.desc;
+    p.span_file = w.span_file;
+    hipLaunchKernelGGL(sst_stream_plan_kernel, dim3(1), dim3(kSegThreads), 0, s, p);
+    LSM_HIP_CHECK(hipGetLastError());
+    if (n == 0 || nfile_max == 0) return 0;
+    const uint32_t maxr = (uint32_t)stream_max_recs(n, threshold);
+    if (stream_split(n, threshold, m, k)) {
+        // go-lsm's filter shape: every launch sized on the bounds, the counts
+        // stay on the device
+        StreamGrid g{w.span_file, w.desc, (uint32_t)span_max, d_counts};
+        return build_sst_impl(ctx, d_keys, d_koff, d_vals, d_voff, d_file_start, nfile_max, maxr, m, k, d_out,
+                              d_file_off, d_footer, w.rest, w.rest_bytes, stream, nullptr, &g);
+    }
+    // other filter shapes size their launches on the real counts: read back
+    uint64_t *h = static_cast<uint64_t *>(ctx->host_rb);
+    LSM_HIP_CHECK(hipMemcpyAsync(h, d_counts, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    LSM_HIP_CHECK(hipStreamSynchronize(s));
+    if (h[3]) return LSM_ESPACE;
+    return build_sst_impl(ctx, d_keys, d_koff, d_vals, d_voff, d_file_start, (uint32_t)h[0], (uint32_t)h[1], m, k,
+                          d_out, d_file_off, d_footer, w.rest, w.rest_bytes, stream, nullptr);
 }
 
 extern "C" int lsm_bloom_probe(lsm_ctx *ctx, const uint64_t *d_words, uint64_t m, uint32_t k,

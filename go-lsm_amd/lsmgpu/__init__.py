@@ -16,5 +16,6 @@ from .codec import (  # noqa: F401
     level_get_tree, SeekTree,
     GET_ABSENT, GET_FOUND, GET_SEEK_FAILED, GET_VALUE_LENGTH, GET_VALUE_TOO_LONG, GET_VALUE_SHORT, Merge, alloc_merge, merge_kvs, merge_kvs_into, gather_kvs,
     prepare_sst_device, sst_pairs, sst_pairs_into, compact_merge_into, TOMBSTONE, build_sst_views_into,
-    TIE_INPUT, TIE_GOHEAP, goheap_pop_order)
+    TIE_INPUT, TIE_GOHEAP, goheap_pop_order,
+    SstStream, prepare_sst_stream, build_sst_stream, build_sst_stream_into, segment_files_device)
 from . import synth  # noqa: F401

@@ -36,6 +36,7 @@ SIGNATURES = {
     "lsm_abi_version": (ctypes.c_int, []),
     "lsm_input_slack": (ctypes.c_int, []),
     "lsm_build_id": (ctypes.c_char_p, []),
+    "lsm_build_flags": (ctypes.c_char_p, []),
     "lsm_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "lsm_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "lsm_ctx_num_cus": (ctypes.c_int, [ctypes.c_void_p]),
@@ -153,6 +154,22 @@ SIGNATURES = {
                                           ctypes.c_void_p, c_u64p, ctypes.c_uint64, c_u8p, c_u64p,
                                           c_u8p, c_u64p, ctypes.c_void_p, ctypes.c_size_t,
                                           ctypes.c_void_p]),
+    "lsm_stream_max_files": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                               ctypes.c_uint64]),
+    "lsm_segment_files": (ctypes.c_int, [ctypes.c_void_p, c_u64p, c_u64p, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_uint32, c_u64p, c_u64p,
+                                         ctypes.c_void_p]),
+    "lsm_build_sst_stream_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint64, ctypes.c_uint64,
+                                                                ctypes.c_uint32, ctypes.c_uint64,
+                                                                ctypes.c_uint32]),
+    "lsm_build_sst_stream_out_bytes": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64,
+                                                          ctypes.c_uint64, ctypes.c_uint32,
+                                                          ctypes.c_uint64, ctypes.c_uint32]),
+    "lsm_build_sst_stream": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u8p, c_u64p,
+                                            ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_u8p,
+                                            c_u64p, c_u64p, ctypes.c_void_p, c_u64p,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "lsm_sst_image_sizes": (ctypes.c_int, [ctypes.c_void_p, c_u64p, c_u64p, c_u64p,
                                            ctypes.c_uint32, ctypes.c_uint64, c_u64p,
                                            ctypes.c_void_p]),
@@ -179,7 +196,7 @@ SIGNATURES = {
     "lsm_stream_sync": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 6   # LSM_ABI_VERSION this binding is written against
+ABI_VERSION = 7   # LSM_ABI_VERSION this binding is written against
 INPUT_SLACK = 32  # LSM_INPUT_SLACK: device inputs are padded by this much
 
 _lib = None
@@ -214,7 +231,11 @@ def load():
         spec = importlib.util.spec_from_file_location("_lsm_build_id", os.path.join(pkg, "build_id.py"))
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
-        want, have = mod.source_id(pkg), lib.lsm_build_id().decode()
+        # hashed with the compiler, target and flags the library records it
+        # was built with (a `make ARCH=... HIPFLAGS=...` build is accepted)
+        flags = lib.lsm_build_flags().decode().split("|")
+        want = mod.source_id(pkg, flags=flags if len(flags) == 3 else None)
+        have = lib.lsm_build_id().decode()
         if want != have:
             raise RuntimeError(
                 f"{LIB_PATH} was built from other sources (build id {have}, the tree's "

@@ -719,6 +719,93 @@ def build_sst(ctx: Context, batch: RecordBatch, file_start: np.ndarray,
     return sb
 
 
+class SstStream:
+    """lsm_build_sst_stream's buffers for one sorted stream: the rule, the
+    layout and the images in one call, sized on lsm_stream_max_files' bound.
+    The counts stay on the device ({nfile, most records in a file, image
+    bytes, overflow}); result() reads them back after the build."""
+
+    def __init__(self, ctx, batch, threshold, m, k, align):
+        dev = ctx.torch_device
+        lib = ctx.lib
+        n = batch.n
+        kb, vb = int(batch.keys.numel()), int(batch.vals.numel())
+        self.threshold, self.m, self.k, self.align, self.n = threshold, m, k, align, n
+        self.nfile_max = int(lib.lsm_stream_max_files(n, kb, vb, threshold))
+        out_bytes = int(lib.lsm_build_sst_stream_out_bytes(n, kb, vb, self.nfile_max, m, align))
+        ws = int(lib.lsm_build_sst_stream_workspace_bytes(n, threshold, self.nfile_max, m, k))
+        self.out = torch.empty(pad16(max(out_bytes, 1)), dtype=torch.uint8, device=dev)
+        self.workspace = torch.empty(max(ws, 16), dtype=torch.uint8, device=dev)
+        self.d_file_start = torch.empty(self.nfile_max + 1, dtype=torch.int64, device=dev)
+        self.d_file_off = torch.empty(self.nfile_max + 1, dtype=torch.int64, device=dev)
+        self.footer = torch.empty(max(self.nfile_max, 1) * 4, dtype=torch.int64, device=dev)
+        self.counts = torch.zeros(4, dtype=torch.int64, device=dev)
+        self._koff, self._voff = batch.koff, batch.voff
+        self._filter = int(lib.lsm_filter_block_size(m))
+
+    def result(self) -> "SstBuild":
+        """The build as an SstBuild with host copies of its layout (reads
+        back; raises on overflow)."""
+        torch.cuda.synchronize(self.out.device)
+        c = self.counts.cpu().numpy().view(np.uint64)
+        if int(c[3]):
+            raise RuntimeError("lsm_build_sst_stream: the stream needs more than nfile_max files")
+        nf = int(c[0])
+        fs = self.d_file_start[:nf + 1].cpu().numpy().view(np.uint64).copy()
+        fo = self.d_file_off[:nf + 1].cpu().numpy().view(np.uint64).copy()
+        # image sizes (sstable.go:131-193) from the device offsets
+        ko, vo = self._koff, self._voff
+        r0, r1 = self.d_file_start[:nf], self.d_file_start[1:nf + 1]
+        sz = (8 + (ko[r0 + 1] - ko[r0]) + (ko[r1] - ko[r1 - 1]) + self._filter + 16 * (r1 - r0) +
+              (ko[r1] - ko[r0]) + (vo[r1] - vo[r0]) + 32) if nf else torch.zeros(0, dtype=torch.int64)
+        return SstBuild(out=self.out, footer=self.footer, workspace=self.workspace,
+                        d_file_start=self.d_file_start[:nf + 1], d_file_off=self.d_file_off[:nf + 1],
+                        max_recs=int(c[1]), m=self.m, k=self.k, nfile=nf, file_start=fs,
+                        file_off=fo[:nf], file_size=sz.cpu().numpy().view(np.uint64).copy(),
+                        d_file_size=None)
+
+
+def prepare_sst_stream(ctx: Context, batch: RecordBatch, threshold: int = MAX_SSTABLE_SIZE,
+                       m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K, align: int = 16) -> SstStream:
+    return SstStream(ctx, batch, threshold, m, k, align)
+
+
+def build_sst_stream_into(ctx: Context, batch: RecordBatch, ss: SstStream, stream=None) -> None:
+    """lsm_build_sst_stream: Builder.Add / ShouldFlush / Build over the sorted
+    stream (merge.go:106-128) with SSTable.EncodeTo and Filter.Add per file."""
+    _lib.check(ctx.lib.lsm_build_sst_stream(
+        ctx.handle, _ptr(batch.keys), _ptr(batch.koff), _ptr(batch.vals), _ptr(batch.voff), batch.n,
+        ss.threshold, ss.nfile_max, ss.m, ss.k, ss.align, _ptr(ss.out), _ptr(ss.d_file_start),
+        _ptr(ss.d_file_off), _ptr(ss.footer), _ptr(ss.counts), _ptr(ss.workspace),
+        ss.workspace.numel(), _stream_handle(stream)), "lsm_build_sst_stream")
+
+
+def build_sst_stream(ctx: Context, batch: RecordBatch, threshold: int = MAX_SSTABLE_SIZE,
+                     m: int = DEFAULT_BLOOM_M, k: int = DEFAULT_BLOOM_K, align: int = 16,
+                     stream=None) -> SstStream:
+    ss = prepare_sst_stream(ctx, batch, threshold, m, k, align)
+    build_sst_stream_into(ctx, batch, ss, stream=stream)
+    return ss
+
+
+def segment_files_device(ctx: Context, batch: RecordBatch, threshold: int = MAX_SSTABLE_SIZE,
+                         nfile_max: Optional[int] = None, stream=None):
+    """lsm_segment_files (the builder rule on the device) -> (file starts as a
+    host array, counts {nfile, most records in a file, 0, overflow})."""
+    dev = ctx.torch_device
+    if nfile_max is None:
+        nfile_max = int(ctx.lib.lsm_stream_max_files(batch.n, int(batch.keys.numel()),
+                                                     int(batch.vals.numel()), threshold))
+    fs = torch.full((nfile_max + 1,), -1, dtype=torch.int64, device=dev)
+    counts = torch.full((4,), -1, dtype=torch.int64, device=dev)
+    _lib.check(ctx.lib.lsm_segment_files(ctx.handle, _ptr(batch.koff), _ptr(batch.voff), batch.n,
+                                         threshold, nfile_max, _ptr(fs), _ptr(counts),
+                                         _stream_handle(stream)), "lsm_segment_files")
+    torch.cuda.synchronize(dev)
+    c = counts.cpu().numpy().view(np.uint64).copy()
+    return fs[:int(c[0]) + 1].cpu().numpy().view(np.uint64).copy(), c
+
+
 def sum256(ctx: Context, batch: RecordBatch, stream=None) -> torch.Tensor:
     out = torch.empty((max(batch.n, 1), 4), dtype=torch.int64, device=ctx.torch_device)
     _lib.check(ctx.lib.lsm_sum256(ctx.handle, _ptr(batch.keys), _ptr(batch.koff), batch.n,

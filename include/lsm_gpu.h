@@ -42,8 +42,12 @@ extern "C" {
  * (lsm_level_index_build, lsm_level_may_contain_indexed).
  * v6: lsm_level_get (the batched Get past MayContain: Seek + the value) and
  * its Seek tree (lsm_level_get_tree_bytes, lsm_level_get_tree_build);
- * lsm_compact_merge_async (the join and the merge as one call). */
-#define LSM_ABI_VERSION 6
+ * lsm_compact_merge_async (the join and the merge as one call).
+ * v7: the builder rule on the device (lsm_segment_files) and the builder path
+ * over one sorted stream as one call (lsm_build_sst_stream: rule, layout and
+ * images with the fused bloom, no host round trip); lsm_level_get takes the
+ * Seek tree's size; lsm_level0_get (searchFromLevel0 over every table). */
+#define LSM_ABI_VERSION 7
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
 /* Record grammars (all fixed-width little-endian). */
@@ -63,9 +67,28 @@ enum lsm_status {
     LSM_ST_TRUNC_VLEN = 4,       /* kv.go:98 "decode value length"                 */
     LSM_ST_VAL_TOO_LONG = 5,     /* kv.go:102 "invalid value length: %d" (> 1<<30) */
     LSM_ST_TRUNC_VAL = 6,        /* data.go:71 "read value data failed", kv.go:108 "decode value" */
-    LSM_ST_IDX_OVERRUN = 7,      /* index.go:88-91 "unexpected EOF: size limit reached while reading key length" */
+    LSM_ST_IDX_OVERRUN = 7,      /* an index entry crosses the block's end: see below */
     LSM_ST_CAPACITY = 8,         /* record capacity rec_base[b+1]-rec_base[b] exhausted (not a reference error) */
 };
+
+/* LSM_ST_IDX_OVERRUN and the reference's three messages.  IndexBlock.DecodeFrom
+ * (index.go:61-101) reads an entry whole -- Key.DecodeFrom, then the i64
+ * offset -- and only then compares totalRead with the size.  Which error Go
+ * returns for an entry that crosses the block's end therefore depends on the
+ * bytes its io.Reader holds PAST the block:
+ *   - enough bytes (SSTable.DecodeFrom's reader is the whole file, the footer
+ *     follows the index, sstable.go:122; index_test.go's reader holds the
+ *     whole buffer): "unexpected EOF: size limit reached while reading key
+ *     length" (index.go:88-91);
+ *   - the reader ends inside the key length or the key (a reader cut at the
+ *     block): "decode index key length failed" (index.go:73-76);
+ *   - the reader ends inside the offset: "decode index offset failed"
+ *     (index.go:81-84).
+ * The library never reads past blk_len, so it reports this one status for
+ * all three, with d_nrec = the entries before the crossing one -- what Go
+ * appended in every case (the oracle, oracle/lsm_oracle.c, follows the first
+ * reading: bytes past the block present).  A binding that needs Go's message
+ * picks it from the bytes its own reader holds past the block. */
 
 enum lsm_error {
     LSM_EINVAL = -1,  /* bad argument                        */
@@ -121,6 +144,9 @@ int lsm_input_slack(void);
  * go-lsm_amd/build_id.py): a binding shipped beside the sources compares it
  * and refuses a stale prebuilt library.  Not part of the Go surface. */
 const char *lsm_build_id(void);
+/* "HIPCC|ARCH|HIPFLAGS" the library was compiled with: the build id hashes
+ * these with the sources, so a binding recomputes the id from this string. */
+const char *lsm_build_flags(void);
 /* One context per goroutine / OS thread (callers are concurrent goroutines,
  * sstable_test.go:379-400); no hidden global mutable state. */
 int lsm_ctx_create(int device, lsm_ctx **out);
@@ -558,6 +584,47 @@ int lsm_sst_pairs(lsm_ctx *ctx, const lsm_sst_meta *d_meta, const uint64_t *d_fi
                   uint32_t nfile, const lsm_rec_desc *d_idx_desc, const lsm_rec_desc *d_data_desc,
                   lsm_rec_desc *d_key_out, lsm_rec_desc *d_val_out, uint64_t *d_prefix,
                   void *stream);
+
+/* ---- the builder path over one sorted stream (ABI 7) ----------------------- */
+
+/* The builder rule on the device: lsm_segment_files_host's file starts for
+ * the device CSR offsets d_koff / d_voff (n + 1 entries each) -- Builder.Add /
+ * ShouldFlush (builder.go:34-42, EstimateSize kv.go:118-121) as driven by
+ * CompactAndMergeKVs (merge.go:106-128); threshold 0 = never flush.  Writes
+ * d_file_start[0 .. nfile] (d_file_start[nfile] = n; nfile_max + 1 entries)
+ * and d_counts (device, 4 entries) = {nfile, the most records in one file, 0,
+ * overflow}.  nfile_max = lsm_stream_max_files(n, key bytes, value bytes,
+ * threshold) always suffices; with a smaller bound a stream needing more files
+ * gets nfile = 0 and overflow = 1.  One workgroup; asynchronous. */
+uint32_t lsm_stream_max_files(uint64_t n, uint64_t key_bytes, uint64_t val_bytes, uint64_t threshold);
+int lsm_segment_files(lsm_ctx *ctx, const uint64_t *d_koff, const uint64_t *d_voff, uint64_t n,
+                      uint64_t threshold, uint32_t nfile_max, uint64_t *d_file_start,
+                      uint64_t *d_counts, void *stream);
+
+/* Builder.Add / ShouldFlush / Build over one sorted record stream, every file
+ * flushed at `threshold` (merge.go:106-128's loop; sstable.go:21's 2 MiB in
+ * go-lsm), with SSTable.Add / EncodeTo and Filter.Add for every file -- the
+ * rule (lsm_segment_files), the layout (lsm_sst_layout's: each image at a
+ * multiple of `align` in d_out) and the images (lsm_build_sst's bytes) in one
+ * call, with no host round trip for go-lsm's filter shape (two LDS slices,
+ * k <= 16): every launch is sized on nfile_max and the counts stay on the
+ * device.  Other filter shapes read the counts back (the call synchronizes).
+ * Outputs: d_file_start (nfile_max + 1), d_file_off (nfile_max + 1: the last
+ * entry used is the total), d_footer (optional, 4 * nfile_max), d_counts (4:
+ * {nfile, most records in a file, image bytes, overflow}); d_out must hold
+ * lsm_build_sst_stream_out_bytes(...) bytes, the workspace
+ * lsm_build_sst_stream_workspace_bytes(...).  Same images, file for file, as
+ * lsm_segment_files_host + lsm_build_sst. */
+size_t lsm_build_sst_stream_workspace_bytes(uint64_t n, uint64_t threshold, uint32_t nfile_max,
+                                            uint64_t m, uint32_t k);
+uint64_t lsm_build_sst_stream_out_bytes(uint64_t n, uint64_t key_bytes, uint64_t val_bytes,
+                                        uint32_t nfile_max, uint64_t m, uint32_t align);
+int lsm_build_sst_stream(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d_koff,
+                         const uint8_t *d_vals, const uint64_t *d_voff, uint64_t n,
+                         uint64_t threshold, uint32_t nfile_max, uint64_t m, uint32_t k,
+                         uint32_t align, uint8_t *d_out, uint64_t *d_file_start,
+                         uint64_t *d_file_off, int64_t *d_footer, uint64_t *d_counts,
+                         void *d_workspace, size_t ws_bytes, void *stream);
 
 /* .sst image size of each file f = records [d_file_start[f], d_file_start[f+1])
  * of a device CSR batch (as lsm_sst_image_size_host, sstable.go:131-193). */

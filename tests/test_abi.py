@@ -31,7 +31,7 @@ def test_header_functions_exported():
 
 
 def test_abi_version():
-    assert _lib.load().lsm_abi_version() == 6
+    assert _lib.load().lsm_abi_version() == 7
     assert _lib.load().lsm_input_slack() == 32
 
 
@@ -151,3 +151,43 @@ def test_build_id_covers_compiler_flags():
         return out.split("LSM_BUILD_ID='\"")[1].split('"')[0]
     assert make_id() == bid.source_id(pkg)
     assert make_id("HIPFLAGS=-O1 --offload-arch=gfx950") != bid.source_id(pkg)
+
+
+def test_build_flags_recorded():
+    """The library records the compiler, target and flags it was built with
+    (lsm_build_flags); the build id is the sources hashed with exactly those,
+    so a `make ARCH=... HIPFLAGS=...` build is accepted by load()."""
+    import importlib.util
+    pkg = os.path.join(ROOT, "go-lsm_amd")
+    spec = importlib.util.spec_from_file_location("bid", os.path.join(pkg, "build_id.py"))
+    bid = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bid)
+    lib = _lib.load()
+    flags = lib.lsm_build_flags().decode().split("|")
+    assert len(flags) == 3 and flags[1] == "gfx950"
+    assert lib.lsm_build_id().decode() == bid.source_id(pkg, flags=flags)
+    other = [flags[0], flags[1], flags[2] + " -DX"]
+    assert bid.source_id(pkg, flags=other) != bid.source_id(pkg, flags=flags)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_stream_max_files_bounds_the_rule(seed):
+    """lsm_stream_max_files bounds the file count of every stream: each file
+    but the last holds EstimateSize sums >= threshold (builder.go:40-42)."""
+    lib = _lib.load()
+    rng = np.random.default_rng(seed)
+    for _ in range(20):
+        n = int(rng.integers(0, 4000))
+        kl = rng.integers(0, 64, n).astype(np.uint64)
+        vl = rng.integers(0, int(rng.choice([1, 100, 5000])), n).astype(np.uint64)
+        koff = np.zeros(n + 1, np.uint64)
+        voff = np.zeros(n + 1, np.uint64)
+        koff[1:] = np.cumsum(kl)
+        voff[1:] = np.cumsum(vl)
+        for thr in (0, 1, 16, 17, 4096, 2 * 1024 * 1024):
+            nf = len(ora.segment_files(koff, voff, thr)) - 1
+            bound = lib.lsm_stream_max_files(n, int(koff[-1]), int(voff[-1]), thr)
+            assert nf <= bound <= n
+    assert lib.lsm_stream_max_files(3_300_000, 16 * 3_300_000, 100 * 3_300_000, 2 * 1024 * 1024) == 208
+    assert lib.lsm_stream_max_files(0, 0, 0, 100) == 0
+    assert lib.lsm_stream_max_files(5, 0, 0, 0) == 1

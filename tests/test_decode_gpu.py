@@ -170,6 +170,37 @@ def test_index_test_vectors(ctx):
     assert list(r.idx_value.cpu().numpy()[r.rec_base.cpu().numpy()[0]:][:3]) == [100, 200, 300]
 
 
+def test_index_block_cut_inside_last_entry(ctx):
+    """An IDX block whose size ends inside its last entry: inside the key
+    length, the key, or the i64 offset, with the entry's remaining bytes
+    present past the block (the .sst's reader) or not (the block ends the
+    buffer).  Go appends the entries before it and fails on that entry
+    (index.go:61-101, one of three messages by what the reader holds past the
+    block: include/lsm_gpu.h); the library and the oracle both report
+    LSM_ST_IDX_OVERRUN with the same records."""
+    ent = [(b"alpha", 100), (b"bravo-key", -7), (b"charlie-longer-key", 2**40)]
+    full = idx_block(ent)
+    last = len(idx_block(ent[:2]))
+    klen_cut = [last + 1, last + 2, last + 3]                 # inside the key length
+    key_cut = [last + 4, last + 4 + 7, last + 4 + 17]         # inside the key
+    off_cut = [last + 4 + 18 + j for j in (0, 1, 4, 7)]       # inside the offset
+    blocks = [full[:c] for c in klen_cut + key_cut + off_cut]
+    # the same cuts with the rest of the entry present past the block
+    buf = np.frombuffer(full, np.uint8)
+    dev = ctx.torch_device
+    cuts = klen_cut + key_cut + off_cut
+    d_in = lsmgpu.to_device_bytes(buf, dev)
+    d_off = torch.zeros(len(cuts), dtype=torch.int64, device=dev)
+    d_len = torch.tensor(np.array(cuts, np.uint32).view(np.int32), device=dev)
+    r = lsmgpu.decode_blocks(ctx, lsmgpu.GRAMMAR_IDX, d_in, d_off, d_len)
+    torch.cuda.synchronize()
+    check_against_oracle(lsmgpu.GRAMMAR_IDX, buf, np.zeros(len(cuts), np.uint64),
+                         np.array(cuts, np.uint32), r)
+    assert (r.status.cpu().numpy() == 7).all() and (r.nrec.cpu().numpy() == 2).all()
+    r2 = run(ctx, lsmgpu.GRAMMAR_IDX, blocks)
+    assert (r2.status.cpu().numpy() == 7).all() and (r2.nrec.cpu().numpy() == 2).all()
+
+
 # ---- fuzz ---------------------------------------------------------------------------
 
 def rand_records(rng, grammar, n, kmax=40, vmax=300):
