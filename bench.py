@@ -47,7 +47,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="decode4k",
                     choices=["decode4k", "decode64k", "mixed", "sst", "sstdec", "sstdec1", "wal",
-                             "probe", "level", "get", "compact"])
+                             "probe", "level", "get", "get0", "compact"])
     ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU (weak scaling)")
     ap.add_argument("--global-blocks", type=int, default=None,
                     help="fixed global batch dealt round-robin over the ranks (strong "
@@ -786,6 +786,10 @@ def main(argv=None):
         # level search, reference shape (§8(f) f3); get: + Seek + value
         from bench_sstdec import bench_level_search
         out, data = bench_level_search(args, world, rank, local)
+    elif args.config == "get0":
+        # level 0's Get (§8(f) f3): every table in order (searchFromLevel0)
+        from bench_sstdec import bench_level0_get
+        out, data = bench_level0_get(args, world, rank, local)
     elif args.config == "compact":
         from bench_compact import bench_compact  # L0 -> L1 compaction (§8(f) f1 + f2)
         out, data = bench_compact(args, world, rank, local)
@@ -806,6 +810,9 @@ def main(argv=None):
         elif args.config in ("level", "get"):
             from bench_sstdec import cpu_baseline_level_search
             out["cpu_baseline"] = cpu_baseline_level_search(args, data)
+        elif args.config == "get0":
+            from bench_sstdec import cpu_baseline_level0_get
+            out["cpu_baseline"] = cpu_baseline_level0_get(args, data)
         elif args.config == "compact":
             from bench_compact import cpu_baseline_compact
             out["cpu_baseline"] = cpu_baseline_compact(args, data)

@@ -421,3 +421,175 @@ def cpu_baseline_level_search(args, data):
             "sample": f"all {nprobe} probes x {passes} passes on {cpu['threads']} threads in "
                       f"{tn:.1f} s; 1 thread: {min(done, nprobe)} probes in {t1:.1f} s",
             "value_1t": round(min(done, nprobe) / t1 / 1e6, 4), "host": cpu}
+
+
+def level0_tables(rank, ntab=3, per=15_888, space=40_000):
+    """go-lsm's level 0: ntab memtable flushes (2 MiB each, memtable.go:26;
+    a third table triggers the level-0 compaction, manager.go:389-395), newest
+    first (manager.go:284-287).  Table t holds `per` distinct random ids of one
+    key space of `space` ids, so the tables overlap and share keys (the newer
+    version wins); values differ per table.  -> list of (sorted ids, values)."""
+    rng = np.random.default_rng(synth.SEED + 77 + rank)
+    out = []
+    for t in range(ntab):
+        ids = np.sort(rng.choice(space, per, replace=False)).astype(np.int64)
+        vals = synth.value_bytes(ids + (t + 1) * 10 ** 9, synth.VAL_LEN)
+        out.append((ids, vals))
+    return out
+
+
+def bench_level0_get(args, world, rank, local):
+    """SURVEY.md §8(f) f3 at level 0: batched Manager.searchFromLevel0
+    (manager.go:160-176) -- per probe every level-0 table in order, newest
+    first: MayContain, Seek, the value; the first value wins -- 1M probes
+    (half held by some table, a quarter absent inside the tables' ranges, a
+    quarter above them) against the 3 overlapping 2 MiB tables of a full
+    level 0."""
+    from bench import sum_over_ranks, timed_region, kernel_times, traffic_from_profile
+    ctx = lsmgpu.Context(local)
+    dev = ctx.torch_device
+    space = 40_000
+    tabs = level0_tables(rank, space=space)
+    nf = len(tabs)
+    # the tables' images, built on the device one after the other into one buffer
+    imgs, offs, lens = [], [], []
+    pos = 0
+    for ids, vals in tabs:
+        n = ids.size
+        keys = synth.keys_for(ids).reshape(-1)
+        batch = lsmgpu.batch_to_device(ctx, keys, np.arange(n + 1, dtype=np.uint64) * np.uint64(16),
+                                       vals.reshape(-1).copy(),
+                                       np.arange(n + 1, dtype=np.uint64) * np.uint64(synth.VAL_LEN))
+        sb = lsmgpu.build_sst(ctx, batch, np.array([0, n], np.uint64))
+        torch.cuda.synchronize()
+        size = int(sb.file_size[0])
+        imgs.append(sb.out[:size])
+        offs.append(pos)
+        lens.append(size)
+        pos += (size + 15) // 16 * 16
+    d_img = torch.zeros(pos + 64, dtype=torch.uint8, device=dev)
+    for im, o in zip(imgs, offs):
+        d_img[o:o + im.numel()] = im
+    del imgs
+    offs = np.array(offs, np.uint64)
+    lens = np.array(lens, np.uint64)
+    r = lsmgpu.decode_sst(ctx, d_img, offs, lens)
+    tree = lsmgpu.level_get_tree(ctx, d_img, r)
+    torch.cuda.synchronize()
+    nprobe = 1 << 20
+    rng = np.random.default_rng(synth.SEED + 5 + rank)
+    union = np.unique(np.concatenate([t[0] for t in tabs]))
+    missing = np.setdiff1d(np.arange(space), union)
+    held = rng.choice(union, nprobe // 2)
+    inside = rng.choice(missing, nprobe // 4)
+    above = rng.integers(10 ** 12, 10 ** 13, nprobe - nprobe // 2 - nprobe // 4)
+    ids = rng.permutation(np.concatenate([held, inside, above]))
+    pk = synth.keys_for(ids).reshape(-1)
+    pko = np.arange(nprobe + 1, dtype=np.uint64) * np.uint64(synth.KEY_LEN)
+    probes = lsmgpu.batch_to_device(ctx, pk, pko, np.zeros(1, np.uint8), np.zeros(nprobe + 1, np.uint64))
+    table = torch.empty(nprobe, dtype=torch.int32, device=dev)
+    result = torch.empty(nprobe, dtype=torch.int32, device=dev)
+    value = torch.empty((nprobe, 4), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        lsmgpu.level0_get_into(ctx, d_img, r, probes, table, result, value, tree=tree, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_region(world, step, args.steps)
+    times, kern_ms = kernel_times(step, stream, args.steps)
+    # the timed output against the tables' own contents: a held key is
+    # answered by the newest table holding it, with that version's value view
+    # in that table's data region; every other key absent
+    t_h, res = table.cpu().numpy(), result.cpu().numpy()
+    val = value.cpu().numpy().view(lsmgpu.DESC_DTYPE).reshape(-1)
+    want_t = np.full(nprobe, -1, np.int64)
+    want_off = np.zeros(nprobe, np.int64)
+    data_off = 8 + 2 * synth.KEY_LEN + 32 + 8 * ((lsmgpu.DEFAULT_BLOOM_M + 63) // 64)
+    for t in range(nf - 1, -1, -1):  # older first, newer overwrite
+        tid = tabs[t][0]
+        j = np.searchsorted(tid, ids)
+        inn = (j < tid.size) & (tid[np.minimum(j, tid.size - 1)] == ids)
+        want_t[inn] = t
+        want_off[inn] = int(offs[t]) + data_off + j[inn] * (4 + synth.VAL_LEN)
+    found = want_t >= 0
+    assert np.array_equal(t_h.astype(np.int64), want_t), "answering table"
+    assert (res[found] == lsmgpu.GET_FOUND).all() and (res[~found] == lsmgpu.GET_ABSENT).all()
+    assert np.array_equal(val["rec_off"][found].astype(np.int64), want_off[found]), "value view"
+    assert (val["val_len"][found] == synth.VAL_LEN).all()
+    total = sum_over_ranks(world, float(nprobe))
+    fbits = r.meta_numpy()["filter_nbits"].astype(np.float64)
+    # algorithmic bytes per launch: the probe keys and offsets read once, 24 B
+    # out per probe (table, result, value view), every stored filter word read
+    # once, and per table a probe is sought in (held keys: the tables up to the
+    # answering one that hold it or pass its filter; counted here as the
+    # answering table alone, a lower bound) its index entry (4 + key + 8 B)
+    # and the value's length prefix (4 B) read once
+    alg = pk.size + 8.0 * (nprobe + 1) + 24.0 * nprobe + float((8 * np.ceil(fbits / 64)).sum()) + \
+        float(found.sum()) * (4 + synth.KEY_LEN + 8 + 4)
+    traffic, tsrc = traffic_from_profile(f"get0:{nf}:{nprobe}")
+    out = {
+        "metric": "M keys/s looked up in level 0 (every table in order: MayContain + Seek + value)",
+        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "unit": "M keys/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic: level 0 of {nf} overlapping 2 MiB tables (15,888 random keys each of one "
+                f"{space}-key space, newest first); probes half held, a quarter absent inside the "
+                "ranges, a quarter above them",
+        "verified": "every probe: the answering table = the newest holding the key, its value's view; "
+                    "every other probe absent",
+        "config": {"workload": f"{nprobe} keys x level 0 of {nf} .sst files per GPU "
+                               "(searchFromLevel0 -> searchFromTable per table: MayContain -> "
+                               "Iterator.Seek -> GetValueByOffset, bloom m=1.6M k=16)",
+                   "files_per_gpu": nf, "probes_per_gpu": nprobe,
+                   "found": int(found.sum()),
+                   "parallelism": f"dp{world} (probe batches per rank, no collective)",
+                   "scaling_note": "weak, per-rank copy: every rank probes its own level copy"},
+        "seek_tree": {"bytes": int(tree.data.numel()), "max_nidx": tree.max_nidx,
+                      "note": "built with the level (lsm_level_get_tree_build), outside the step"},
+        "roofline": {"bound": "hbm", "kernel": "lsm_level0_get (level0_get_kernel)",
+                     "kernel_ms": round(kern_ms, 5),
+                     "kernel_ms_median": round(float(np.median(times)), 5),
+                     "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1),
+                     "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(alg / (kern_ms * 1e-3) / 1e9 / 8000.0, 4),
+                     "traffic": traffic, "traffic_source": tsrc, "alg_bytes_per_launch": int(alg)},
+    }
+    return out, (d_img.cpu().numpy(), offs, lens, pk, nprobe)
+
+
+def cpu_baseline_level0_get(args, data):
+    """The oracle's searchFromLevel0 (ora_level0_get: per probe every table in
+    order, MayContain then Seek and the value) over the same images and probes:
+    1 thread, and the CPU share's threads over probe chunks."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as ora
+    from bench import host_cpu, timed_threads
+    img, offs, lens, pk, nprobe = data
+    cpu = host_cpu()
+    nf = len(offs)
+    dec = [ora.sst_decode(img[int(offs[f]):int(offs[f]) + int(lens[f])]) for f in range(nf)]
+    metas = [d[1] for d in dec]
+    gidx = ora.level_get_index([d[2] for d in dec], [d[3] for d in dec])
+    pko = np.arange(nprobe + 1, dtype=np.uint64) * np.uint64(16)
+    chunk = 16384
+
+    def one(c):
+        ora.level0_get(img, offs, lens, metas, None, None, pk, pko, c, min(nprobe, c + chunk), index=gidx)
+
+    t1, done = 0.0, 0
+    while (t1 < args.cpu_seconds / 3 or done == 0) and done < nprobe:
+        t0 = time.perf_counter()
+        one(done)
+        t1 += time.perf_counter() - t0
+        done += chunk
+    sample = list(range(0, nprobe, chunk))
+    passes, tn = timed_threads(one, sample, cpu["threads"], args.cpu_seconds)
+    return {"value": round(nprobe * passes / tn / 1e6, 4), "unit": "M keys/s",
+            "cores": cpu["threads"], "kind": "port",
+            "sample": f"all {nprobe} probes x {passes} passes on {cpu['threads']} threads in "
+                      f"{tn:.1f} s; 1 thread: {min(done, nprobe)} probes in {t1:.1f} s",
+            "value_1t": round(min(done, nprobe) / t1 / 1e6, 4), "host": cpu}

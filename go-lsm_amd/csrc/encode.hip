@@ -3229,6 +3229,108 @@ __device__ __forceinline__ int tree_cmp(const GetArgs &a, uint64_t base, uint32_
     return c;
 }
 
+// searchFromTable past MayContain (manager.go:209-223) on table t: Go's
+// bisection (through the Seek tree, or over the index), the exact-match
+// test, then GetValueByOffset (sstable.go:271-296).  -> a lsm_get_result;
+// the value's view in v on LSM_GET_FOUND.
+__device__ __forceinline__ int32_t get_in_table(const GetArgs &a, uint32_t t, const uint32_t kw[4],
+                                                uint64_t kl, const uint8_t *kp, lsm_rec_desc &v) {
+    int32_t res = LSM_GET_ABSENT;
+    const lsm_sst_meta &M = a.meta[t];
+    const uint64_t fo = a.file_off[t], fl = a.file_len[t];
+    const uint64_t base = a.rec_base ? a.rec_base[t] : fo / 4;
+    const uint32_t n = M.nidx;
+    uint32_t left = 0, right = n;
+    bool hit = false;
+    if (a.tree && n <= a.tree_nidx) {
+        // Go's bisection through the Seek tree: one 128-byte block per
+        // three steps.  The final left is the midpoint of the last step
+        // that set right, so Indexes[left].Key == target is that step's
+        // comparison being 0 (hit).
+        const uint8_t *tb = a.tree + (uint64_t)t * a.tree_stride;
+        uint64_t off = 0, cnt = 1, bi = 0;
+        uint32_t levels = a.tree_top;
+        while (left < right) {
+            const u32x4 *B = reinterpret_cast<const u32x4 *>(tb + (off + bi) * 128);
+            u32x4 nd[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) nd[q] = B[q];
+            uint32_t j = 0;
+#pragma unroll
+            for (uint32_t d = 0; d < 3; d++) {
+                if (d >= levels || left >= right) break;
+                u32x4 e = nd[0];
+                if (d == 1) e = j == 1 ? nd[1] : nd[2];
+                if (d == 2) {
+                    const u32x4 lo = j == 3 ? nd[3] : nd[4], hi = j == 5 ? nd[5] : nd[6];
+                    e = j < 5 ? lo : hi;
+                }
+                const uint32_t lw = j < 2 ? nd[7].x : j < 4 ? nd[7].y : j < 6 ? nd[7].z : nd[7].w;
+                const uint32_t el = (lw >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t ew[4] = {e.x, e.y, e.z, e.w};
+                const uint32_t mid = left + (right - left) / 2;
+                const int c = tree_cmp(a, base, mid, ew, el, kw, kl, kp);
+                if (c < 0) {
+                    left = mid + 1;
+                    j = 2 * j + 2;
+                } else {
+                    right = mid;
+                    hit = c == 0;
+                    j = 2 * j + 1;
+                }
+            }
+            // the child block: group g + 1, index 8 bi + the exit's rank
+            bi = off == 0 ? j - ((1u << levels) - 1) : 8 * bi + (j - 7);
+            off += cnt;
+            cnt = off == 1 ? (1ull << a.tree_top) : cnt * 8;
+            levels = 3;
+        }
+    } else {
+        // Go's bisection over the index (a variant loading both possible
+        // next midpoints' entries before each compare measured slower:
+        // 0.549 vs 0.375 ms per 1M-key Get, 3.0 GB of HBM traffic per
+        // call -- round 5, A/B)
+        while (left < right) {
+            const uint32_t mid = left + (right - left) / 2;
+            const lsm_rec_desc d = a.idx_desc[base + mid];
+            const uint8_t *ep = a.img + d.rec_off + 4;
+            uint32_t ew[4];
+            key_prefix(ep, d.key_len, ew);
+            const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
+            if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
+            else right = mid;
+        }
+        if (left < n) {
+            const lsm_rec_desc d = a.idx_desc[base + left];
+            const uint8_t *ep = a.img + d.rec_off + 4;
+            hit = d.key_len == kl && go_cmp(ep, d.key_len, kp, kl) == 0;
+        }
+    }
+    if (hit) {
+        const int64_t off = a.idx_value[base + left];
+        if (off < 0) {
+            res = LSM_GET_SEEK_FAILED;  // file.Seek to a negative offset
+        } else {
+            // Value.DecodeFrom from the file at off: u32 length, cap, bytes
+            const uint64_t rem = (uint64_t)off < fl ? fl - (uint64_t)off : 0;
+            if (rem < 4) {
+                res = LSM_GET_VALUE_LENGTH;
+            } else {
+                const uint8_t *vp = a.img + fo + (uint64_t)off;
+                const uint32_t vl = (uint32_t)vp[0] | (uint32_t)vp[1] << 8 | (uint32_t)vp[2] << 16 |
+                                    (uint32_t)vp[3] << 24;
+                if (vl > (1u << 30)) res = LSM_GET_VALUE_TOO_LONG;
+                else if (rem - 4 < vl) res = LSM_GET_VALUE_SHORT;
+                else {
+                    res = LSM_GET_FOUND;
+                    v = lsm_rec_desc{fo + (uint64_t)off, 0, vl};
+                }
+            }
+        }
+    }
+    return res;
+}
+
 __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.nkeys) return;
@@ -3236,105 +3338,98 @@ __global__ __launch_bounds__(256) void level_get_kernel(GetArgs a) {
     lsm_rec_desc v{0, 0, 0};
     const int32_t t = a.table[i];
     if (a.may[i] && t >= 0 && (uint32_t)t < a.nfile) {
-        const lsm_sst_meta &M = a.meta[t];
-        const uint64_t fo = a.file_off[t], fl = a.file_len[t];
-        const uint64_t base = a.rec_base ? a.rec_base[t] : fo / 4;
-        const uint32_t n = M.nidx;
         const uint64_t k0 = a.koff[i], kl = a.koff[i + 1] - k0;
         const uint8_t *kp = a.keys + k0;
         uint32_t kw[4];
         key_prefix(kp, kl, kw);
-        uint32_t left = 0, right = n;
-        bool hit = false;
-        if (a.tree && n <= a.tree_nidx) {
-            // Go's bisection through the Seek tree: one 128-byte block per
-            // three steps.  The final left is the midpoint of the last step
-            // that set right, so Indexes[left].Key == target is that step's
-            // comparison being 0 (hit).
-            const uint8_t *tb = a.tree + (uint64_t)t * a.tree_stride;
-            uint64_t off = 0, cnt = 1, bi = 0;
-            uint32_t levels = a.tree_top;
-            while (left < right) {
-                const u32x4 *B = reinterpret_cast<const u32x4 *>(tb + (off + bi) * 128);
-                u32x4 nd[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) nd[q] = B[q];
-                uint32_t j = 0;
-#pragma unroll
-                for (uint32_t d = 0; d < 3; d++) {
-                    if (d >= levels || left >= right) break;
-                    u32x4 e = nd[0];
-                    if (d == 1) e = j == 1 ? nd[1] : nd[2];
-                    if (d == 2) {
-                        const u32x4 lo = j == 3 ? nd[3] : nd[4], hi = j == 5 ? nd[5] : nd[6];
-                        e = j < 5 ? lo : hi;
-                    }
-                    const uint32_t lw = j < 2 ? nd[7].x : j < 4 ? nd[7].y : j < 6 ? nd[7].z : nd[7].w;
-                    const uint32_t el = (lw >> (16 * (j & 1))) & 0xFFFFu;
-                    const uint32_t ew[4] = {e.x, e.y, e.z, e.w};
-                    const uint32_t mid = left + (right - left) / 2;
-                    const int c = tree_cmp(a, base, mid, ew, el, kw, kl, kp);
-                    if (c < 0) {
-                        left = mid + 1;
-                        j = 2 * j + 2;
-                    } else {
-                        right = mid;
-                        hit = c == 0;
-                        j = 2 * j + 1;
-                    }
-                }
-                // the child block: group g + 1, index 8 bi + the exit's rank
-                bi = off == 0 ? j - ((1u << levels) - 1) : 8 * bi + (j - 7);
-                off += cnt;
-                cnt = off == 1 ? (1ull << a.tree_top) : cnt * 8;
-                levels = 3;
-            }
-        } else {
-            // Go's bisection over the index (a variant loading both possible
-            // next midpoints' entries before each compare measured slower:
-            // 0.549 vs 0.375 ms per 1M-key Get, 3.0 GB of HBM traffic per
-            // call -- round 5, A/B)
-            while (left < right) {
-                const uint32_t mid = left + (right - left) / 2;
-                const lsm_rec_desc d = a.idx_desc[base + mid];
-                const uint8_t *ep = a.img + d.rec_off + 4;
-                uint32_t ew[4];
-                key_prefix(ep, d.key_len, ew);
-                const int c = bound_cmp_fast(ew, d.key_len, ep, kw, kl, kp);
-                if (c < 0) left = mid + 1;  // Indexes[mid].Key < target
-                else right = mid;
-            }
-            if (left < n) {
-                const lsm_rec_desc d = a.idx_desc[base + left];
-                const uint8_t *ep = a.img + d.rec_off + 4;
-                hit = d.key_len == kl && go_cmp(ep, d.key_len, kp, kl) == 0;
-            }
-        }
-        if (hit) {
-            const int64_t off = a.idx_value[base + left];
-            if (off < 0) {
-                res = LSM_GET_SEEK_FAILED;  // file.Seek to a negative offset
-            } else {
-                // Value.DecodeFrom from the file at off: u32 length, cap, bytes
-                const uint64_t rem = (uint64_t)off < fl ? fl - (uint64_t)off : 0;
-                if (rem < 4) {
-                    res = LSM_GET_VALUE_LENGTH;
-                } else {
-                    const uint8_t *vp = a.img + fo + (uint64_t)off;
-                    const uint32_t vl = (uint32_t)vp[0] | (uint32_t)vp[1] << 8 | (uint32_t)vp[2] << 16 |
-                                        (uint32_t)vp[3] << 24;
-                    if (vl > (1u << 30)) res = LSM_GET_VALUE_TOO_LONG;
-                    else if (rem - 4 < vl) res = LSM_GET_VALUE_SHORT;
-                    else {
-                        res = LSM_GET_FOUND;
-                        v = lsm_rec_desc{fo + (uint64_t)off, 0, vl};
-                    }
-                }
-            }
-        }
+        res = get_in_table(a, (uint32_t)t, kw, kl, kp, v);
     }
     a.result[i] = res;
     a.value[i] = v;
+}
+
+// ---- level 0: Manager.searchFromLevel0 (manager.go:160-176) ---------------
+//
+// Level 0's tables overlap (each is one memtable flush, newest first:
+// addNewSSTables prepends, manager.go:284-287), so a key is searched in every
+// table in order: searchFromTable (:209-223) -- MayContain (the range check,
+// then Filter.Test), Seek, the value -- and the first non-nil value or error
+// ends the search.  One thread per key: the key is hashed once, the tables'
+// bounds and filter shapes are staged per workgroup in LDS tiles, and a
+// false positive or a Seek miss moves on to the next table.
+constexpr uint32_t kL0Threads = 256;
+constexpr uint32_t kL0Tile = 64;
+
+// Filter.Test (bloom.go:371-379) of an image's stored filter, every m (the
+// per-probe path's form: sixteen bit reads in flight at a time).
+__device__ __forceinline__ uint32_t filter_test_any(const McFile &F, const uint64_t h[4], const uint8_t *img) {
+    const uint64_t m = F.m;
+    // hashNum 0: true; m == 0 < k: Go panics, answered false
+    uint32_t r = F.k == 0 || m != 0;
+    for (uint32_t j0 = 0; j0 < F.k && r; j0 += 16) {
+        uint32_t bits = 1;
+#pragma unroll
+        for (uint32_t u = 0; u < 16; u++) {
+            const uint32_t j = j0 + u;
+            if (j < F.k) {
+                const uint64_t x = location(h[0], h[1], h[2], h[3], j);
+                const uint64_t p = m < (1ull << 63) ? mod_barrett(x, m, F.mr) : x % m;
+                bits &= p < F.nbits ? (uint32_t)(img[F.words_at + 8 * (p >> 6) + 7 - ((p & 63) >> 3)] >> (p & 7)) & 1
+                                    : 0u;
+            }
+        }
+        r &= bits;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(kL0Threads) void level0_get_kernel(GetArgs a, int32_t *table_out) {
+    __shared__ McFile tile[kL0Tile];
+    const uint64_t i = (uint64_t)blockIdx.x * kL0Threads + threadIdx.x;
+    const bool act = i < a.nkeys;
+    uint64_t k0 = 0, kl = 0;
+    uint32_t kw[4] = {0, 0, 0, 0};
+    if (act) {
+        k0 = a.koff[i];
+        kl = a.koff[i + 1] - k0;
+        key_prefix(a.keys + k0, kl, kw);
+    }
+    const uint8_t *kp = a.keys + k0;
+    uint64_t h[4] = {0, 0, 0, 0};
+    bool hashed = false, done = !act;
+    int32_t res = LSM_GET_ABSENT, tab = -1;
+    lsm_rec_desc v{0, 0, 0};
+    for (uint32_t f0 = 0; f0 < a.nfile; f0 += kL0Tile) {
+        const uint32_t nt = a.nfile - f0 < kL0Tile ? a.nfile - f0 : kL0Tile;
+        __syncthreads();  // the previous tile is consumed
+        for (uint32_t t = threadIdx.x; t < nt; t += kL0Threads) tile[t] = mc_file(a.img, a.file_off, a.meta[f0 + t], f0 + t);
+        __syncthreads();
+        for (uint32_t t = 0; t < nt && !done; t++) {
+            const McFile &F = tile[t];
+            // MayContain (sstable.go:300-305): a table whose header or filter
+            // did not decode answers false (the Manager never loads one)
+            if (!F.ok) continue;
+            if (bound_cmp_fast(F.lo, F.lo_len, a.img + F.lo_at, kw, kl, kp) > 0 ||
+                bound_cmp_fast(F.hi, F.hi_len, a.img + F.hi_at, kw, kl, kp) < 0)
+                continue;
+            if (!hashed) {
+                sum256(kp, kl, h);
+                hashed = true;
+            }
+            if (!filter_test_any(F, h, a.img)) continue;
+            const int32_t r = get_in_table(a, f0 + t, kw, kl, kp, v);
+            if (r != LSM_GET_ABSENT) {  // a value or an error: the search ends
+                res = r;
+                tab = (int32_t)(f0 + t);
+                done = true;
+            }
+        }
+    }
+    if (act) {
+        a.result[i] = res;
+        a.value[i] = v;
+        table_out[i] = tab;
+    }
 }
 
 template <int G>
@@ -4001,13 +4096,27 @@ extern "C" int lsm_level_get_tree_build(lsm_ctx *ctx, const uint8_t *d_img, cons
     return 0;
 }
 
+// The Seek tree of a Get: it must span nfile tables of tree_nidx entries
+// (a tree built for fewer tables would be read past its end).
+static int get_tree_args(GetArgs &a, uint32_t nfile, const void *d_tree, uint32_t tree_nidx,
+                         size_t tree_bytes) {
+    const TreeShape T = tree_shape(tree_nidx);
+    if (!d_tree || !T.D) return 0;
+    if (tree_bytes < lsm_level_get_tree_bytes(nfile, tree_nidx)) return LSM_ESPACE;
+    a.tree = static_cast<const uint8_t *>(d_tree);
+    a.tree_nidx = tree_nidx;
+    a.tree_top = T.t;
+    a.tree_stride = T.blocks * 128;
+    return 0;
+}
+
 extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
                              const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
                              const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
                              const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
                              uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may,
                              int32_t *d_result, lsm_rec_desc *d_value, const void *d_tree,
-                             uint32_t tree_nidx, void *stream) {
+                             uint32_t tree_nidx, size_t tree_bytes, void *stream) {
     if (!ctx) return LSM_EINVAL;
     if (nkeys == 0) return 0;
     if (!d_keys || !d_koff || !d_table || !d_may || !d_result || !d_value) return LSM_EINVAL;
@@ -4022,17 +4131,40 @@ extern "C" int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t 
     a.may = d_may;
     a.result = d_result;
     a.value = d_value;
-    const TreeShape T = tree_shape(tree_nidx);
-    if (d_tree && T.D) {
-        a.tree = static_cast<const uint8_t *>(d_tree);
-        a.tree_nidx = tree_nidx;
-        a.tree_top = T.t;
-        a.tree_stride = T.blocks * 128;
-    }
+    const int rc = get_tree_args(a, nfile, d_tree, tree_nidx, tree_bytes);
+    if (rc) return rc;
     const uint64_t grid = (nkeys + 255) / 256;
     if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
     hipLaunchKernelGGL(level_get_kernel, dim3((uint32_t)grid), dim3(256), 0,
                        static_cast<hipStream_t>(stream), a);
+    LSM_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int lsm_level0_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                              const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
+                              const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
+                              const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
+                              uint64_t nkeys, int32_t *d_table, int32_t *d_result, lsm_rec_desc *d_value,
+                              const void *d_tree, uint32_t tree_nidx, size_t tree_bytes, void *stream) {
+    if (!ctx) return LSM_EINVAL;
+    if (nkeys == 0) return 0;
+    if (!d_keys || !d_koff || !d_table || !d_result || !d_value) return LSM_EINVAL;
+    if (nfile && (!d_img || !d_file_off || !d_file_len || !d_meta || !d_idx_desc || !d_idx_value))
+        return LSM_EINVAL;
+    GetArgs a = get_args(d_img, d_file_off, d_file_len, d_meta, nfile, d_rec_base, d_idx_desc,
+                         d_idx_value);
+    a.keys = d_keys;
+    a.koff = d_koff;
+    a.nkeys = nkeys;
+    a.result = d_result;
+    a.value = d_value;
+    const int rc = get_tree_args(a, nfile, d_tree, tree_nidx, tree_bytes);
+    if (rc) return rc;
+    const uint64_t grid = (nkeys + kL0Threads - 1) / kL0Threads;
+    if (grid > 0x7FFFFFFFull) return LSM_EINVAL;
+    hipLaunchKernelGGL(level0_get_kernel, dim3((uint32_t)grid), dim3(kL0Threads), 0,
+                       static_cast<hipStream_t>(stream), a, d_table);
     LSM_HIP_CHECK(hipGetLastError());
     return 0;
 }

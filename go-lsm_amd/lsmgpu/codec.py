@@ -542,7 +542,8 @@ def level_get_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "Reco
         _ptr(r.idx_desc) if r.nfile else None, _ptr(r.idx_value) if r.nfile else None,
         _ptr(batch.keys), _ptr(batch.koff), batch.n, _ptr(table), _ptr(may), _ptr(result),
         _ptr(value), _ptr(tree.data) if tree is not None else None,
-        tree.max_nidx if tree is not None else 0, _stream_handle(stream)), "lsm_level_get")
+        tree.max_nidx if tree is not None else 0, tree.data.numel() if tree is not None else 0,
+        _stream_handle(stream)), "lsm_level_get")
 
 
 def level_get(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
@@ -554,6 +555,34 @@ def level_get(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBat
     if batch.n:
         level_get_into(ctx, d_img, r, batch, table, may, result, value, tree=tree, stream=stream)
     return result[:batch.n], value[:batch.n]
+
+
+def level0_get_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                    table: torch.Tensor, result: torch.Tensor, value: torch.Tensor,
+                    tree: Optional[SeekTree] = None, stream=None) -> None:
+    """lsm_level0_get: searchFromLevel0 (manager.go:160-176) over r's tables in
+    order (newest first): MayContain, Seek and the value per table until the
+    first value or error.  table int32 per key (the answering table or -1),
+    result / value as level_get_into."""
+    _lib.check(ctx.lib.lsm_level0_get(
+        ctx.handle, _ptr(d_img) if r.nfile else None, _ptr(r.d_file_off) if r.nfile else None,
+        _ptr(r.d_file_len) if r.nfile else None, _ptr(r.meta) if r.nfile else None, r.nfile, None,
+        _ptr(r.idx_desc) if r.nfile else None, _ptr(r.idx_value) if r.nfile else None,
+        _ptr(batch.keys), _ptr(batch.koff), batch.n, _ptr(table), _ptr(result), _ptr(value),
+        _ptr(tree.data) if tree is not None else None, tree.max_nidx if tree is not None else 0,
+        tree.data.numel() if tree is not None else 0, _stream_handle(stream)), "lsm_level0_get")
+
+
+def level0_get(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+               tree: Optional[SeekTree] = None, stream=None):
+    """-> (table int32[nkeys], result int32[nkeys], value int32[nkeys, 4]) on the device."""
+    dev = ctx.torch_device
+    table = torch.empty(max(batch.n, 1), dtype=torch.int32, device=dev)
+    result = torch.empty(max(batch.n, 1), dtype=torch.int32, device=dev)
+    value = torch.empty((max(batch.n, 1), 4), dtype=torch.int32, device=dev)
+    if batch.n:
+        level0_get_into(ctx, d_img, r, batch, table, result, value, tree=tree, stream=stream)
+    return table[:batch.n], result[:batch.n], value[:batch.n]
 
 
 # ---- encode -----------------------------------------------------------------

@@ -324,7 +324,8 @@ int lsm_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_o
  * decode, answers 0 -- go-lsm's Manager.Recover (manager.go:226-275) would
  * have failed on such a file and never listed it in the level, so the
  * reference has no answer to restate; filter deviations as lsm_may_contain.  Level 0 (searchFromLevel0, :160-176, every table in
- * order) is lsm_may_contain.  Workspace: lsm_level_may_contain_workspace_bytes. */
+ * order): lsm_may_contain for the may-bits, lsm_level0_get for the Get.
+ * Workspace: lsm_level_may_contain_workspace_bytes. */
 size_t lsm_level_may_contain_workspace_bytes(uint32_t nfile, uint64_t nkeys);
 int lsm_level_may_contain(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
                           const lsm_sst_meta *d_meta, uint32_t nfile, const uint8_t *d_keys,
@@ -362,7 +363,12 @@ int lsm_level_may_contain_indexed(lsm_ctx *ctx, const uint8_t *d_img, const void
  * d_tree (or NULL) is the level's Seek tree from lsm_level_get_tree_build
  * over the same decoded tables with max_nidx = tree_nidx; tables with more
  * index entries than that walk the index.  The steps are Go's either way, so
- * the answers are the same with and without the tree. */
+ * the answers are the same with and without the tree.  tree_bytes (ABI 7) is
+ * the tree buffer's size: below lsm_level_get_tree_bytes(nfile, tree_nidx) (a
+ * tree built for fewer tables) the call returns LSM_ESPACE.  A tree built for
+ * an earlier state of the level with the same shape cannot be detected: the
+ * caller rebuilds it whenever the level's tables change, as it re-decodes
+ * them. */
 enum lsm_get_result {
     LSM_GET_ABSENT = 0,         /* (nil, nil): not MayContain, or no entry equals the key        */
     LSM_GET_FOUND = 1,          /* the value, d_value[i]                                          */
@@ -376,7 +382,28 @@ int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off
                   const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
                   const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
                   uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may, int32_t *d_result,
-                  lsm_rec_desc *d_value, const void *d_tree, uint32_t tree_nidx, void *stream);
+                  lsm_rec_desc *d_value, const void *d_tree, uint32_t tree_nidx, size_t tree_bytes,
+                  void *stream);
+
+/* Batched Manager.searchFromLevel0 (sstable/manager.go:160-176) for level 0,
+ * whose tables overlap: the nfile images are the level's tables in the
+ * Manager's order (newest first -- addNewSSTables prepends, manager.go:
+ * 284-287), with lsm_decode_sst's outputs as for lsm_level_get.  Per key i,
+ * searchFromTable (:209-223) on table 0, 1, ...: MayContain (sstable.go:
+ * 300-305: the range check, then Filter.Test), Iterator.Seek, the value; a
+ * false positive or a Seek miss goes on to the next table, the first value or
+ * error ends the search (`return nil, err`).  d_table[i] = the table that
+ * answered (LSM_GET_FOUND or an error code in d_result[i], the value's view
+ * in d_value[i] as lsm_level_get), -1 with LSM_GET_ABSENT when none did.
+ * MayContain's deviations are lsm_may_contain's (corrupted filters only).
+ * d_tree / tree_nidx / tree_bytes as lsm_level_get (the level-0 tables'
+ * Seek tree, or NULL). */
+int lsm_level0_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off,
+                   const uint64_t *d_file_len, const lsm_sst_meta *d_meta, uint32_t nfile,
+                   const uint64_t *d_rec_base, const lsm_rec_desc *d_idx_desc,
+                   const int64_t *d_idx_value, const uint8_t *d_keys, const uint64_t *d_koff,
+                   uint64_t nkeys, int32_t *d_table, int32_t *d_result, lsm_rec_desc *d_value,
+                   const void *d_tree, uint32_t tree_nidx, size_t tree_bytes, void *stream);
 
 /* The Seek tree of a level for lsm_level_get, built once when the level is
  * loaded (the Manager keeps each table's decoded IndexBlock in memory,

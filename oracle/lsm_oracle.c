@@ -694,10 +694,43 @@ void ora_level_may_contain(const uint8_t *img, const uint64_t *file_off, const o
     }
 }
 
-/* searchFromTable past MayContain (sstable/manager.go:209-223): Iterator.Seek
- * (sstable/block/index.go:157-181) over the table's decoded IndexBlock, then
- * Iterator.Value (sstable/iterator.go:34-46) -> GetValueByOffset
- * (sstable.go:271-296) -> Value.DecodeFrom (kv.go:181-200) reading the file. */
+/* searchFromTable past MayContain (sstable/manager.go:209-223) on table t:
+ * Iterator.Seek (sstable/block/index.go:157-181) over the table's decoded
+ * IndexBlock, then Iterator.Value (sstable/iterator.go:34-46) ->
+ * GetValueByOffset (sstable.go:271-296) -> Value.DecodeFrom (kv.go:181-200)
+ * reading the file.  -> an ORA_GET_* code; the value's view on FOUND. */
+static int32_t get_one(const uint8_t *img, const uint64_t *file_off, const uint64_t *file_len,
+                       const ora_sst_meta *meta, const ora_desc *idx_desc, const int64_t *idx_val,
+                       const uint64_t *idx_base, uint32_t t, const uint8_t *key, uint64_t kl,
+                       uint64_t *val_off, uint32_t *val_len) {
+    const uint8_t *file = img + file_off[t];
+    const ora_desc *D = idx_desc + idx_base[t];
+    const int64_t *V = idx_val + idx_base[t];
+    const uint64_t n = meta[t].nidx;
+    /* Seek: left, right := 0, len; for left < right { mid := left + (right-left)/2;
+     * if Indexes[mid].Key < target { left = mid + 1 } else { right = mid } } */
+    uint64_t left = 0, right = n;
+    while (left < right) {
+        const uint64_t mid = left + (right - left) / 2;
+        if (go_strcmp(file + D[mid].rec_off + 4, D[mid].key_len, key, kl) < 0) left = mid + 1;
+        else right = mid;
+    }
+    /* out of range or not an exact match: invalid, it.Valid() false -> (nil, nil) */
+    if (left >= n || go_strcmp(file + D[left].rec_off + 4, D[left].key_len, key, kl) != 0)
+        return ORA_GET_ABSENT;
+    const int64_t off = V[left];
+    if (off < 0) return ORA_GET_SEEK_FAILED; /* file.Seek: negative position */
+    const uint64_t fl = file_len[t];
+    const uint64_t rem = (uint64_t)off < fl ? fl - (uint64_t)off : 0;
+    if (rem < 4) return ORA_GET_VALUE_LENGTH; /* binary.Read: EOF */
+    const uint32_t vl = ld_u32le(file + off);
+    if (vl > (1u << 30)) return ORA_GET_VALUE_TOO_LONG;
+    if (rem - 4 < vl) return ORA_GET_VALUE_SHORT; /* io.ReadFull */
+    *val_off = file_off[t] + (uint64_t)off;
+    *val_len = vl;
+    return ORA_GET_FOUND;
+}
+
 void ora_level_get(const uint8_t *img, const uint64_t *file_off, const uint64_t *file_len,
                    const ora_sst_meta *meta, const ora_desc *idx_desc, const int64_t *idx_val,
                    const uint64_t *idx_base, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
@@ -709,35 +742,39 @@ void ora_level_get(const uint8_t *img, const uint64_t *file_off, const uint64_t 
         val_off[o] = 0;
         val_len[o] = 0;
         if (!may[o] || table[o] < 0) continue; /* searchFromTable: !MayContain -> (nil, nil) */
-        const uint32_t t = (uint32_t)table[o];
-        const uint8_t *file = img + file_off[t];
-        const ora_desc *D = idx_desc + idx_base[t];
-        const int64_t *V = idx_val + idx_base[t];
-        const uint64_t n = meta[t].nidx;
+        res[o] = get_one(img, file_off, file_len, meta, idx_desc, idx_val, idx_base, (uint32_t)table[o],
+                         keys + koff[i], koff[i + 1] - koff[i], &val_off[o], &val_len[o]);
+    }
+}
+
+/* Manager.searchFromLevel0 (sstable/manager.go:160-176): every level-0 table
+ * in the Manager's order (newest first: addNewSSTables prepends,
+ * manager.go:284-287), searchFromTable (:209-223) on each -- MayContain
+ * (sstable.go:300-305), then Seek and the value -- and the first non-nil
+ * value wins; an error ends the search (`return nil, err`).  table[o] = the
+ * table that answered (FOUND or an error), -1 when none did. */
+void ora_level0_get(const uint8_t *img, const uint64_t *file_off, const uint64_t *file_len,
+                    const ora_sst_meta *meta, uint32_t nfile, const ora_desc *idx_desc,
+                    const int64_t *idx_val, const uint64_t *idx_base, const uint8_t *keys,
+                    const uint64_t *koff, uint64_t k0, uint64_t k1, int32_t *table, int32_t *res,
+                    uint64_t *val_off, uint32_t *val_len) {
+    for (uint64_t i = k0; i < k1; i++) {
+        const uint64_t o = i - k0;
         const uint8_t *key = keys + koff[i];
         const uint64_t kl = koff[i + 1] - koff[i];
-        /* Seek: left, right := 0, len; for left < right { mid := left + (right-left)/2;
-         * if Indexes[mid].Key < target { left = mid + 1 } else { right = mid } } */
-        uint64_t left = 0, right = n;
-        while (left < right) {
-            const uint64_t mid = left + (right - left) / 2;
-            if (go_strcmp(file + D[mid].rec_off + 4, D[mid].key_len, key, kl) < 0) left = mid + 1;
-            else right = mid;
+        res[o] = ORA_GET_ABSENT;
+        table[o] = -1;
+        val_off[o] = 0;
+        val_len[o] = 0;
+        for (uint32_t t = 0; t < nfile; t++) {
+            if (!may_contain_one(img + file_off[t], &meta[t], key, kl)) continue; /* (nil, nil) */
+            const int32_t r = get_one(img, file_off, file_len, meta, idx_desc, idx_val, idx_base, t, key,
+                                      kl, &val_off[o], &val_len[o]);
+            if (r == ORA_GET_ABSENT) continue; /* val == nil: the next table */
+            res[o] = r;
+            table[o] = (int32_t)t;
+            break;
         }
-        /* out of range or not an exact match: invalid, it.Valid() false -> (nil, nil) */
-        if (left >= n || go_strcmp(file + D[left].rec_off + 4, D[left].key_len, key, kl) != 0)
-            continue;
-        const int64_t off = V[left];
-        if (off < 0) { res[o] = ORA_GET_SEEK_FAILED; continue; } /* file.Seek: negative position */
-        const uint64_t fl = file_len[t];
-        const uint64_t rem = (uint64_t)off < fl ? fl - (uint64_t)off : 0;
-        if (rem < 4) { res[o] = ORA_GET_VALUE_LENGTH; continue; } /* binary.Read: EOF */
-        const uint32_t vl = ld_u32le(file + off);
-        if (vl > (1u << 30)) { res[o] = ORA_GET_VALUE_TOO_LONG; continue; }
-        if (rem - 4 < vl) { res[o] = ORA_GET_VALUE_SHORT; continue; } /* io.ReadFull */
-        res[o] = ORA_GET_FOUND;
-        val_off[o] = file_off[t] + (uint64_t)off;
-        val_len[o] = vl;
     }
 }
 

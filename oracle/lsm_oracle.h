@@ -194,6 +194,14 @@ void ora_level_get(const uint8_t *img, const uint64_t *file_off, const uint64_t 
                    const uint64_t *idx_base, const uint8_t *keys, const uint64_t *koff, uint64_t k0,
                    uint64_t k1, const int32_t *table, const uint8_t *may, int32_t *res,
                    uint64_t *val_off, uint32_t *val_len);
+/* Manager.searchFromLevel0 (manager.go:160-176): every table in order,
+ * searchFromTable on each, the first non-nil value or error wins; table[o] =
+ * the answering table or -1. */
+void ora_level0_get(const uint8_t *img, const uint64_t *file_off, const uint64_t *file_len,
+                    const ora_sst_meta *meta, uint32_t nfile, const ora_desc *idx_desc,
+                    const int64_t *idx_val, const uint64_t *idx_base, const uint8_t *keys,
+                    const uint64_t *koff, uint64_t k0, uint64_t k1, int32_t *table, int32_t *res,
+                    uint64_t *val_off, uint32_t *val_len);
 
 /* ---- compaction merge ----------------------------- */
 

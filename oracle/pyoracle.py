@@ -55,6 +55,8 @@ def lib():
         "ora_may_contain_batch": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp]),
         "ora_level_may_contain": (None, [vp, vp, vp, ctypes.c_uint32, vp, vp, u64, u64, vp, vp]),
         "ora_level_get": (None, [vp, vp, vp, vp, vp, vp, vp, vp, vp, u64, u64, vp, vp, vp, vp, vp]),
+        "ora_level0_get": (None, [vp, vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, u64, u64, vp, vp,
+                                  vp, vp]),
         "ora_estimate_parameters": (None, [u64, ctypes.c_double, vp, vp]),
         "ora_filter_block_size": (u64, [u64]),
         "ora_filter_encode": (u64, [vp, u64, u64, vp]),
@@ -375,3 +377,26 @@ def level_get(img, file_off, file_len, metas, idx_descs, idx_vals, keys, koff, k
                         _p(base), _p(keys), _p(koff), k0, k1, _p(table), _p(may), _p(res), _p(voff),
                         _p(vlen))
     return res[:n], voff[:n], vlen[:n]
+
+
+def level0_get(img, file_off, file_len, metas, idx_descs, idx_vals, keys, koff, k0, k1, index=None):
+    """Manager.searchFromLevel0 (manager.go:160-176) for keys [k0, k1): every
+    table in order (newest first), searchFromTable on each; the first value or
+    error wins.  -> (int32 table, int32 res, uint64 val_off, uint32 val_len)."""
+    img = _bytes(img)
+    nfile = len(metas)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64) if nfile else np.zeros(1, np.uint64)
+    file_len = np.ascontiguousarray(file_len, dtype=np.uint64) if nfile else np.zeros(1, np.uint64)
+    arr = metas if isinstance(metas, ctypes.Array) else (SstMeta * max(nfile, 1))(*metas)
+    desc, vals, base = index if index is not None else level_get_index(idx_descs, idx_vals)
+    keys = _bytes(keys) if len(keys) else np.zeros(1, np.uint8)
+    koff = np.ascontiguousarray(koff, dtype=np.uint64)
+    n = k1 - k0
+    table = np.zeros(max(n, 1), np.int32)
+    res = np.zeros(max(n, 1), np.int32)
+    voff = np.zeros(max(n, 1), np.uint64)
+    vlen = np.zeros(max(n, 1), np.uint32)
+    lib().ora_level0_get(_p(img), _p(file_off), _p(file_len), ctypes.cast(arr, vp), nfile, _p(desc),
+                         _p(vals), _p(base), _p(keys), _p(koff), k0, k1, _p(table), _p(res), _p(voff),
+                         _p(vlen))
+    return table[:n], res[:n], voff[:n], vlen[:n]
