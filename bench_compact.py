@@ -146,11 +146,13 @@ def bench_compact(args, world, rank, local):
         ids = np.concatenate(level0_ids(n1, first, rank) + [np.arange(first, first + n1)])
         ranks = (ids - first).astype(np.uint32)
         assert ranks.size == n
-        rep = []
+        rep, push, pop = [], [], []
         for _ in range(3):
             t0 = time.perf_counter()
-            lsmgpu.goheap_pop_order(ctx, ranks)
+            _, pu, po = lsmgpu.goheap_pop_order(ctx, ranks, phases=True)
             rep.append(time.perf_counter() - t0)
+            push.append(pu)
+            pop.append(po)
         evi = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(3)]
         for s_ in range(3):
             step(evi[s_], tie=lsmgpu.TIE_INPUT)
@@ -158,6 +160,9 @@ def bench_compact(args, world, rank, local):
         merge_in = float(np.mean([e[2].elapsed_time(e[3]) for e in evi]))
         goheap = {"replay_host_ms": round(min(rep) * 1e3, 2),
                   "replay_host_ms_mean": round(float(np.mean(rep)) * 1e3, 2),
+                  "push_ms": round(float(np.median(push)), 2),
+                  "pop_ms": round(float(np.median(pop)), 2),
+                  "replays_in_timed_steps": int(ctx.lib.lsm_goheap_replays(ctx.handle)),
                   "merge_stage_ms": round(stage_ms["merge"], 3),
                   "merge_stage_input_order_ms": round(merge_in, 4),
                   "chain_ms": round(elapsed * 1e3 / steps, 3),

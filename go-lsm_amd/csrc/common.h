@@ -29,6 +29,9 @@ struct lsm_ctx {
     // pop-order upload (pageable copies staged through the runtime: slower)
     void *host_big;
     size_t host_big_bytes;
+    // LSM_TIE_GOHEAP calls that replayed the heap (keys with duplicates;
+    // distinct keys skip the replay): lsm_goheap_replays
+    uint64_t goheap_replays;
 };
 constexpr size_t kHostReadback = 256 * 1024;
 

@@ -940,6 +940,7 @@ struct SstArgs {
     // for the file-major grid of lsm_build_sst
     const uint32_t *span_file;
     const struct FileDesc *desc;
+    const uint32_t *plan;  // {nfile, spans, common span count, 0}
 };
 
 // One file of a stream build, as the plan kernel lays it out: records
@@ -1229,8 +1230,11 @@ __global__ __launch_bounds__(kRegWaves *kWave) void sst_regions_kernel(SstArgs a
     SstLayout L;
     uint64_t c0, imgo, Ks, Vs, K0;
     if (Desc) {
-        const uint32_t f = a.span_file[blockIdx.x];
-        if (f == ~0u) return;
+        // span j's file: j / the common span count when every file but the
+        // last has it (files of one record size: no table), else the table
+        const uint32_t j = blockIdx.x, nf = a.plan[0], nsp = a.plan[2];
+        if (j >= a.plan[1]) return;
+        const uint32_t f = nsp ? min(j / nsp, nf - 1) : a.span_file[j];
         const FileDesc D = a.desc[f];
         L.s = D.s;
         L.e = D.e;
@@ -1358,8 +1362,18 @@ struct StreamPlanArgs {
     uint64_t *file_off;    // nfile_max + 1, or null (the rule alone)
     FileDesc *desc;        // nfile_max, or null
     uint32_t *span_file;   // span_max, or null
+    uint32_t *plan;        // 4: {nfile, spans, the common span count or 0, 0}
     uint64_t *counts;      // {nfile, most records in a file, image bytes, overflow}
 };
+
+// The plan kernel's barrier: LDS only.  A __syncthreads() also waits for
+// the workgroup's global stores to complete (its release fence): after the
+// file starts, descriptors and span table were stored that cost ~3.5 us per
+// launch.  Global data one thread wrote and another reads back (file starts
+// past kSegLdsFiles) takes a __syncthreads() of its own.
+__device__ __forceinline__ void seg_barrier() {
+    __asm__ __volatile__("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 struct SegPair {
     uint64_t s, c;
@@ -1376,7 +1390,7 @@ __device__ __forceinline__ SegPair seg_block_scan2(uint64_t s, uint64_t c, SegPa
         ws_[w] = ts;
         wc_[w] = tc;
     }
-    __syncthreads();
+    seg_barrier();
     uint64_t ps = 0, pc = 0, as = 0, ac = 0;
     for (uint32_t i = 0; i < NW; i++) {
         if (i < w) {
@@ -1386,9 +1400,20 @@ __device__ __forceinline__ SegPair seg_block_scan2(uint64_t s, uint64_t c, SegPa
         as += ws_[i];
         ac += wc_[i];
     }
-    __syncthreads();
+    seg_barrier();
     *total = SegPair{as, ac};
     return SegPair{ps + xs, pc + xc};
+}
+
+// The largest value over the wave (lane 0 holds it, as every lane).
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint64_t o = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d) << 32 |
+                           (uint32_t)__shfl_xor((int)(uint32_t)v, d);
+        v = o > v ? o : v;
+    }
+    return v;
 }
 
 __device__ __forceinline__ uint64_t est_at(const uint64_t *koff, const uint64_t *voff, uint64_t t) {
@@ -1451,10 +1476,20 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
     __shared__ uint64_t s_carry, s_scarry, s_maxr;
     const uint32_t tid = threadIdx.x;
     const uint64_t n = a.n, T = a.T;
-    // every thread reads the stream's ends itself (the same two lines: no
-    // round trip through thread 0 and a barrier)
-    const uint64_t Sn = n ? est_at(a.koff, a.voff, n) : 0;
+    // every thread reads the stream's ends itself (the same lines: no round
+    // trip through thread 0 and a barrier); koff[n - 1] for the last file's
+    // layout
+    const uint64_t kn = n ? a.koff[n] : 0, vn = n ? a.voff[n] : 0, knm = n ? a.koff[n - 1] : 0;
+    const uint64_t Sn = 16 * n + kn + vn;
     const uint64_t S0 = n ? est_at(a.koff, a.voff, 0) : 0;
+    // Round 1 (W = 1) leaves slot tid's file layout inputs in registers --
+    // koff at the file's first two and last two records, voff at its ends --
+    // so that when that round resolves every file (records of one size) the
+    // layout below reads nothing: thread tid is file tid's slot and its
+    // layout thread.
+    uint64_t rk0 = 0, rk01 = 0, rk1m = 0, rk1 = 0, rv0 = 0, rv1 = 0;
+    bool rhave = false;
+    uint32_t rounds = 0;
     if (tid == 0) {
         s_cur = 0;
         s_nf = 0;
@@ -1465,7 +1500,7 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
         const double g = tot ? ceil((double)T * (double)n / (double)tot) : 1.0;
         s_G = g < 1.0 ? 1 : (g > 4.0e18 ? (uint64_t)4e18 : (uint64_t)g);
     }
-    __syncthreads();
+    seg_barrier();
     if (n && T == 0) {  // never flush (BuildSSTableFromIMemTable): one file
         if (tid == 0) {
             if (a.nfile_max >= 1) {
@@ -1477,7 +1512,7 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
             }
             s_cur = n;
         }
-        __syncthreads();
+        seg_barrier();
     }
     for (;;) {
         const uint64_t cur = s_cur;
@@ -1499,25 +1534,41 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
             // S(P) and the predicted end's bracket S(g - 1), S(g) in one
             // round trip (T > 0 here, so S(P) < target: g = P + 1 is covered)
             const uint64_t g = P + G < n ? P + G : n;
-            const uint64_t sp = est_at(a.koff, a.voff, P);
-            const uint64_t sa = est_at(a.koff, a.voff, g - 1), sb = est_at(a.koff, a.voff, g);
+            const uint64_t kp = a.koff[P], vp = a.voff[P], kp1 = a.koff[P + 1];
+            const uint64_t kg1 = a.koff[g - 1], vg1 = a.voff[g - 1], kg = a.koff[g], vg = a.voff[g];
+            const uint64_t sp = 16 * P + kp + vp;
+            const uint64_t sa = 16 * (g - 1) + kg1 + vg1, sb = 16 * g + kg + vg;
             const uint64_t target = sp + T;
-            nx = Sn < target ? n : (sb >= target && sa < target ? g : seg_next(a.koff, a.voff, P, n, target, g));
+            const bool bracket = sb >= target && sa < target;
+            nx = Sn < target ? n : (bracket ? g : seg_next(a.koff, a.voff, P, n, target, g));
+            if (rounds == 0 && W == 1) {
+                rk0 = kp;
+                rk01 = kp1;
+                rv0 = vp;
+                // the file's end: the bracket's g, or the stream's end
+                rhave = Sn < target || bracket;
+                rk1m = Sn < target ? knm : kg1;
+                rk1 = Sn < target ? kn : kg;
+                rv1 = Sn < target ? vn : vg;
+            }
         }
         s_pos[tid] = P;
         s_nxt[tid] = nx;
         if (tid == 0) s_brk = R - 1;
-        __syncthreads();
+        seg_barrier();
         uint32_t adv = 0;  // files whose start this round resolved
         uint64_t ncur = cur;
         if (W == 1) {
             // slot tid is the chain's last of this round if its next() is
-            // not slot tid + 1's prediction (or ends the stream)
-            if (tid < R - 1 && s_nxt[tid] != kSegNone &&
-                (s_nxt[tid] >= n || s_nxt[tid] != s_pos[tid + 1]))
-                atomicMin(&s_brk, tid);
-            if (tid < R - 1 && s_nxt[tid] == kSegNone) atomicMin(&s_brk, tid);
-            __syncthreads();
+            // not slot tid + 1's prediction (or ends the stream, or the slot
+            // has no position); the first such slot by a ballot per wave and
+            // one LDS atomic per wave (an atomic per thread serialized ~800
+            // of them on one address: 3 us)
+            const bool brk = tid < R - 1 && (s_nxt[tid] == kSegNone || s_nxt[tid] >= n ||
+                                             s_nxt[tid] != s_pos[tid + 1]);
+            const uint64_t bb = __ballot(brk);
+            if (bb && lane_id() == 0) atomicMin(&s_brk, (tid & ~(kWave - 1)) + (uint32_t)__builtin_ctzll(bb));
+            seg_barrier();
             const uint32_t J = s_brk;  // slots 0 .. J are starts; slot J's next() is exact
             adv = J + 1;
             ncur = s_nxt[J];
@@ -1551,11 +1602,11 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
                 s_brk = k - nf;
                 s_pos[0] = c;
             }
-            __syncthreads();
+            seg_barrier();
             adv = s_brk;
             ncur = s_pos[0];
         }
-        __syncthreads();
+        seg_barrier();
         if (tid == 0) {
             if (adv) {
                 const uint64_t g = (ncur - cur + adv / 2) / adv;  // mean records per file
@@ -1565,9 +1616,13 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
             s_cur = ncur;
             s_nf = nf + adv;
         }
-        __syncthreads();
+        rounds++;
+        seg_barrier();
     }
+    // the registers hold file tid's inputs when round 1 resolved every file
+    rhave = rhave && rounds == 1 && s_cur >= n && !s_over;
     const uint32_t nfile = s_over ? 0 : s_nf;
+    if (!a.file_off && nfile > kSegLdsFiles) __syncthreads();  // as below, for the rule alone
     if (tid == 0) {
         a.file_start[nfile] = n;
         if (nfile <= kSegLdsFiles) s_fs[nfile] = n;
@@ -1577,7 +1632,7 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
         s_scarry = 0;
         s_maxr = 0;
     }
-    __syncthreads();
+    seg_barrier();
     if (!a.file_off) {
         // the rule alone: the most records in one file
         uint64_t mr = 0;
@@ -1586,18 +1641,20 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
                                (f <= kSegLdsFiles ? s_fs[f] : a.file_start[f]);
             mr = r > mr ? r : mr;
         }
-        __syncthreads();
-        if (mr) atomicMax((unsigned long long *)&s_maxr, (unsigned long long)mr);
-        __syncthreads();
+        mr = wave_max64(mr);  // one LDS atomic per wave, not per thread
+        if (lane_id() == 0 && mr) atomicMax((unsigned long long *)&s_maxr, (unsigned long long)mr);
+        seg_barrier();
         if (tid == 0) {
             a.counts[1] = s_maxr;
             a.counts[2] = 0;
         }
         return;
     }
-    __syncthreads();
+    seg_barrier();
+    if (nfile > kSegLdsFiles) __syncthreads();  // the later file starts are read back from global memory
     // layout: sizes, aligned offsets, FileDesc, span starts (tile after tile)
-    __shared__ uint32_t s_span0[kSegThreads + 1];
+    __shared__ uint32_t s_nsp0, s_nonuni;
+    if (tid == 0) s_nonuni = 0;
     for (uint32_t f0 = 0; f0 < nfile; f0 += kSegThreads) {
         const uint32_t f = f0 + tid;
         uint64_t sz = 0, nr = 0, r0 = 0, r1 = 0, k0 = 0, k1 = 0, v0 = 0, v1 = 0, hdr = 8;
@@ -1605,15 +1662,28 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
             r0 = f <= kSegLdsFiles ? s_fs[f] : a.file_start[f];
             r1 = f + 1 <= kSegLdsFiles ? s_fs[f + 1] : a.file_start[f + 1];
             nr = r1 - r0;
-            k0 = a.koff[r0];
-            k1 = a.koff[r1];
-            v0 = a.voff[r0];
-            v1 = a.voff[r1];
-            hdr += (a.koff[r0 + 1] - k0) + (k1 - a.koff[r1 - 1]);  // nr >= 1
+            uint64_t k01, k1m;
+            if (f0 == 0 && rhave) {  // round 1's registers (thread tid = file tid)
+                k0 = rk0;
+                k01 = rk01;
+                k1m = rk1m;
+                k1 = rk1;
+                v0 = rv0;
+                v1 = rv1;
+            } else {
+                k0 = a.koff[r0];
+                k01 = a.koff[r0 + 1];
+                k1m = a.koff[r1 - 1];
+                k1 = a.koff[r1];
+                v0 = a.voff[r0];
+                v1 = a.voff[r1];
+            }
+            hdr += (k01 - k0) + (k1 - k1m);  // nr >= 1
             // Header | Filter | V region (4 + vlen) | IDX region (4 + klen + 8) | Footer
             sz = hdr + a.filter_bytes + 4 * nr + (v1 - v0) + 12 * nr + (k1 - k0) + 32;
         }
         const uint64_t nsp = (nr + kRegSpanRecs - 1) / kRegSpanRecs;
+        if (f == 0) s_nsp0 = (uint32_t)nsp;
         SegPair tot;
         const SegPair x = seg_block_scan2((sz + a.align - 1) / a.align * a.align, nsp, &tot);
         if (f < nfile) {
@@ -1630,30 +1700,42 @@ __global__ __launch_bounds__(kSegThreads) void sst_stream_plan_kernel(StreamPlan
             D.span0 = (uint32_t)(s_scarry + x.c);
             D.pad = 0;
             a.desc[f] = D;
-            s_span0[tid] = D.span0;
-            atomicMax((unsigned long long *)&s_maxr, (unsigned long long)nr);
         }
-        if (tid == 0) s_span0[min(kSegThreads, nfile - f0)] = (uint32_t)(s_scarry + tot.c);
-        __syncthreads();
-        // the span table, one wave per file (lane-strided stores)
-        const uint32_t wv = tid / kWave, nw = kSegThreads / kWave;
-        for (uint32_t g = wv; g < kSegThreads && f0 + g < nfile; g += nw) {
-            const uint32_t b0 = s_span0[g], b1 = s_span0[g + 1];
-            for (uint32_t j = b0 + lane_id(); j < b1; j += kWave) a.span_file[j] = f0 + g;
-        }
-        __syncthreads();
+        const uint64_t wm = wave_max64(nr);  // one LDS atomic per wave
+        if (lane_id() == 0 && wm) atomicMax((unsigned long long *)&s_maxr, (unsigned long long)wm);
+        // every file but the last of one span count: the region writer's span
+        // j is then file j / that count, no table (s_nsp0 was set before the
+        // scan's barriers)
+        const uint64_t nu = __ballot(f + 1 < nfile && nsp != s_nsp0);
+        if (nu && lane_id() == 0) s_nonuni = 1;
+        seg_barrier();
         if (tid == 0) {
             s_carry += tot.s;
             s_scarry += tot.c;
         }
-        __syncthreads();
+        seg_barrier();
     }
-    // spans past the last file's: no work (the grid is sized on the bound)
-    for (uint32_t j = (uint32_t)s_scarry + tid; j < a.span_max; j += kSegThreads) a.span_file[j] = ~0u;
+    if (s_nonuni) {
+        // files of several span counts: the span table, one wave per file
+        // (lane-strided stores), from the descriptors just written
+        __syncthreads();
+        const uint32_t wv = tid / kWave, nw = kSegThreads / kWave;
+        for (uint32_t g = wv; g < nfile; g += nw) {
+            const uint32_t b0 = a.desc[g].span0;
+            const uint32_t b1 = g + 1 < nfile ? a.desc[g + 1].span0 : (uint32_t)s_scarry;
+            for (uint32_t j = b0 + lane_id(); j < b1; j += kWave) a.span_file[j] = g;
+        }
+    }
     if (tid == 0) {
         a.file_off[nfile] = s_carry;
         a.counts[1] = s_maxr;
         a.counts[2] = s_carry;
+        // the region writer's grid header: files, spans, the span count of
+        // every file but the last (0: look spans up in the table)
+        a.plan[0] = nfile;
+        a.plan[1] = (uint32_t)s_scarry;
+        a.plan[2] = s_nonuni ? 0u : s_nsp0;
+        a.plan[3] = 0;
     }
 }
 
@@ -3564,6 +3646,7 @@ static uint64_t barrett_recip(uint64_t m) { return ~0ull / m; }
 struct StreamGrid {
     const uint32_t *span_file;
     const FileDesc *desc;
+    const uint32_t *plan;
     uint32_t span_max;
     const uint64_t *dnf;
 };
@@ -3602,6 +3685,7 @@ static int build_sst_impl(lsm_ctx *ctx, const uint8_t *d_keys, const uint64_t *d
     a.hm = a.hrl = a.hrh = 0;
     a.span_file = sg ? sg->span_file : nullptr;
     a.desc = sg ? sg->desc : nullptr;
+    a.plan = sg ? sg->plan : nullptr;
 
     // Bloom: filter words go straight into each image (big-endian).
     const uint64_t sb = slice_bits_for(m);
@@ -3803,6 +3887,7 @@ static bool stream_split(uint64_t n, uint64_t threshold, uint64_t m, uint32_t k)
 
 struct StreamWs {
     FileDesc *desc;
+    uint32_t *plan;
     uint32_t *span_file;
     void *rest;  // the hash records (split build) or lsm_build_sst's workspace
     size_t rest_bytes;
@@ -3810,6 +3895,8 @@ struct StreamWs {
 static size_t stream_ws_layout(uint8_t *base, uint64_t n, uint64_t threshold, uint32_t nfile_max,
                                uint64_t m, uint32_t k, StreamWs *w) {
     size_t o = 64ull * nfile_max;
+    const size_t pl = o;
+    o += 256;
     const size_t sp = o;
     o += (4 * stream_span_max(n, nfile_max) + 255) / 256 * 256;
     const size_t rest = stream_split(n, threshold, m, k)
@@ -3819,6 +3906,7 @@ static size_t stream_ws_layout(uint8_t *base, uint64_t n, uint64_t threshold, ui
     if (w) {
         w->desc = reinterpret_cast<FileDesc *>(base);
         w->span_file = reinterpret_cast<uint32_t *>(base + sp);
+        w->plan = reinterpret_cast<uint32_t *>(base + pl);
         w->rest = base + o;
         w->rest_bytes = rest;
     }
@@ -3882,6 +3970,7 @@ extern "C" int lsm_build_sst_stream(lsm_ctx *ctx, const uint8_t *d_keys, const u
     p.file_off = d_file_off;
     p.desc = w.desc;
     p.span_file = w.span_file;
+    p.plan = w.plan;
     hipLaunchKernelGGL(sst_stream_plan_kernel, dim3(1), dim3(kSegThreads), 0, s, p);
     LSM_HIP_CHECK(hipGetLastError());
     if (n == 0 || nfile_max == 0) return 0;
@@ -3889,7 +3978,7 @@ extern "C" int lsm_build_sst_stream(lsm_ctx *ctx, const uint8_t *d_keys, const u
     if (stream_split(n, threshold, m, k)) {
         // go-lsm's filter shape: every launch sized on the bounds, the counts
         // stay on the device
-        StreamGrid g{w.span_file, w.desc, (uint32_t)span_max, d_counts};
+        StreamGrid g{w.span_file, w.desc, w.plan, (uint32_t)span_max, d_counts};
         return build_sst_impl(ctx, d_keys, d_koff, d_vals, d_voff, d_file_start, nfile_max, maxr, m, k, d_out,
                               d_file_off, d_footer, w.rest, w.rest_bytes, stream, nullptr, &g);
     }

@@ -40,6 +40,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <vector>
 
 #include "common.h"
@@ -1660,9 +1661,10 @@ uint32_t grid_for(uint64_t n) { return (uint32_t)((n + kMergeThreads - 1) / kMer
 // same array as down() leaves, after every pop.  down()'s child choice is an
 // unpredictable branch per level; here the descent has none, and it prefetches
 // three and four levels ahead (a 64-byte block each).
-void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order) {
+void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order, uint64_t *phase_ns = nullptr) {
     std::vector<uint64_t> h(n ? n : 1);
     uint64_t *H = h.data();
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0; i < n; i++) {  // Push: append, up(h, i)
         const uint64_t x = (uint64_t)rank[i] << 32 | i;
         uint32_t j = i;
@@ -1674,6 +1676,7 @@ void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order) {
         }
         H[j] = x;
     }
+    const auto t1 = std::chrono::steady_clock::now();
     for (uint32_t r = n; r > 0; r--) {  // Pop: swap(0, r-1), down(0, r-1)
         const uint64_t top = H[0], x = H[r - 1];
         const uint32_t m = r - 1, xr = (uint32_t)(x >> 32);
@@ -1701,17 +1704,25 @@ void goheap_pop_order(const uint32_t *rank, uint32_t n, uint32_t *order) {
         H[m] = top;
         order[n - r] = (uint32_t)top;
     }
+    if (phase_ns) {
+        const auto t2 = std::chrono::steady_clock::now();
+        phase_ns[0] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+        phase_ns[1] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+    }
 }
 
 }  // namespace lsm
 
 using namespace lsm;
 
-extern "C" int lsm_goheap_pop_order_host(const uint32_t *rank, uint64_t n, uint32_t *order) {
+extern "C" int lsm_goheap_pop_order_host(const uint32_t *rank, uint64_t n, uint32_t *order,
+                                         uint64_t *phase_ns) {
     if (n >= 0xFFFFFFFFull || (n && (!rank || !order))) return LSM_EINVAL;
-    goheap_pop_order(rank, (uint32_t)n, order);
+    goheap_pop_order(rank, (uint32_t)n, order, phase_ns);
     return 0;
 }
+
+extern "C" uint64_t lsm_goheap_replays(const lsm_ctx *ctx) { return ctx ? ctx->goheap_replays : 0; }
 
 static_assert(sizeof(MergeFile) == 16, "MergeFile layout");
 static_assert(sizeof(SumPair) == 16, "SumPair layout");
@@ -1913,6 +1924,16 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
         hipLaunchKernelGGL(goheap_rank_apply, dim3(ntiles), dim3(kMergeThreads), 0, s, w.csize, N,
                            w.scan_part, perm, rank_d);
         LSM_HIP_CHECK(hipGetLastError());
+        // Every key distinct (N - 1 new-key flags: position 0 has rank 0 and
+        // no flag): the heap pops in key order, the sorted order already is
+        // its pop order -- no replay
+        SumPair *ng = static_cast<SumPair *>(ctx->host_rb);  // pinned
+        LSM_HIP_CHECK(hipMemcpyAsync(ng, w.sc + N, sizeof(SumPair), hipMemcpyDeviceToHost, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));
+        ctx->goheap_replays += ng->s + 1 != N;
+    }
+    if (tie == LSM_TIE_GOHEAP && static_cast<SumPair *>(ctx->host_rb)->s + 1 != N) {
+        uint32_t *rank_d = w.perm[cur ^ 1];
         const size_t need = 8ull * N;  // ranks, then the pop order
         if (ctx->host_big_bytes < need) {
             LSM_HIP_CHECK(hipStreamSynchronize(s));

@@ -150,7 +150,9 @@ SIGNATURES = {
                                                c_u64p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                                                ctypes.c_void_p, c_u64p, c_u64p, ctypes.c_void_p,
                                                ctypes.c_size_t, ctypes.c_void_p]),
-    "lsm_goheap_pop_order_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "lsm_goheap_pop_order_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
+    "lsm_goheap_replays": (ctypes.c_uint64, [ctypes.c_void_p]),
     "lsm_gather_kvs_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint64]),
     "lsm_gather_kvs": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_uint64, c_u8p, c_u64p, c_u8p,

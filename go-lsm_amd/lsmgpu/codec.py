@@ -911,13 +911,17 @@ def merge_kvs(ctx: Context, d_bytes: torch.Tensor, key_desc: torch.Tensor,
     return merge_kvs_into(ctx, d_bytes, key_desc, val_desc, r, level, threshold, stream, tie)
 
 
-def goheap_pop_order(ctx_or_lib, rank: np.ndarray) -> np.ndarray:
-    """lsm_goheap_pop_order_host: container/heap's pop order over key ranks."""
+def goheap_pop_order(ctx_or_lib, rank: np.ndarray, phases: bool = False):
+    """lsm_goheap_pop_order_host: container/heap's pop order over key ranks.
+    phases=True -> (order, push_ms, pop_ms)."""
     lib = ctx_or_lib.lib if isinstance(ctx_or_lib, Context) else ctx_or_lib
     rank = np.ascontiguousarray(rank, dtype=np.uint32)
     order = np.zeros(max(rank.size, 1), np.uint32)
-    _lib.check(lib.lsm_goheap_pop_order_host(rank.ctypes.data, rank.size, order.ctypes.data),
+    ns = np.zeros(2, np.uint64)
+    _lib.check(lib.lsm_goheap_pop_order_host(rank.ctypes.data, rank.size, order.ctypes.data, ns.ctypes.data),
                "lsm_goheap_pop_order_host")
+    if phases:
+        return order[:rank.size], float(ns[0]) / 1e6, float(ns[1]) / 1e6
     return order[:rank.size]
 
 

@@ -548,8 +548,14 @@ int lsm_merge_kvs_tie(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *
                       void *d_ws, size_t ws_bytes, void *stream);
 /* container/heap's pop order over dense key ranks (host, no device): Push of
  * 0 .. n-1, then Pop until empty, Less = rank <; order[j] = the j-th popped
- * index.  What LSM_TIE_GOHEAP replays. */
-int lsm_goheap_pop_order_host(const uint32_t *rank, uint64_t n, uint32_t *order);
+ * index.  What LSM_TIE_GOHEAP replays.  phase_ns (optional, 2 entries): the
+ * nanoseconds of the push and the pop phases (ABI 7).
+ * LSM_TIE_GOHEAP skips the replay when every key is distinct (the device's
+ * group count equals n): the heap then pops in key order, which the sort
+ * already is -- both tie modes give the same output.  lsm_goheap_replays
+ * counts the replays a context has run. */
+int lsm_goheap_pop_order_host(const uint32_t *rank, uint64_t n, uint32_t *order, uint64_t *phase_ns);
+uint64_t lsm_goheap_replays(const lsm_ctx *ctx);
 int lsm_merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
                   const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
                   uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts, void *d_ws,

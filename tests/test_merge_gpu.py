@@ -582,3 +582,23 @@ def test_compact_merge_matches_two_calls_full_size(ctx):
     for tie in TIES:
         c = _compare_compact_merge(ctx, img, r, 1, MiB2, tie)
         assert c[1] >= 200
+
+
+def test_goheap_distinct_keys_skip_the_replay(ctx):
+    """LSM_TIE_GOHEAP on distinct keys: the device's group count equals n, the
+    heap would pop in key order, so the host replay is skipped
+    (lsm_goheap_replays unchanged) and the output equals both oracle modes
+    bit for bit; one duplicate key brings the replay back."""
+    rng = random.Random(77)
+    keys = rng.sample(range(10 ** 6), 5000)
+    pairs = [(b"dk%07d" % k, bytes(rng.randint(0, 255) for _ in range(rng.randint(0, 30)))) for k in keys]
+    for level, threshold in ((1, MiB2), (6, 700), (1, 1)):
+        before = ctx.lib.lsm_goheap_replays(ctx.handle)
+        _, _, _, _, got, starts = run(ctx, pairs, level, threshold, tie=lsmgpu.TIE_GOHEAP)
+        assert ctx.lib.lsm_goheap_replays(ctx.handle) == before, "a replay ran on distinct keys"
+        _, _, _, _, got_in, starts_in = run(ctx, pairs, level, threshold, tie=lsmgpu.TIE_INPUT)
+        assert np.array_equal(got, got_in) and np.array_equal(starts, starts_in)
+    dup = pairs + [(pairs[17][0], b"newer")]
+    before = ctx.lib.lsm_goheap_replays(ctx.handle)
+    run(ctx, dup, 1, MiB2, tie=lsmgpu.TIE_GOHEAP)
+    assert ctx.lib.lsm_goheap_replays(ctx.handle) == before + 1
