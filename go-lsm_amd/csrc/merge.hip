@@ -1763,12 +1763,21 @@ static int merge_path(const MergeWs &w, const MergeIn &m, const SortGroup &g, ui
 static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d_key_desc,
                      const lsm_rec_desc *d_val_desc, uint64_t n, int level, uint64_t threshold,
                      int tie, uint32_t *d_out, uint64_t *d_file_start, uint64_t *h_counts,
-                     uint64_t *d_counts, void *d_ws, size_t ws_bytes, void *stream) {
+                     uint64_t *d_counts, void *d_ws, size_t ws_bytes, void *stream,
+                     const uint64_t *d_expect_n = nullptr) {
     if (!ctx || (!h_counts && !d_counts) || threshold == 0 || n >= 0xFFFFFFFFull) return LSM_EINVAL;
     if (tie != LSM_TIE_INPUT && tie != LSM_TIE_GOHEAP) return LSM_EINVAL;
     if (n && (!d_bytes || !d_key_desc || !d_out || !d_ws)) return LSM_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (h_counts) h_counts[0] = h_counts[1] = h_counts[2] = 0;
+    // d_expect_n (lsm_compact_merge_async): the join's pair count, computed on
+    // the device, read back with the key statistics and checked against n
+    uint64_t *expect_h = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(ctx->host_rb) + kHostReadback - 64);
+    if (n == 0 && d_expect_n) {
+        LSM_HIP_CHECK(hipMemcpyAsync(expect_h, d_expect_n, 8, hipMemcpyDeviceToHost, s));
+        LSM_HIP_CHECK(hipStreamSynchronize(s));
+        if (*expect_h != 0) return LSM_EINVAL;
+    }
     if (n == 0) {
         if (d_file_start) LSM_HIP_CHECK(hipMemsetAsync(d_file_start, 0, 8, s));
         if (d_counts) LSM_HIP_CHECK(hipMemsetAsync(d_counts, 0, 24, s));
@@ -1784,10 +1793,12 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
     //    tiles, per-tile partials reduced here
     const uint32_t chunk = (N + sb - 1) / sb;
     hipLaunchKernelGGL(merge_stats_kernel, dim3(sb), dim3(kMergeThreads), 0, s, m, chunk, w.part);
-    static_assert((size_t)kStatBlocks * kStatWords * 8 + 64 <= kHostReadback, "read-back buffer");
+    static_assert((size_t)kStatBlocks * kStatWords * 8 + 64 <= kHostReadback - 64, "read-back buffer");
     const uint64_t *part = static_cast<const uint64_t *>(ctx->host_rb);  // pinned
     LSM_HIP_CHECK(hipMemcpyAsync(ctx->host_rb, w.part, (size_t)sb * kStatWords * 8, hipMemcpyDeviceToHost, s));
+    if (d_expect_n) LSM_HIP_CHECK(hipMemcpyAsync(expect_h, d_expect_n, 8, hipMemcpyDeviceToHost, s));
     LSM_HIP_CHECK(hipStreamSynchronize(s));
+    if (d_expect_n && *expect_h != n) return LSM_EINVAL;  // n is not the join's pair count
     uint64_t st[kStatCore];
     for (uint32_t t = 0; t < kStatCore; t++) st[t] = part[t];
     uint64_t run_s = 0, run_e = 0, cur_s = 0;  // the longest run found, the open one
@@ -2121,7 +2132,7 @@ extern "C" int lsm_compact_merge_async(lsm_ctx *ctx, const uint8_t *d_img, const
                                  d_val_out, d_prefix, stream);
     if (rc) return rc;
     return merge_kvs(ctx, d_img, d_key_out, d_val_out, n, level, threshold, tie, d_out, d_file_start,
-                     nullptr, d_counts, d_ws, ws_bytes, stream);
+                     nullptr, d_counts, d_ws, ws_bytes, stream, d_prefix + nfile);
 }
 
 extern "C" int lsm_sst_pairs(lsm_ctx *ctx, const lsm_sst_meta *d_meta, const uint64_t *d_file_off,

@@ -597,7 +597,9 @@ int lsm_gather_kvs_dev(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc 
  * decoded), known to the caller; outputs, workspace
  * (lsm_merge_kvs_workspace_bytes(n)) and d_counts exactly as the two calls.
  * Waits on the host for the merge's key statistics, as lsm_merge_kvs_async
- * does.  (Statistics taken before the join, to overlap their read-back with
+ * does; the join's own count d_prefix[nfile] comes back with them, and a call
+ * whose n differs returns LSM_EINVAL before any pass indexes past the join
+ * (the join's outputs and the statistics pass are then the only work done).  (Statistics taken before the join, to overlap their read-back with
  * it, measured slower and are not used: DESIGN.md section 7.) */
 int lsm_compact_merge_async(lsm_ctx *ctx, const uint8_t *d_img, const lsm_sst_meta *d_meta,
                             const uint64_t *d_file_off, uint32_t nfile, const lsm_rec_desc *d_idx_desc,

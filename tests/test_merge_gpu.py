@@ -566,6 +566,20 @@ def test_compact_merge_matches_two_calls_small(ctx, tie):
     d_img, r = _decode_level(ctx, images, rng)
     for level, thr in ((1, MiB2), (6, 3000), (1, 700)):
         _compare_compact_merge(ctx, d_img, r, level, thr, tie)
+    # n is an exact precondition: a count other than the join's own
+    # (d_prefix[nfile], read back with the key statistics) is refused
+    kd, vd, prefix = lsmgpu.sst_pairs(ctx, r)
+    n = int(kd.shape[0])
+    cap = int(r.idx_desc.shape[0])
+    for bad in (n + 1, n - 1, 0):
+        kd2 = torch.empty((cap, 4), dtype=torch.int32, device=ctx.torch_device)
+        vd2 = torch.empty((cap, 4), dtype=torch.int32, device=ctx.torch_device)
+        pre2 = torch.empty((r.nfile + 1,), dtype=torch.int64, device=ctx.torch_device)
+        mg = lsmgpu.alloc_merge(ctx, max(bad, 1))
+        mg.n = bad
+        dc = torch.zeros((3,), dtype=torch.int64, device=ctx.torch_device)
+        with pytest.raises(RuntimeError, match="code -1"):
+            lsmgpu.compact_merge_into(ctx, d_img, r, kd2, vd2, pre2, mg, dc, tie=tie)
 
 
 def test_compact_merge_matches_two_calls_full_size(ctx):

@@ -203,3 +203,33 @@ def test_fuzz_record_shapes(ctx, profile):
             lg = lg[:int(rng.integers(1, len(lg)))]
         logs.append(lg)
     replay_and_check(ctx, logs)
+
+
+def test_escaped_key_lengths(ctx):
+    """Keys of 2^18 - 1 bytes and more: the segment kernel's 4-byte scratch
+    entry holds an escape value for such a key length and the compact pass
+    re-reads it from the log, the value length from the next record's start.
+    Logs long enough for the segment grid (many 16 KiB segments), the long
+    keys between ordinary records, intact and cut inside a long key, inside
+    its value length and inside the record after it."""
+    rng = np.random.default_rng(21)
+
+    def rec(k, v):
+        return struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v
+
+    small = [rec(b"k_%d_ab" % i, b"v_%d_xyz" % i) for i in range(3000)]
+    longs = [(1 << 18) - 1, 1 << 18, 300_000, (1 << 20)]  # the escape boundary, up to kv.go's cap
+    parts, cuts = [], []
+    for j, L in enumerate(longs):
+        parts += small[j * 500:(j + 1) * 500]
+        key = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        val = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        start = sum(len(p) for p in parts)
+        parts.append(rec(key, val))
+        cuts += [start + 4 + L // 2, start + 4 + L + 2, start + len(parts[-1]) + 3]
+    parts += small[2000:]
+    log = b"".join(parts)
+    logs = [log] + [log[:c] for c in cuts]
+    status, nrec = replay_and_check(ctx, logs)
+    assert status[0] == 0 and nrec[0] == 3000 + len(longs)
+    assert (status[1:] != 0).all()
