@@ -299,11 +299,12 @@ def bench_level_search(args, world, rank, local):
         tree_build_ms = (time.perf_counter() - t0) * 1e3
 
     def step():
-        lsmgpu.level_may_contain_into(ctx, sb.out, r, probes, table, may, ws=ws, stream=stream,
-                                      index=index)
-        if get:
-            lsmgpu.level_get_into(ctx, sb.out, r, probes, table, may, result, value,
-                                  tree=gtree, stream=stream)
+        if get:  # the level's search and Get in one call (lsm_level_search_get)
+            lsmgpu.level_search_get_into(ctx, sb.out, r, probes, index, table, may, result, value,
+                                         tree=gtree, ws=ws, stream=stream)
+        else:
+            lsmgpu.level_may_contain_into(ctx, sb.out, r, probes, table, may, ws=ws, stream=stream,
+                                          index=index)
 
     for _ in range(args.warmup):
         step()
@@ -368,10 +369,12 @@ def bench_level_search(args, world, rank, local):
                           "note": "built with the level (lsm_level_get_tree_build), outside the step, "
                                   "like the sparse index"} if gtree is not None else
                          "off: Seek bisects the decoded index")} if get else {}),
-        "roofline": {"bound": "hbm", "kernel": "lsm_level_may_contain_indexed (all launches; the level's "
-                               "sparse index built once, outside the step)" +
-                               (" + lsm_level_get (Seek tree built once, outside the step)"
-                                if gtree is not None else " + lsm_level_get" if get else ""),
+        "roofline": {"bound": "hbm", "kernel": ("lsm_level_search_get: lv_classify_kernel -> lv_test_kernel "
+                                                "(MayContain) -> level_get_kernel (Seek through the Seek "
+                                                "tree + value); sparse index and tree built once, "
+                                                "outside the step" if get else
+                                                "lsm_level_may_contain_indexed (all launches; the level's "
+                                                "sparse index built once, outside the step)"),
                      "kernel_ms": round(kern_ms, 5),
                      "kernel_ms_median": round(float(np.median(times)), 5),
                      "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1),

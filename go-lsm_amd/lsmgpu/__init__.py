@@ -13,7 +13,7 @@ from .codec import (  # noqa: F401
     decode_sst, decode_sst_into, wal_replay, wal_replay_into, wal_workspace,
     may_contain, may_contain_into, may_contain_workspace, level_may_contain,
     level_may_contain_into, level_may_contain_workspace, level_index, level_get, level_get_into,
-    level_get_tree, SeekTree, level0_get, level0_get_into,
+    level_get_tree, SeekTree, level0_get, level0_get_into, level_search_get, level_search_get_into,
     GET_ABSENT, GET_FOUND, GET_SEEK_FAILED, GET_VALUE_LENGTH, GET_VALUE_TOO_LONG, GET_VALUE_SHORT, Merge, alloc_merge, merge_kvs, merge_kvs_into, gather_kvs,
     prepare_sst_device, sst_pairs, sst_pairs_into, compact_merge_into, TOMBSTONE, build_sst_views_into,
     TIE_INPUT, TIE_GOHEAP, goheap_pop_order,

@@ -121,6 +121,12 @@ SIGNATURES = {
                                      c_u8p, c_u64p, ctypes.c_uint64, ctypes.c_void_p, c_u8p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p]),
+    "lsm_level_search_get": (ctypes.c_int, [ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_uint32,
+                                            c_u64p, c_u64p, ctypes.c_void_p, c_u64p, ctypes.c_void_p,
+                                            ctypes.c_void_p, c_u8p, c_u64p, ctypes.c_uint64,
+                                            ctypes.c_void_p, c_u8p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "lsm_level0_get": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u64p, c_u64p, ctypes.c_void_p,
                                       ctypes.c_uint32, c_u64p, ctypes.c_void_p, ctypes.c_void_p,
                                       c_u8p, c_u64p, ctypes.c_uint64, ctypes.c_void_p,

@@ -557,6 +557,42 @@ def level_get(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBat
     return result[:batch.n], value[:batch.n]
 
 
+def level_search_get_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                          index: torch.Tensor, table: torch.Tensor, may: torch.Tensor,
+                          result: torch.Tensor, value: torch.Tensor, tree: Optional[SeekTree] = None,
+                          ws: Optional[torch.Tensor] = None, stream=None) -> None:
+    """lsm_level_search_get: a level's whole batched Get in one call --
+    searchFromLevelWithSparseIndex then searchFromTable -- the outputs of
+    level_may_contain_into (table, may) and level_get_into (result, value)."""
+    if ws is None:
+        ws = level_may_contain_workspace(ctx, r.nfile, batch.n)
+    nf = r.nfile
+    _lib.check(ctx.lib.lsm_level_search_get(
+        ctx.handle, _ptr(d_img) if nf else None, _ptr(index) if nf else None, nf,
+        _ptr(r.d_file_off) if nf else None, _ptr(r.d_file_len) if nf else None, _ptr(r.meta) if nf else None,
+        None, _ptr(r.idx_desc) if nf else None, _ptr(r.idx_value) if nf else None,
+        _ptr(batch.keys), _ptr(batch.koff), batch.n, _ptr(table), _ptr(may), _ptr(result), _ptr(value),
+        _ptr(tree.data) if tree is not None else None, tree.max_nidx if tree is not None else 0,
+        tree.data.numel() if tree is not None else 0, _ptr(ws), ws.numel(), _stream_handle(stream)),
+        "lsm_level_search_get")
+
+
+def level_search_get(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
+                     tree: Optional[SeekTree] = None, index: Optional[torch.Tensor] = None, stream=None):
+    """-> (table, may, result, value) on the device."""
+    dev = ctx.torch_device
+    n = max(batch.n, 1)
+    table = torch.empty(n, dtype=torch.int32, device=dev)
+    may = torch.empty(n, dtype=torch.uint8, device=dev)
+    result = torch.empty(n, dtype=torch.int32, device=dev)
+    value = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    if index is None:
+        index = level_index(ctx, d_img, r, stream=stream)
+    if batch.n:
+        level_search_get_into(ctx, d_img, r, batch, index, table, may, result, value, tree=tree, stream=stream)
+    return table[:batch.n], may[:batch.n], result[:batch.n], value[:batch.n]
+
+
 def level0_get_into(ctx: Context, d_img: torch.Tensor, r: SstDecode, batch: "RecordBatch",
                     table: torch.Tensor, result: torch.Tensor, value: torch.Tensor,
                     tree: Optional[SeekTree] = None, stream=None) -> None:

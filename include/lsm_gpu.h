@@ -46,7 +46,10 @@ extern "C" {
  * v7: the builder rule on the device (lsm_segment_files) and the builder path
  * over one sorted stream as one call (lsm_build_sst_stream: rule, layout and
  * images with the fused bloom, no host round trip); lsm_level_get takes the
- * Seek tree's size; lsm_level0_get (searchFromLevel0 over every table). */
+ * Seek tree's size; lsm_level0_get (searchFromLevel0 over every table);
+ * lsm_level_search_get (a level's search and Get in one call);
+ * lsm_goheap_pop_order_host reports its phases, lsm_goheap_replays;
+ * lsm_build_flags. */
 #define LSM_ABI_VERSION 7
 #define LSM_INPUT_SLACK 32  /* readable bytes past roundup16(n) of any device input */
 
@@ -384,6 +387,22 @@ int lsm_level_get(lsm_ctx *ctx, const uint8_t *d_img, const uint64_t *d_file_off
                   uint64_t nkeys, const int32_t *d_table, const uint8_t *d_may, int32_t *d_result,
                   lsm_rec_desc *d_value, const void *d_tree, uint32_t tree_nidx, size_t tree_bytes,
                   void *stream);
+
+/* The whole batched Get of one level >= 1 in one call (ABI 7):
+ * Manager.searchFromLevelWithSparseIndex (manager.go:178-207) and
+ * searchFromTable (:209-223) -- lsm_level_may_contain_indexed's outputs
+ * (d_table, d_may) and lsm_level_get's (d_result, d_value) for the same
+ * inputs, queued on one stream.  d_index: lsm_level_index_build; the decode
+ * outputs and the tree as lsm_level_get.  Workspace:
+ * lsm_level_may_contain_workspace_bytes. */
+int lsm_level_search_get(lsm_ctx *ctx, const uint8_t *d_img, const void *d_index, uint32_t nfile,
+                         const uint64_t *d_file_off, const uint64_t *d_file_len,
+                         const lsm_sst_meta *d_meta, const uint64_t *d_rec_base,
+                         const lsm_rec_desc *d_idx_desc, const int64_t *d_idx_value,
+                         const uint8_t *d_keys, const uint64_t *d_koff, uint64_t nkeys,
+                         int32_t *d_table, uint8_t *d_may, int32_t *d_result, lsm_rec_desc *d_value,
+                         const void *d_tree, uint32_t tree_nidx, size_t tree_bytes,
+                         void *d_workspace, size_t ws_bytes, void *stream);
 
 /* Batched Manager.searchFromLevel0 (sstable/manager.go:160-176) for level 0,
  * whose tables overlap: the nfile images are the level's tables in the

@@ -61,6 +61,12 @@ def run(ctx, rng, images, probes):
         part = lsmgpu.level_get_tree(ctx, d_img, r, max_nidx=tree.max_nidx // 2)
         res1, val1 = lsmgpu.level_get(ctx, d_img, r, batch, table, may, tree=part)
         assert torch.equal(res, res1) and torch.equal(val, val1)
+    # the level's whole Get in one call (the Seek inside the filter test, the
+    # tree's top groups in LDS), with the tree, a partial tree and none
+    for tr in (tree, part if tree.max_nidx > 1 else tree, None):
+        ft, fm, fr, fv = lsmgpu.level_search_get(ctx, d_img, r, batch, tree=tr)
+        assert torch.equal(ft, table) and torch.equal(fm, may)
+        assert torch.equal(fr, res) and torch.equal(fv, val)
     torch.cuda.synchronize()
     assert torch.equal(res, res0) and torch.equal(val, val0)
     table, may = table.cpu().numpy(), may.cpu().numpy()
@@ -203,3 +209,19 @@ def test_seek_tree_shapes(ctx):
         probes += keys + [b"t%03d-%05d" % (n, 10 * x + 5) for x in range(-1, n)]
     res, _ = run(ctx, rng, images, probes)
     assert (res == ora.GET_FOUND).sum() == sum(list(range(1, 18)) + [31, 32, 33, 63, 64, 65, 70])
+
+
+def test_get_other_filter_shapes(ctx):
+    """Tables whose filters are not go-lsm's shape (m above 2^21, k above 16:
+    the level search passes the full sum256, and the fused Get reads the
+    probe's key instead of a stashed prefix) beside go-lsm-shaped ones."""
+    rng = np.random.default_rng(207)
+    images, held = [], []
+    for f in range(6):
+        keys = sorted({b"fs%06d" % (f * 1000 + int(x)) for x in rng.integers(100, 900, 80)})
+        m, k = ((3_000_000, 20) if f % 2 else (1 << 15, 5))
+        images.append(build(keys, [b"v%d" % f] * len(keys), m=m, k=k))
+        held += keys
+    probes = held[::2] + [b"fs%06d" % int(x) for x in rng.integers(0, 7000, 1500)]
+    res, _ = run(ctx, rng, images, probes)
+    assert (res[:len(held[::2])] == ora.GET_FOUND).all()
