@@ -181,6 +181,9 @@ def bench_compact(args, world, rank, local):
     from bench import HBM_PEAK_GBS
     b_ach = build_alg / (stage_ms["build"] * 1e-3) / 1e9
     chain_alg = in_bytes + float(sb.file_size.astype(np.float64).sum())
+    # HBM bytes of every kernel of one compaction (PMC, scripts/gpu_evidence.sh)
+    from bench import traffic_from_profile
+    traffic, tsrc = traffic_from_profile(f"compact:{nf_in}")
     out = {
         "metric": "GiB/s of input .sst bytes compacted (decode + merge + rebuild)",
         "value": round(total * steps / elapsed / GIB, 3),
@@ -209,7 +212,7 @@ def bench_compact(args, world, rank, local):
                      "achieved": round(chain_alg / (elapsed / steps) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(chain_alg / (elapsed / steps) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": None,
+                     "traffic": traffic, "traffic_source": tsrc,
                      "alg_bytes_per_launch": int(chain_alg),
                      "alg_bytes_def": "input image bytes read once + output image bytes written once",
                      "kernel_ms": round(elapsed * 1e3 / steps, 5),

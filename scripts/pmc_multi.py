@@ -8,11 +8,15 @@ usage: pmc_multi.py FETCH_DIR WRITE_DIR k1,k2,.. ANCHOR WORKLOAD_KEY OUT..."""
 import csv
 import glob
 import json
+import os
 import sys
 
 fetch_dir, write_dir, names, anchor, key = sys.argv[1:6]
 outs = sys.argv[6:]
 names = names.split(",")
+
+
+SKIP = int(os.environ.get("SKIP_ANCHORS", "0"))  # set-up calls before the measured ones
 
 
 def per_call(d, counter):
@@ -22,10 +26,17 @@ def per_call(d, counter):
             if r["Counter_Name"] != counter:
                 continue
             kn = r["Kernel_Name"]
+            did = int(r["Dispatch_Id"])
             if anchor in kn:
-                calls.add(r["Dispatch_Id"])
+                calls.add(did)
             if any(n in kn for n in names):
-                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+                vals[did] = vals.get(did, 0.0) + float(r["Counter_Value"])
+    # SKIP_ANCHORS = k: the first k anchor dispatches and everything before
+    # the k-th are set-up (e.g. the compaction bench's input build and decode)
+    if SKIP:
+        first = sorted(calls)[SKIP]
+        calls = {c for c in calls if c >= first}
+        vals = {k: v for k, v in vals.items() if k >= first}
     return sum(vals.values()) / max(1, len(calls)), len(calls)
 
 
