@@ -1773,7 +1773,9 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         if (e0 != 0xFFFFFFFFu) { c0 = ca; x0 = xa; st0 = sa; }
         if (e1 != 0xFFFFFFFFu) { c1 = cb; x1 = xb; st1 = sb; }
     }
-    // 2. + 3. per phase: stitch from the entry, then write the accepted chains
+    // 2. per phase: stitch from the entry (each lane's accepted chain)
+    uint32_t wpre[2] = {0, 0}, wentry[2] = {0, 0}, wcnt[2] = {0, 0};
+#pragma unroll
     for (uint32_t ph = 0; ph < 2; ph++) {
         const uint64_t q = q0 + ph;
         const uint32_t gp = ph ? g1 : g;
@@ -1893,18 +1895,34 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
             }
         }
         uint32_t tot;
-        const uint32_t pre = wave_excl_scan(acc_cnt, &tot);
-        if (acc_cnt) {
-            uint32_t *dst = reinterpret_cast<uint32_t *>(a.scratch + q * kWalSegSlots) + pre;
-            uint32_t p = acc_entry;
-            for (uint32_t i = 0; i < acc_cnt; i++) {
-                uint32_t kl = 0, vl = 0;
-                L.record(p, kl, vl);
-                dst[i] = (p - start) | (kl < kWalKlEsc ? kl : kWalKlEsc) << kWalPosBits;
-                p += 8 + kl + vl;
+        wpre[ph] = wave_excl_scan(acc_cnt, &tot);
+        wentry[ph] = acc_entry;
+        wcnt[ph] = acc_cnt;
+        if (lane == 0) a.seg[q] = WalSeg{gp, e, total, status};
+    }
+    // 3. both phases' accepted chains walked together, a 4-byte scratch entry
+    //    per record: each step reads both key lengths in one LDS round trip,
+    //    then both value lengths (walked one phase after the other they were
+    //    two serial chains: 1,117 -> 1,167 GiB/s, A/B)
+    {
+        uint32_t *dst0 = reinterpret_cast<uint32_t *>(a.scratch + q0 * kWalSegSlots) + wpre[0];
+        uint32_t *dst1 = reinterpret_cast<uint32_t *>(a.scratch + (q0 + 1) * kWalSegSlots) + wpre[1];
+        uint32_t pa = wentry[0], pb = wentry[1];
+        const uint32_t n = wcnt[0] > wcnt[1] ? wcnt[0] : wcnt[1];
+        for (uint32_t i = 0; i < n; i++) {
+            const bool ra = i < wcnt[0], rb = i < wcnt[1];
+            uint32_t ka, kb, va, vb;
+            L.rd32x2(ra ? pa : start, rb ? pb : start, ka, kb);
+            L.rd32x2(ra ? pa + 4 + ka : start, rb ? pb + 4 + kb : start, va, vb);
+            if (ra) {
+                dst0[i] = (pa - start) | (ka < kWalKlEsc ? ka : kWalKlEsc) << kWalPosBits;
+                pa += 8 + ka + va;
+            }
+            if (rb) {
+                dst1[i] = (pb - start) | (kb < kWalKlEsc ? kb : kWalKlEsc) << kWalPosBits;
+                pb += 8 + kb + vb;
             }
         }
-        if (lane == 0) a.seg[q] = WalSeg{gp, e, total, status};
     }
 }
 
