@@ -1584,9 +1584,15 @@ struct WalLog {
     __device__ __forceinline__ void chase2(uint32_t pa, uint32_t pb, uint32_t end, uint32_t park,
                                            uint32_t &ca, uint32_t &xa, int32_t &sa, uint32_t &cb,
                                            uint32_t &xb, int32_t &sb) const {
+        chase2(pa, pb, end, end, park, ca, xa, sa, cb, xb, sb);
+    }
+    // the same with an end per chain
+    __device__ __forceinline__ void chase2(uint32_t pa, uint32_t pb, uint32_t enda, uint32_t endb,
+                                           uint32_t park, uint32_t &ca, uint32_t &xa, int32_t &sa,
+                                           uint32_t &cb, uint32_t &xb, int32_t &sb) const {
         ca = cb = 0;
         sa = sb = LSM_OK;
-        bool ra = pa < end && pa < len, rb = pb < end && pb < len;
+        bool ra = pa < enda && pa < len, rb = pb < endb && pb < len;
         while (ra || rb) {
             // kv.go:77-115 order, as record(): length prefix, key, value length, value
             const uint32_t rma = len - pa, rmb = len - pb;
@@ -1611,7 +1617,7 @@ struct WalLog {
                 } else {
                     ca++;
                     pa += 8 + ka + va;
-                    ra = pa < end && pa < len;
+                    ra = pa < enda && pa < len;
                 }
             }
             if (rb) {
@@ -1628,7 +1634,7 @@ struct WalLog {
                 } else {
                     cb++;
                     pb += 8 + kb + vb;
-                    rb = pb < end && pb < len;
+                    rb = pb < endb && pb < len;
                 }
             }
         }
@@ -1773,6 +1779,24 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         if (e0 != 0xFFFFFFFFu) { c0 = ca; x0 = xa; st0 = sa; }
         if (e1 != 0xFFFFFFFFu) { c1 = cb; x1 = xb; st1 = sb; }
     }
+    // The share holding each phase's entry is chased exactly from the entry
+    // (the fast stitch below), both phases together.
+    uint32_t kc[2], cc[2], xc[2];
+    int32_t sc[2];
+    {
+        const uint32_t live1 = s > 0 && g1 < E;  // phase 1 exists (g < E always)
+        kc[0] = (g - start) / W;
+        kc[1] = live1 ? (g1 - start) / W : 0;
+        const uint32_t se0 = uni(__builtin_amdgcn_readlane(se, kc[0]));
+        const uint32_t se1 = uni(__builtin_amdgcn_readlane(se, kc[1]));
+        L.chase2(g, live1 ? g1 : se1, se0, se1, start, cc[0], xc[0], sc[0], cc[1], xc[1], sc[1]);
+#pragma unroll
+        for (uint32_t i = 0; i < 2; i++) {
+            cc[i] = uni(cc[i]);
+            xc[i] = uni(xc[i]);
+            sc[i] = (int32_t)uni((uint32_t)sc[i]);
+        }
+    }
     // 2. per phase: stitch from the entry (each lane's accepted chain)
     uint32_t wpre[2] = {0, 0}, wentry[2] = {0, 0}, wcnt[2] = {0, 0};
 #pragma unroll
@@ -1798,15 +1822,10 @@ __global__ __launch_bounds__(64) void wal_seg_lanes_kernel(WalArgs a) {
         // the serial stitch below.
         bool fast = false;
         {
-            const uint32_t k = (gp - start) / W;
+            const uint32_t k = kc[ph];
             const uint32_t last = (E - 1 - start) / W < kWave - 1 ? (E - 1 - start) / W : kWave - 1;
-            const uint32_t sek = uni(__builtin_amdgcn_readlane(se, k));
-            uint32_t ck, xk;
-            int32_t stk;
-            L.chase(gp, sek, ck, xk, stk);
-            ck = uni(ck);
-            xk = uni(xk);
-            stk = (int32_t)uni((uint32_t)stk);
+            const uint32_t ck = cc[ph], xk = xc[ph];
+            const int32_t stk = sc[ph];
             auto match = [&](uint32_t x) -> uint32_t {
                 return (e0 != 0xFFFFFFFFu && x == e0) ? 0u : (e1 != 0xFFFFFFFFu && x == e1) ? 1u : 2u;
             };
