@@ -124,3 +124,27 @@ def test_launcher_gpus2_deals_sst_files_exactly():
     assert j["records_per_rank"] == [2 * 15888 + last, 2 * 15888]   # files 0, 2, 4 | 1, 3
     j, _ = _bench_dry("--config", "sst", "--gpus", "3", "--blocks", "2000")
     assert j["blocks_per_rank"] == [2, 2, 1] and sum(j["records_per_rank"]) == 66_000
+
+
+def test_sst_deal_rule_rederives_each_ranks_files():
+    """At N > 1 each rank's step runs the builder rule on the device over its
+    own concatenation of dealt files (bench_sst.py).  That re-derives exactly
+    the dealt files: every dealt file but the global last is full, the rule
+    restarts at each file start, and the partial last file ends its rank's
+    stream.  Checked here with the oracle's rule (ora_segment_files, the
+    restatement of builder.go:34-42 the device rule is tested against)."""
+    import argparse
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "go-lsm_amd"), os.path.join(ROOT, "oracle")]
+    import bench_sst
+    import lsmgpu
+    import pyoracle as ora
+    args = argparse.Namespace(blocks=2000)
+    for world in (2, 3):
+        seen = 0
+        for rank in range(world):
+            (keys, koff, vals, voff), starts, mine, nf, _ = bench_sst.sst_deal(args, world, rank)
+            again = ora.segment_files(koff, voff, lsmgpu.MAX_SSTABLE_SIZE)
+            assert np.array_equal(again.astype(np.int64), starts.astype(np.int64)), (world, rank)
+            assert len(starts) - 1 == len(mine)
+            seen += len(mine)
+        assert seen == nf
