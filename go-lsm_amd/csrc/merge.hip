@@ -371,8 +371,9 @@ template <class K>
 __global__ __launch_bounds__(kMergeThreads) void merge_extract_split_kernel(MergeIn m, SortGroup g,
                                                                             uint32_t s, uint32_t e,
                                                                             K *run_keys, K *oth_keys,
-                                                                            uint32_t *oth_idx) {
+                                                                            uint32_t *oth_idx, uint32_t *zero) {
     const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x;
+    if (j == 0 && zero) *zero = 0;  // the k-way path's run-start count
     if (j >= m.n) return;
     if (j >= s && j < e) {
         run_keys[j - s] = packed_key<K>(m, g, j);
@@ -1732,21 +1733,163 @@ extern "C" size_t lsm_merge_kvs_workspace_bytes(uint64_t n) {
     return merge_ws_layout(nullptr, (uint32_t)n).total;
 }
 
+namespace lsm {
+namespace {
+
+// The others as a k-way merge.  The pairs outside the longest run are, in
+// input order, a few sorted runs when the input is a compaction's files (each
+// file is sorted: level 0's flushes and the pieces of level 1 around the run),
+// and the key statistics count the input's descents exactly, which bounds the
+// runs.  With at most kKwayMaxRuns runs the others are ranked instead of
+// radix-sorted: a pair's place is its place in its own run plus, in every
+// other run, the pairs before it -- those <= its key in an earlier run, < in a
+// later one (the stable order: equal keys in input order, as the radix sort
+// leaves them).  merge_kway_runs_kernel lists the run starts (a descent of
+// the packed keys, or the junction of the pairs before the long run with those
+// after it); merge_kway_rank_kernel sorts the list, stages every kKwaySample-th
+// key of each run in LDS, and per pair searches all runs side by side: first
+// in the samples, then in the one sample interval in global memory.
+constexpr uint32_t kKwayMaxRuns = 16;
+constexpr uint32_t kKwayThreads = 1024;
+constexpr uint32_t kKwaySamples = 4096;  // LDS samples per workgroup, all runs
+
+template <class K>
+__global__ __launch_bounds__(kMergeThreads) void merge_kway_runs_kernel(const K *ok0, uint32_t no, uint32_t junction,
+                                                                        uint32_t *list) {
+    // list[0] (the count) was zeroed by merge_extract_split_kernel
+    const uint32_t j = blockIdx.x * kMergeThreads + threadIdx.x + 1;
+    if (j < no && (j == junction || ok0[j] < ok0[j - 1])) {
+        const uint32_t q = atomicAdd(&list[0], 1u);
+        if (q < 2 * kKwayMaxRuns) list[1 + q] = j;
+    }
+}
+
+template <class K>
+__global__ __launch_bounds__(kKwayThreads) void merge_kway_rank_kernel(const K *ok0, const uint32_t *oi0, uint32_t no,
+                                                                       const uint32_t *list, K *ok1, uint32_t *oi1) {
+    __shared__ uint32_t sb[kKwayMaxRuns + 1];  // run b = [sb[b], sb[b + 1])
+    __shared__ uint32_t sbase[kKwayMaxRuns + 1];  // its first sample
+    __shared__ uint32_t s_R, s_stride;
+    __shared__ K smp[kKwaySamples + kKwayMaxRuns];
+    if (threadIdx.x == 0) {
+        // the host's bound admits at most kKwayMaxRuns - 1 starts past 0
+        uint32_t p[kKwayMaxRuns];
+        const uint32_t c = list[0], n = c < kKwayMaxRuns - 1 ? c : kKwayMaxRuns - 1;
+        for (uint32_t a = 0; a < n; a++) {  // insertion sort of the starts
+            const uint32_t x = list[1 + a];
+            uint32_t b = a;
+            while (b > 0 && p[b - 1] > x) {
+                p[b] = p[b - 1];
+                b--;
+            }
+            p[b] = x;
+        }
+        sb[0] = 0;
+        for (uint32_t a = 0; a < n; a++) sb[a + 1] = p[a];
+        sb[n + 1] = no;
+        s_R = n + 1;
+        // every stride-th key of a run, so that all runs' samples fit
+        const uint32_t st = (no + kKwaySamples - 1) / kKwaySamples;
+        s_stride = st < 1 ? 1 : st;
+        uint32_t o = 0;
+        for (uint32_t b = 0; b <= n; b++) {
+            sbase[b] = o;
+            o += (sb[b + 1] - sb[b] + s_stride - 1) / s_stride;
+        }
+        sbase[n + 1] = o;
+    }
+    __syncthreads();
+    const uint32_t R = s_R, stride = s_stride;
+    for (uint32_t b = 0; b < R; b++) {
+        const uint32_t cnt = sbase[b + 1] - sbase[b];
+        for (uint32_t t = threadIdx.x; t < cnt; t += kKwayThreads) smp[sbase[b] + t] = ok0[sb[b] + t * stride];
+    }
+    __syncthreads();
+    const uint32_t j = blockIdx.x * kKwayThreads + threadIdx.x;
+    if (j >= no) return;
+    const K k = ok0[j];
+    uint32_t a = 0;
+    while (a + 1 < R && sb[a + 1] <= j) a++;
+    // the bound in run b: the first position whose key is > k (earlier runs)
+    // or >= k (later runs); samples first, then the one interval between two
+    uint32_t lo[kKwayMaxRuns], hi[kKwayMaxRuns];
+#pragma unroll
+    for (uint32_t b = 0; b < kKwayMaxRuns; b++) {
+        uint32_t l = 0, h = 0;
+        if (b < R && b != a) {  // samples: the first sample index t with smp > / >= k
+            l = sbase[b];
+            h = sbase[b + 1];
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                const K x = smp[mid];
+                if (b < a ? x <= k : x < k) l = mid + 1;
+                else h = mid;
+            }
+            // positions before sample t are all "before"; the bound is in
+            // (position of sample t - 1, position of sample t]
+            const uint32_t t = l - sbase[b];
+            const uint32_t end = sb[b + 1];
+            lo[b] = t == 0 ? sb[b] : sb[b] + (t - 1) * stride + 1;
+            hi[b] = sb[b] + t * stride < end ? sb[b] + t * stride : end;
+        } else {
+            lo[b] = hi[b] = 0;
+        }
+    }
+    for (;;) {
+        bool any = false;
+        K x[kKwayMaxRuns];
+#pragma unroll
+        for (uint32_t b = 0; b < kKwayMaxRuns; b++)
+            if (lo[b] < hi[b]) x[b] = ok0[(lo[b] + hi[b]) >> 1];
+#pragma unroll
+        for (uint32_t b = 0; b < kKwayMaxRuns; b++) {
+            if (lo[b] < hi[b]) {
+                const uint32_t mid = (lo[b] + hi[b]) >> 1;
+                if (b < a ? x[b] <= k : x[b] < k) lo[b] = mid + 1;
+                else hi[b] = mid;
+                any = true;
+            }
+        }
+        if (!any) break;
+    }
+    uint32_t pos = j - sb[a];
+#pragma unroll
+    for (uint32_t b = 0; b < kKwayMaxRuns; b++)
+        if (b < R && b != a) pos += lo[b] - sb[b];
+    ok1[pos] = k;
+    oi1[pos] = oi0[j];
+}
+
+}  // namespace
+}  // namespace lsm
+
 // The merge path (merge_rank_*): the pairs outside the run [rs, re) are
-// packed and radix-sorted (with their input index), the run's keys packed,
-// and each pair's sorted position written to w.perm[0].  Workspace: the
-// run's keys in w.keys[0]; the others' keys (two buffers) in w.keys[1] and
-// their indices in w.perm[1] (no <= n / 2).
+// packed and sorted (with their input index: ranked as a k-way merge when
+// they are at most kKwayMaxRuns sorted runs, radix-sorted otherwise), the
+// run's keys packed, and each pair's sorted position written to w.perm[0].
+// Workspace: the run's keys in w.keys[0]; the others' keys (two buffers) in
+// w.keys[1] and their indices in w.perm[1] (no <= n / 2).
 template <class K>
 static int merge_path(const MergeWs &w, const MergeIn &m, const SortGroup &g, uint32_t bits,
-                      uint32_t rs, uint32_t re, uint32_t no, hipStream_t s) {
+                      uint32_t rs, uint32_t re, uint32_t no, uint64_t descents, hipStream_t s) {
     const uint32_t N = m.n, nrun = re - rs;
     K *run_keys = reinterpret_cast<K *>(w.keys[0]);
     K *ok0 = reinterpret_cast<K *>(w.keys[1]), *ok1 = ok0 + no;
     uint32_t *oi0 = w.perm[1], *oi1 = w.perm[1] + no;
+    const bool kway = no && descents + 2 <= kKwayMaxRuns && w.sort_bytes >= 4 * (2 * kKwayMaxRuns + 1);
+    uint32_t *list = kway ? static_cast<uint32_t *>(w.sort_tmp) : nullptr;
     hipLaunchKernelGGL(merge_extract_split_kernel<K>, dim3(grid_for(N)), dim3(kMergeThreads), 0, s, m,
-                       g, rs, re, run_keys, ok0, oi0);
-    if (no) {
+                       g, rs, re, run_keys, ok0, oi0, list);
+    if (kway) {
+        // the others' runs: the input's descents outside [rs, re), and the
+        // junction of the pairs before the run with those after it
+        hipLaunchKernelGGL(merge_kway_runs_kernel<K>, dim3(grid_for(no)), dim3(kMergeThreads), 0, s, ok0, no,
+                           rs, list);
+        hipLaunchKernelGGL(merge_kway_rank_kernel<K>, dim3((no + kKwayThreads - 1) / kKwayThreads),
+                           dim3(kKwayThreads), 0, s, ok0, oi0, no, list, ok1, oi1);
+        hipLaunchKernelGGL(merge_rank_others_kernel<K>, dim3(grid_for(no)), dim3(kMergeThreads), 0, s,
+                           run_keys, nrun, rs, ok1, oi1, no, w.perm[0]);
+    } else if (no) {
         size_t tb = w.sort_bytes;
         const hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, tb, ok0, ok1, oi0, oi1, no, 0, bits, s);
         if (e != hipSuccess) return -(1000 + (int)e);
@@ -1802,6 +1945,7 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
     uint64_t st[kStatCore];
     for (uint32_t t = 0; t < kStatCore; t++) st[t] = part[t];
     uint64_t run_s = 0, run_e = 0, cur_s = 0;  // the longest run found, the open one
+    uint64_t descents = 0;                     // of the whole input (exact)
     auto run = [&](uint64_t a, uint64_t b) {
         if (b - a > run_e - run_s) { run_s = a; run_e = b; }
     };
@@ -1816,6 +1960,7 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
             }
         }
         const uint64_t *r = q + kStatCore;  // first, last descent, count, inner run
+        descents += r[2];
         if (r[2] == 0) continue;
         run(cur_s, r[0]);
         if (r[4] > r[3]) run(r[3], r[4]);
@@ -1868,8 +2013,8 @@ static int merge_kvs(lsm_ctx *ctx, const uint8_t *d_bytes, const lsm_rec_desc *d
             g.mask[t] = fields[g.nf - 1 - t].second;
         }
         const int rc = all_bits <= 32
-                           ? merge_path<uint32_t>(w, m, g, all_bits, rs, re, no, s)
-                           : merge_path<uint64_t>(w, m, g, all_bits, rs, re, no, s);
+                           ? merge_path<uint32_t>(w, m, g, all_bits, rs, re, no, descents, s)
+                           : merge_path<uint64_t>(w, m, g, all_bits, rs, re, no, descents, s);
         if (rc) return rc;
         fields.clear();
         have_perm = true;  // w.perm[0]
