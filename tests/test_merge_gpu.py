@@ -421,6 +421,29 @@ def test_merge_path_one_long_run(ctx, tie, shape):
 
 
 @pytest.mark.parametrize("tie", TIES)
+@pytest.mark.parametrize("nfiles", [1, 2, 7, 13, 14, 15, 16, 40])
+def test_merge_path_kway_runs(ctx, tie, nfiles):
+    """The merge path's others as a k-way merge of their sorted runs (at most
+    16, bounded by the input's descent count; more take the radix sort):
+    nfiles sorted, overlapping update files before and after one long run,
+    keys repeated across the files and with the run (the stable order: the
+    earlier file's pair first), tombstones, and file counts on both sides of
+    the bound."""
+    rng = random.Random(977 + nfiles)
+    base = sorted({b"k%06d" % rng.randint(0, 999999) for _ in range(5000)})
+    runp = [(k, b"r" * rng.randint(0, 20)) for k in base]
+    files = []
+    for f in range(nfiles):
+        ks = sorted({rng.choice(base) if rng.random() < 0.5 else b"k%06d" % rng.randint(0, 999999)
+                     for _ in range(rng.randint(1, 120))})
+        files.append([(k, TOMB if rng.random() < 0.1 else b"f%d" % f) for k in ks])
+    cut = rng.randint(0, nfiles)
+    pairs = [p for fl in files[:cut] for p in fl] + runp + [p for fl in files[cut:] for p in fl]
+    for level, thr in ((1, MiB2), (6, 3000)):
+        run(ctx, pairs, level, thr, seed=nfiles, tie=tie)
+
+
+@pytest.mark.parametrize("tie", TIES)
 def test_async_merge_and_device_count_gather(ctx, tie):
     """lsm_merge_kvs_async (counts left on the device) + lsm_gather_kvs_dev
     (the gather on that device count, launched on a bound) equal the
