@@ -1749,7 +1749,7 @@ namespace {
 // after it); merge_kway_rank_kernel sorts the list, stages every kKwaySample-th
 // key of each run in LDS, and per pair searches all runs side by side: first
 // in the samples, then in the one sample interval in global memory.
-constexpr uint32_t kKwayMaxRuns = 16;
+constexpr uint32_t kKwayMaxRuns = 12;
 constexpr uint32_t kKwayThreads = 1024;
 constexpr uint32_t kKwaySamples = 4096;  // LDS samples per workgroup, all runs
 

@@ -421,10 +421,10 @@ def test_merge_path_one_long_run(ctx, tie, shape):
 
 
 @pytest.mark.parametrize("tie", TIES)
-@pytest.mark.parametrize("nfiles", [1, 2, 7, 13, 14, 15, 16, 40])
+@pytest.mark.parametrize("nfiles", [1, 2, 7, 9, 10, 11, 12, 16, 40])
 def test_merge_path_kway_runs(ctx, tie, nfiles):
     """The merge path's others as a k-way merge of their sorted runs (at most
-    16, bounded by the input's descent count; more take the radix sort):
+    12, bounded by the input's descent count; more take the radix sort):
     nfiles sorted, overlapping update files before and after one long run,
     keys repeated across the files and with the run (the stable order: the
     earlier file's pair first), tombstones, and file counts on both sides of
